@@ -1,0 +1,122 @@
+"""Headline benchmark: output tokens/s (node) + p50 latency for batched generation.
+
+Config (BASELINE.json): Llama-2-7B with tensor parallelism TP = N (one process per GPU, RCCL over
+xGMI; TP=8 at N=8) - or ``--model gpt2-xl`` for the GPT-2-XL TP=1 configuration. Random-init
+weights of the exact architecture and synthetic prompt token ids (no network, no checkpoints).
+
+A "step" = one complete batched generation through the serving engine: ``batch`` synthetic
+prompts of ``--prompt-len`` tokens, prefill + ``--gen-len`` decode tokens each (continuous-
+batching scheduler, paged KV cache, HIP-graph decode, on-device sampling with the reference's
+default temperature=1.0 / top_p=0.95 / top_k=50). Weak scaling: the global batch is
+``--batch-per-gpu * N``. ``value`` = total generated tokens / wall time over all ranks (max).
+
+Launch: ``python bench.py`` (N=1) or ``torchrun --nproc-per-node N bench.py --gpus N``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="llama2-7b")
+    ap.add_argument("--batch-per-gpu", type=int, default=64)
+    ap.add_argument("--prompt-len", type=int, default=128)
+    ap.add_argument("--gen-len", type=int, default=128)
+    ap.add_argument("--fp8", action="store_true")
+    ap.add_argument("--greedy", action="store_true")
+    ap.add_argument("--no-graphs", action="store_true")
+    args = ap.parse_args()
+
+    from llmss_amd.engine import LLMEngine, SamplingParams, build_model
+    from llmss_amd.parallel.dist import initialize_distributed
+
+    tp, rank, world = initialize_distributed()
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    dev = torch.device("cuda", torch.cuda.current_device())
+    batch = args.batch_per_gpu * world
+    model = build_model(args.model, tp, "bf16", dev, fp8=args.fp8, random_init=True)
+    max_len = min(model.cfg.max_position_embeddings, max(256, args.prompt_len + args.gen_len))
+    eng = LLMEngine(model, max_num_seqs=batch, max_batched_tokens=max(8192, batch * args.prompt_len),
+                    block_size=16, max_model_len=max_len, use_graphs=not args.no_graphs)
+    rng = np.random.default_rng(1234)
+    V = model.cfg.vocab_size
+
+    def prompts():
+        return [rng.integers(0, V, args.prompt_len).tolist() for _ in range(batch)]
+
+    def params():
+        return SamplingParams(max_new_tokens=args.gen_len, is_greedy=args.greedy, temperature=1.0, top_p=0.95,
+                              top_k=50, ignore_eos=True, seed=7)
+
+    def one_step():
+        rids = [eng.add_request(p, params()) for p in prompts()]
+        n = 0
+        while eng.has_unfinished():
+            n += len(eng.step())
+        reqs = eng.pop_finished()
+        return n, [r.metrics() for r in reqs]
+
+    for _ in range(args.warmup):
+        one_step()
+    tp.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    total, mets = 0, []
+    for _ in range(args.steps):
+        n, m = one_step()
+        total += n
+        mets.extend(m)
+    torch.cuda.synchronize()
+    tp.barrier()
+    el = time.perf_counter() - t0
+    if tp.is_real:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+    tpot = np.nanmedian([m["tpot_s"] for m in mets]) * 1e3
+    ttft = np.nanmedian([m["ttft_s"] for m in mets]) * 1e3
+    e2e = np.nanmedian([m["e2e_s"] for m in mets]) * 1e3
+    value = total / el
+    if rank == 0:
+        print(json.dumps({
+            "metric": "output_tokens_per_sec",
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp8-weights/bf16" if args.fp8 else "bf16",
+            "data": "synthetic prompts, random-init weights",
+            "p50_tpot_ms": round(float(tpot), 3),
+            "p50_ttft_ms": round(float(ttft), 3),
+            "p50_request_latency_ms": round(float(e2e), 3),
+            "config": {"model": args.model, "global_batch": batch, "seq_len": args.prompt_len + args.gen_len,
+                       "prompt_len": args.prompt_len, "gen_len": args.gen_len, "parallelism": f"tp{world}",
+                       "sampling": "greedy" if args.greedy else "temperature=1.0,top_p=0.95,top_k=50",
+                       "engine_stats": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()}},
+        }))
+    if tp.is_real:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,81 @@
+// Python bindings for the gfx950 kernels (module llmss_amd._C).
+//
+// Pointers and the HIP stream are passed as integers: the Python layer (llmss_amd/ops/hip.py)
+// owns tensor validation (dtype, contiguity, shapes vs. the grid each kernel assumes) so that a
+// malformed call raises in Python instead of faulting the GPU. No torch headers are needed, which
+// keeps the build a plain hipcc compile (no hipify step, no CUDA-compat layer).
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <stdint.h>
+
+namespace py = pybind11;
+
+void launch_add_norm(const void* x, int64_t x_stride, const void* res_in, void* res_out, const void* w, const void* b,
+                     void* y, int64_t y_stride, int T, int H, float eps, bool rms, hipStream_t st);
+void launch_embed(const void* ids, const void* pos, const void* wte, const void* wpe, void* out, int T, int H,
+                  int vocab, hipStream_t st);
+void launch_rope_cache(void* qkv, int64_t row_stride, const void* pos, const void* cos_t, const void* sin_t, void* kc,
+                       void* vc, const void* slot, int T, int nh, int nkv, int D, int rot, int block_size, int k_off,
+                       int v_off, int style, bool do_rope, hipStream_t st);
+void launch_attn_decode(const void* q, int64_t q_stride, const void* kc, const void* vc, const void* block_tables,
+                        int bt_stride, const void* ctx_lens, void* out, int64_t out_stride, void* part_o,
+                        void* part_ml, int B, int nh, int nkv, int D, int block_size, int nsplit, int part_size,
+                        float scale, hipStream_t st);
+void launch_attn_prefill(const void* qkv, int64_t row_stride, const void* cu_seqlens, void* out, int64_t out_stride,
+                         int B, int max_seqlen, int nh, int nkv, int D, int k_off, int v_off, float scale,
+                         hipStream_t st);
+void launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_fp8, const void* w_scale,
+                 const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace,
+                 int64_t ws_bytes, hipStream_t st);
+int gemm_skinny_splitk(int M, int N, int K);
+void launch_sample(const void* logits, int64_t ld, bool fp32_logits, int B, int V, const void* temperature,
+                   const void* top_k, const void* top_p, const void* seeds, void* out, void* out2, hipStream_t st);
+void launch_quant_fp8_rows(const void* w, void* q, void* scale, int64_t N, int64_t K, hipStream_t st);
+void launch_allreduce_p2p(void* const* bufs, int world, int rank, void* out, int64_t n_elems, void* flags,
+                          int epoch, hipStream_t st);
+
+void register_runtime(py::module_& m);  // host-side C++ runtime (runtime.cpp)
+
+#define P(x) reinterpret_cast<void*>(static_cast<uintptr_t>(x))
+#define CP(x) reinterpret_cast<const void*>(static_cast<uintptr_t>(x))
+#define S(x) reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(x))
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "llmss_amd gfx950 HIP kernels + native runtime";
+  m.def("add_norm", [](uintptr_t x, int64_t xs, uintptr_t ri, uintptr_t ro, uintptr_t w, uintptr_t b, uintptr_t y,
+                       int64_t ys, int T, int H, float eps, bool rms, uintptr_t st) {
+    launch_add_norm(CP(x), xs, CP(ri), P(ro), CP(w), CP(b), P(y), ys, T, H, eps, rms, S(st));
+  });
+  m.def("embed", [](uintptr_t ids, uintptr_t pos, uintptr_t wte, uintptr_t wpe, uintptr_t out, int T, int H, int V,
+                    uintptr_t st) { launch_embed(CP(ids), CP(pos), CP(wte), CP(wpe), P(out), T, H, V, S(st)); });
+  m.def("rope_cache", [](uintptr_t qkv, int64_t rs, uintptr_t pos, uintptr_t cos_t, uintptr_t sin_t, uintptr_t kc,
+                         uintptr_t vc, uintptr_t slot, int T, int nh, int nkv, int D, int rot, int bs, int k_off,
+                         int v_off, int style, bool do_rope, uintptr_t st) {
+    launch_rope_cache(P(qkv), rs, CP(pos), CP(cos_t), CP(sin_t), P(kc), P(vc), CP(slot), T, nh, nkv, D, rot, bs, k_off,
+                      v_off, style, do_rope, S(st));
+  });
+  m.def("attn_decode", [](uintptr_t q, int64_t qs, uintptr_t kc, uintptr_t vc, uintptr_t bt, int bts, uintptr_t cl,
+                          uintptr_t out, int64_t os, uintptr_t po, uintptr_t pml, int B, int nh, int nkv, int D, int bs,
+                          int nsplit, int psize, float scale, uintptr_t st) {
+    launch_attn_decode(CP(q), qs, CP(kc), CP(vc), CP(bt), bts, CP(cl), P(out), os, P(po), P(pml), B, nh, nkv, D, bs,
+                       nsplit, psize, scale, S(st));
+  });
+  m.def("attn_prefill", [](uintptr_t qkv, int64_t rs, uintptr_t cu, uintptr_t out, int64_t os, int B, int maxlen,
+                           int nh, int nkv, int D, int k_off, int v_off, float scale, uintptr_t st) {
+    launch_attn_prefill(CP(qkv), rs, CP(cu), P(out), os, B, maxlen, nh, nkv, D, k_off, v_off, scale, S(st));
+  });
+  m.def("gemm", [](uintptr_t x, int64_t ldx, uintptr_t w, int64_t ldw, bool fp8, uintptr_t ws, uintptr_t bias,
+                   uintptr_t y, int64_t ldy, int M, int N, int K, int act, bool glu, uintptr_t work, int64_t wbytes,
+                   uintptr_t st) {
+    launch_gemm(CP(x), ldx, CP(w), ldw, fp8, CP(ws), CP(bias), P(y), ldy, M, N, K, act, glu, P(work), wbytes, S(st));
+  });
+  m.def("gemm_skinny_splitk", &gemm_skinny_splitk);
+  m.def("sample", [](uintptr_t logits, int64_t ld, bool fp32, int B, int V, uintptr_t temp, uintptr_t topk,
+                     uintptr_t topp, uintptr_t seeds, uintptr_t out, uintptr_t out2, uintptr_t st) {
+    launch_sample(CP(logits), ld, fp32, B, V, CP(temp), CP(topk), CP(topp), CP(seeds), P(out), P(out2), S(st));
+  });
+  m.def("quant_fp8_rows", [](uintptr_t w, uintptr_t q, uintptr_t scale, int64_t N, int64_t K, uintptr_t st) {
+    launch_quant_fp8_rows(CP(w), P(q), P(scale), N, K, S(st));
+  });
+  register_runtime(m);
+}

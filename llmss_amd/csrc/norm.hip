@@ -1,0 +1,134 @@
+// Fused residual-add + LayerNorm / RMSNorm (reference applies
+// nn.LayerNorm after a separate residual add, gptj_modeling.py:295-310,
+// gpt_bigcode_modeling.py:366-407; the optional external dropout_add_ln_fwd kernel at
+// utils/layers.py:217-253 is the same fusion, which the reference never calls).
+//
+//   r = x (+ residual)            -> stored to residual_out (bf16) when a residual is given
+//   y = norm(r) * w (+ b)         -> bf16
+//
+// One workgroup per row; every lane owns MAXC 16-byte chunks of the row in registers, so the
+// row is read from HBM once and the two-pass (mean, then centred variance) statistics are
+// computed from registers. Memory bound: 16-B vector loads/stores only (guide G13).
+#include "common.h"
+#include <stdexcept>
+#include <string>
+
+template <int MAXC, bool RMS, bool HAS_RES, bool HAS_BIAS>
+__global__ __launch_bounds__(256) void add_norm_kernel(const bf16_t* __restrict__ x, int64_t x_stride,
+                                                       const bf16_t* res_in, bf16_t* res_out,
+                                                       const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
+                                                       bf16_t* __restrict__ y, int64_t y_stride, int H, float eps) {
+  __shared__ float red[16];
+  const int row = blockIdx.x;
+  const int nchunk = H >> 3;
+  float v[MAXC][8];
+  const bf16_t* xr = x + row * x_stride;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = threadIdx.x + c * blockDim.x;
+    if (ch < nchunk) {
+      u16x8 a = *reinterpret_cast<const u16x8*>(xr + ch * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = bf2f(a[j]);
+      if constexpr (HAS_RES) {
+        u16x8 r = *reinterpret_cast<const u16x8*>(res_in + (int64_t)row * H + ch * 8);
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          v[c][j] += bf2f(r[j]);
+          o[j] = f2bf(v[c][j]);
+          v[c][j] = bf2f(o[j]);  // normalise exactly what is stored in the residual stream
+        }
+        *reinterpret_cast<u16x8*>(res_out + (int64_t)row * H + ch * 8) = o;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+    }
+  }
+  float mean = 0.f;
+  if constexpr (!RMS) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[c][j];
+    mean = block_sum(s, red) / H;
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = threadIdx.x + c * blockDim.x;
+    if (ch < nchunk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float d = v[c][j] - mean;
+        ss += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(block_sum(ss, red) / H + eps);
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = threadIdx.x + c * blockDim.x;
+    if (ch < nchunk) {
+      u16x8 wv = *reinterpret_cast<const u16x8*>(w + ch * 8);
+      u16x8 bv;
+      if constexpr (HAS_BIAS) bv = *reinterpret_cast<const u16x8*>(b + ch * 8);
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = (v[c][j] - mean) * rstd * bf2f(wv[j]);
+        if constexpr (HAS_BIAS) t += bf2f(bv[j]);
+        o[j] = f2bf(t);
+      }
+      *reinterpret_cast<u16x8*>(y + row * y_stride + ch * 8) = o;
+    }
+  }
+}
+
+template <bool RMS, bool HAS_RES, bool HAS_BIAS>
+static void launch_norm_t(const bf16_t* x, int64_t xs, const bf16_t* ri, bf16_t* ro, const bf16_t* w,
+                          const bf16_t* b, bf16_t* y, int64_t ys, int T, int H, float eps, hipStream_t st) {
+  const int nchunk = H / 8;
+  int threads = nchunk <= 256 ? ((nchunk + 63) / 64) * 64 : 256;
+  const int maxc = (nchunk + threads - 1) / threads;
+  dim3 grid(T), block(threads);
+  if (maxc == 1)
+    add_norm_kernel<1, RMS, HAS_RES, HAS_BIAS><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps);
+  else if (maxc == 2)
+    add_norm_kernel<2, RMS, HAS_RES, HAS_BIAS><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps);
+  else if (maxc <= 4)
+    add_norm_kernel<4, RMS, HAS_RES, HAS_BIAS><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps);
+  else if (maxc <= 8)
+    add_norm_kernel<8, RMS, HAS_RES, HAS_BIAS><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps);
+  else
+    throw std::runtime_error("add_norm: hidden size too large (max 16384)");
+  HIP_CHECK_LAUNCH();
+}
+
+void launch_add_norm(const void* x, int64_t x_stride, const void* res_in, void* res_out, const void* w,
+                     const void* b, void* y, int64_t y_stride, int T, int H, float eps, bool rms,
+                     hipStream_t st) {
+  if (H % 8 != 0) throw std::runtime_error("add_norm: hidden size must be a multiple of 8");
+  if (T == 0) return;
+  auto X = (const bf16_t*)x;
+  auto RI = (const bf16_t*)res_in;
+  auto RO = (bf16_t*)res_out;
+  auto W = (const bf16_t*)w;
+  auto B = (const bf16_t*)b;
+  auto Y = (bf16_t*)y;
+  const bool has_res = res_in != nullptr, has_b = b != nullptr;
+  if (rms) {
+    if (has_res) launch_norm_t<true, true, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st);
+    else launch_norm_t<true, false, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st);
+  } else {
+    if (has_res) {
+      if (has_b) launch_norm_t<false, true, true>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st);
+      else launch_norm_t<false, true, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st);
+    } else {
+      if (has_b) launch_norm_t<false, false, true>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st);
+      else launch_norm_t<false, false, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st);
+    }
+  }
+}

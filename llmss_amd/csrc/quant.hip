@@ -1,0 +1,41 @@
+// fp8 (OCP e4m3fn, gfx950-native - not the MI300 fnuz variant) weight quantisation at load time:
+// one scale per output row (channel), q = saturate(w / scale), scale = absmax / 448.
+// Used by the W8A16 path of the skinny GEMM (weights dequantised in registers, halving the
+// HBM bytes that bound decode) for the Llama-2-70B TP=8 fp8 configuration.
+#include "common.h"
+
+__global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __restrict__ w, unsigned char* __restrict__ q,
+                                                             float* __restrict__ scale, int64_t K) {
+  __shared__ float red[16];
+  const int64_t r = blockIdx.x;
+  const bf16_t* wr = w + r * K;
+  float amax = 0.f;
+  for (int64_t k = threadIdx.x * 8; k < K; k += blockDim.x * 8) {
+    u16x8 v = *reinterpret_cast<const u16x8*>(wr + k);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(bf2f(v[j])));
+  }
+  amax = block_max(amax, red);
+  const float s = amax > 0.f ? amax / 448.f : 1.f;
+  const float inv = 1.f / s;
+  if (threadIdx.x == 0) scale[r] = s;
+  for (int64_t k = threadIdx.x * 8; k < K; k += blockDim.x * 8) {
+    u16x8 v = *reinterpret_cast<const u16x8*>(wr + k);
+    unsigned lo = 0, hi = 0;
+    float f[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = fminf(fmaxf(bf2f(v[j]) * inv, -448.f), 448.f);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], lo, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], hi, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
+    *reinterpret_cast<uint2*>(q + r * K + k) = make_uint2(lo, hi);
+  }
+}
+
+void launch_quant_fp8_rows(const void* w, void* q, void* scale, int64_t N, int64_t K, hipStream_t st) {
+  if (K % 8) throw std::runtime_error("quant_fp8_rows: K must be a multiple of 8");
+  if (N == 0) return;
+  quant_fp8_rows_kernel<<<(unsigned)N, 256, 0, st>>>((const bf16_t*)w, (unsigned char*)q, (float*)scale, K);
+  HIP_CHECK_LAUNCH();
+}

@@ -1,0 +1,604 @@
+// Native host runtime for the serving engine (part of module llmss_amd._C).
+//
+//   * BlockAllocator  - paged KV-cache block pool (free stack + ref counts).
+//   * Scheduler       - continuous-batching scheduler: FCFS admission of prefills under a token /
+//                       sequence / free-block budget, then one decode token for every running
+//                       sequence; when the pool runs dry the newest running sequence is preempted
+//                       (blocks freed, re-queued at the front, recomputed later). It emits the
+//                       flat step metadata the kernels consume (positions, slot mapping, padded
+//                       block tables, context lengths) so Python never loops over tokens.
+//   * SafetensorsFile - mmap'ed .safetensors reader that copies tensor-parallel shards (row or
+//                       column slices) with several threads straight into caller memory (pinned
+//                       host staging buffers), reading only the bytes of the shard.
+//
+// Reference: the reference has no scheduler at all - one request at a time, batch_size = 1,
+// a spinning broadcast_object_list when idle (consumer_server.py:73-111), and a KV cache grown by
+// torch.cat (gptj_modeling.py:229-236); weights via safetensors' Python safe_open
+// (utils/weights.py:9-115).
+#include <fcntl.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace py = pybind11;
+
+// ============================================================================ BlockAllocator
+class BlockAllocator {
+ public:
+  BlockAllocator(int num_blocks, int block_size) : num_blocks_(num_blocks), block_size_(block_size), ref_(num_blocks, 0) {
+    if (num_blocks <= 0 || block_size <= 0) throw std::invalid_argument("BlockAllocator: bad sizes");
+    free_.reserve(num_blocks);
+    for (int i = num_blocks - 1; i >= 0; --i) free_.push_back(i);
+  }
+  int num_free() const { return (int)free_.size(); }
+  int num_blocks() const { return num_blocks_; }
+  int block_size() const { return block_size_; }
+  bool can_allocate(int n) const { return n <= (int)free_.size(); }
+  int allocate() {
+    if (free_.empty()) throw std::runtime_error("BlockAllocator: out of blocks");
+    int b = free_.back();
+    free_.pop_back();
+    ref_[b] = 1;
+    return b;
+  }
+  std::vector<int> allocate_n(int n) {
+    if (!can_allocate(n)) throw std::runtime_error("BlockAllocator: out of blocks");
+    std::vector<int> out;
+    out.reserve(n);
+    for (int i = 0; i < n; ++i) out.push_back(allocate());
+    return out;
+  }
+  void fork(int b) {  // share a block (copy-on-write style prefix sharing)
+    check(b);
+    if (ref_[b] <= 0) throw std::runtime_error("BlockAllocator: fork of a free block");
+    ++ref_[b];
+  }
+  void free(int b) {
+    check(b);
+    if (ref_[b] <= 0) throw std::runtime_error("BlockAllocator: double free of block " + std::to_string(b));
+    if (--ref_[b] == 0) free_.push_back(b);
+  }
+  void free_all(const std::vector<int>& bs) {
+    for (int b : bs) free(b);
+  }
+  int ref_count(int b) const {
+    check(b);
+    return ref_[b];
+  }
+
+ private:
+  void check(int b) const {
+    if (b < 0 || b >= num_blocks_) throw std::out_of_range("BlockAllocator: bad block id");
+  }
+  int num_blocks_, block_size_;
+  std::vector<int> ref_;
+  std::vector<int> free_;
+};
+
+// ============================================================================ Scheduler
+struct SeqState {
+  int64_t id;
+  int prompt_len;
+  int max_new;
+  int num_tokens;  // prompt + generated
+  std::vector<int> blocks;
+  int status;  // 0 waiting, 1 running, 2 finished
+  int64_t order;
+  int preemptions = 0;
+};
+
+struct StepBatch {
+  int kind = 0;  // 0 idle, 1 prefill, 2 decode
+  std::vector<int64_t> ids;
+  std::vector<int> query_lens;  // new tokens fed this step per sequence
+  std::vector<int> ctx_lens;    // KV length after this step per sequence
+  std::vector<int64_t> positions;
+  std::vector<int64_t> slots;
+  std::vector<int> block_table;  // [B, max_blocks] padded with 0
+  int max_blocks = 0;
+  std::vector<int64_t> preempted;
+};
+
+class Scheduler {
+ public:
+  Scheduler(int num_blocks, int block_size, int max_num_seqs, int max_batched_tokens, int max_model_len)
+      : alloc_(num_blocks, block_size),
+        bs_(block_size),
+        max_seqs_(max_num_seqs),
+        max_tokens_(max_batched_tokens),
+        max_len_(max_model_len) {
+    max_blocks_per_seq_ = (max_model_len + block_size - 1) / block_size;
+  }
+
+  void add(int64_t id, int prompt_len, int max_new) {
+    if (seqs_.count(id)) throw std::invalid_argument("Scheduler.add: duplicate id " + std::to_string(id));
+    if (prompt_len <= 0) throw std::invalid_argument("Scheduler.add: empty prompt");
+    if (prompt_len + max_new > max_len_)
+      throw std::invalid_argument("Scheduler.add: prompt_len + max_new_tokens exceeds max_model_len");
+    SeqState s{id, prompt_len, max_new, prompt_len, {}, 0, counter_++};
+    seqs_.emplace(id, s);
+    waiting_.push_back(id);
+  }
+
+  // A token was sampled for `id`; `finished` releases its blocks.
+  void on_token(int64_t id, bool finished) {
+    auto& s = get(id);
+    if (s.status != 1) throw std::runtime_error("Scheduler.on_token: sequence not running");
+    s.num_tokens += 1;
+    if (finished || s.num_tokens - s.prompt_len >= s.max_new) finish(id);
+  }
+
+  void finish(int64_t id) {
+    auto it = seqs_.find(id);
+    if (it == seqs_.end()) return;
+    auto& s = it->second;
+    alloc_.free_all(s.blocks);
+    s.blocks.clear();
+    if (s.status == 1) running_.erase(std::remove(running_.begin(), running_.end(), id), running_.end());
+    if (s.status == 0) waiting_.erase(std::remove(waiting_.begin(), waiting_.end(), id), waiting_.end());
+    seqs_.erase(it);
+  }
+
+  void abort(int64_t id) { finish(id); }
+
+  StepBatch schedule() {
+    StepBatch b;
+    // ---- admit prefills (FCFS, stop at the first one that does not fit)
+    int tokens = 0;
+    while (!waiting_.empty() && (int)running_.size() + (int)b.ids.size() < max_seqs_) {
+      auto& s = get(waiting_.front());
+      const int n = s.num_tokens;  // full recompute after preemption
+      const int need = blocks_for(n);
+      if (!b.ids.empty() && tokens + n > max_tokens_) break;
+      if (!alloc_.can_allocate(need)) break;
+      s.blocks = alloc_.allocate_n(need);
+      s.status = 1;
+      waiting_.pop_front();
+      b.ids.push_back(s.id);
+      b.query_lens.push_back(n);
+      b.ctx_lens.push_back(n);
+      for (int p = 0; p < n; ++p) {
+        b.positions.push_back(p);
+        b.slots.push_back(slot(s, p));
+      }
+      tokens += n;
+    }
+    if (!b.ids.empty()) {
+      for (auto id : b.ids) running_.push_back(id);
+      b.kind = 1;
+      fill_tables(b);
+      return b;
+    }
+    // ---- decode: one token per running sequence, preempting the newest on exhaustion
+    std::vector<int64_t> order(running_.begin(), running_.end());
+    std::sort(order.begin(), order.end(), [&](int64_t a, int64_t c) { return get(a).order < get(c).order; });
+    std::vector<int64_t> batch;
+    for (size_t i = 0; i < order.size(); ++i) {
+      auto& s = get(order[i]);
+      if (s.status != 1) continue;
+      while ((int)s.blocks.size() * bs_ < s.num_tokens) {
+        if (alloc_.can_allocate(1)) {
+          s.blocks.push_back(alloc_.allocate());
+          continue;
+        }
+        // preempt the newest running sequence that is not s (or s itself if it is the newest)
+        int64_t victim = -1;
+        for (size_t j = order.size(); j-- > i;) {
+          if (get(order[j]).status == 1) {
+            victim = order[j];
+            break;
+          }
+        }
+        preempt(victim);
+        b.preempted.push_back(victim);
+        if (victim == s.id) break;
+      }
+      if (s.status == 1) batch.push_back(s.id);
+    }
+    if (batch.empty()) return b;
+    b.kind = 2;
+    for (auto id : batch) {
+      auto& s = get(id);
+      b.ids.push_back(id);
+      b.query_lens.push_back(1);
+      b.ctx_lens.push_back(s.num_tokens);
+      b.positions.push_back(s.num_tokens - 1);
+      b.slots.push_back(slot(s, s.num_tokens - 1));
+    }
+    fill_tables(b);
+    return b;
+  }
+
+  int num_waiting() const { return (int)waiting_.size(); }
+  int num_running() const { return (int)running_.size(); }
+  int num_free_blocks() const { return alloc_.num_free(); }
+  int max_blocks_per_seq() const { return max_blocks_per_seq_; }
+  bool has_work() const { return !waiting_.empty() || !running_.empty(); }
+  int num_tokens(int64_t id) { return get(id).num_tokens; }
+  std::vector<int> blocks(int64_t id) { return get(id).blocks; }
+  bool contains(int64_t id) const { return seqs_.count(id) > 0; }
+
+ private:
+  SeqState& get(int64_t id) {
+    auto it = seqs_.find(id);
+    if (it == seqs_.end()) throw std::out_of_range("Scheduler: unknown sequence " + std::to_string(id));
+    return it->second;
+  }
+  int blocks_for(int n) const { return (n + bs_ - 1) / bs_; }
+  int64_t slot(const SeqState& s, int p) const { return (int64_t)s.blocks[p / bs_] * bs_ + p % bs_; }
+  void preempt(int64_t id) {
+    auto& s = get(id);
+    alloc_.free_all(s.blocks);
+    s.blocks.clear();
+    s.status = 0;
+    s.preemptions++;
+    running_.erase(std::remove(running_.begin(), running_.end(), id), running_.end());
+    waiting_.push_front(id);
+  }
+  void fill_tables(StepBatch& b) {
+    const int B = (int)b.ids.size();
+    b.max_blocks = max_blocks_per_seq_;
+    b.block_table.assign((size_t)B * b.max_blocks, 0);
+    for (int i = 0; i < B; ++i) {
+      const auto& s = get(b.ids[i]);
+      std::copy(s.blocks.begin(), s.blocks.end(), b.block_table.begin() + (size_t)i * b.max_blocks);
+    }
+  }
+
+  BlockAllocator alloc_;
+  int bs_, max_seqs_, max_tokens_, max_len_, max_blocks_per_seq_;
+  std::unordered_map<int64_t, SeqState> seqs_;
+  std::deque<int64_t> waiting_;
+  std::vector<int64_t> running_;
+  int64_t counter_ = 0;
+};
+
+// ============================================================================ safetensors
+// Minimal JSON reader for the safetensors header: {"name": {"dtype": "...", "shape": [...],
+// "data_offsets": [a, b]}, ..., "__metadata__": {"k": "v"}}.
+struct TensorInfo {
+  std::string dtype;
+  std::vector<int64_t> shape;
+  int64_t begin = 0, end = 0;
+};
+
+class JsonCursor {
+ public:
+  explicit JsonCursor(const std::string& s) : s_(s) {}
+  void ws() {
+    while (i_ < s_.size() && isspace((unsigned char)s_[i_])) ++i_;
+  }
+  char peek() {
+    ws();
+    if (i_ >= s_.size()) throw std::runtime_error("safetensors header: unexpected end");
+    return s_[i_];
+  }
+  void expect(char c) {
+    if (peek() != c) throw std::runtime_error(std::string("safetensors header: expected ") + c);
+    ++i_;
+  }
+  std::string str() {
+    expect('"');
+    std::string out;
+    while (i_ < s_.size() && s_[i_] != '"') {
+      if (s_[i_] == '\\') {
+        ++i_;
+        if (i_ >= s_.size()) break;
+        char c = s_[i_];
+        if (c == 'u') {  // keep escaped code points verbatim (names are ASCII in practice)
+          out += "\\u";
+        } else {
+          out += c == 'n' ? '\n' : c == 't' ? '\t' : c;
+        }
+      } else {
+        out += s_[i_];
+      }
+      ++i_;
+    }
+    expect('"');
+    return out;
+  }
+  int64_t integer() {
+    ws();
+    size_t j = i_;
+    if (j < s_.size() && (s_[j] == '-' || s_[j] == '+')) ++j;
+    while (j < s_.size() && isdigit((unsigned char)s_[j])) ++j;
+    int64_t v = std::stoll(s_.substr(i_, j - i_));
+    i_ = j;
+    return v;
+  }
+  void skip_value() {
+    char c = peek();
+    if (c == '"') {
+      str();
+    } else if (c == '{') {
+      expect('{');
+      if (peek() == '}') {
+        ++i_;
+        return;
+      }
+      while (true) {
+        str();
+        expect(':');
+        skip_value();
+        if (peek() == ',') {
+          ++i_;
+          continue;
+        }
+        expect('}');
+        break;
+      }
+    } else if (c == '[') {
+      expect('[');
+      if (peek() == ']') {
+        ++i_;
+        return;
+      }
+      while (true) {
+        skip_value();
+        if (peek() == ',') {
+          ++i_;
+          continue;
+        }
+        expect(']');
+        break;
+      }
+    } else {
+      while (i_ < s_.size() && s_[i_] != ',' && s_[i_] != '}' && s_[i_] != ']') ++i_;
+    }
+  }
+  size_t pos() const { return i_; }
+  void advance() { ++i_; }
+
+ private:
+  const std::string& s_;
+  size_t i_ = 0;
+};
+
+static int dtype_size(const std::string& d) {
+  if (d == "F64" || d == "I64" || d == "U64") return 8;
+  if (d == "F32" || d == "I32" || d == "U32") return 4;
+  if (d == "F16" || d == "BF16" || d == "I16" || d == "U16") return 2;
+  if (d == "I8" || d == "U8" || d == "BOOL" || d == "F8_E4M3" || d == "F8_E5M2") return 1;
+  throw std::runtime_error("safetensors: unsupported dtype " + d);
+}
+
+class SafetensorsFile {
+ public:
+  explicit SafetensorsFile(const std::string& path) : path_(path) {
+    fd_ = ::open(path.c_str(), O_RDONLY);
+    if (fd_ < 0) throw std::runtime_error("safetensors: cannot open " + path);
+    struct stat st;
+    fstat(fd_, &st);
+    size_ = st.st_size;
+    if (size_ < 8) throw std::runtime_error("safetensors: file too small");
+    map_ = (const char*)mmap(nullptr, size_, PROT_READ, MAP_PRIVATE, fd_, 0);
+    if (map_ == MAP_FAILED) throw std::runtime_error("safetensors: mmap failed");
+    uint64_t hlen;
+    std::memcpy(&hlen, map_, 8);
+    if (8 + hlen > (uint64_t)size_) throw std::runtime_error("safetensors: bad header length");
+    data_ = map_ + 8 + hlen;
+    std::string header(map_ + 8, hlen);
+    parse(header);
+  }
+  ~SafetensorsFile() {
+    if (map_ && map_ != MAP_FAILED) munmap((void*)map_, size_);
+    if (fd_ >= 0) ::close(fd_);
+  }
+  std::vector<std::string> keys() const {
+    std::vector<std::string> k;
+    for (auto& kv : tensors_) k.push_back(kv.first);
+    return k;
+  }
+  py::tuple info(const std::string& name) const {
+    const auto& t = at(name);
+    return py::make_tuple(t.dtype, t.shape, t.begin, t.end);
+  }
+  std::map<std::string, std::string> metadata() const { return meta_; }
+
+  // Copy rows [start, stop) along `dim` (0 or 1) of tensor `name` into dst (contiguous).
+  void copy_slice(const std::string& name, int dim, int64_t start, int64_t stop, uintptr_t dst, int threads) {
+    const auto& t = at(name);
+    const int es = dtype_size(t.dtype);
+    const char* src = data_ + t.begin;
+    char* out = reinterpret_cast<char*>(dst);
+    if (t.shape.empty()) {
+      std::memcpy(out, src, es);
+      return;
+    }
+    int64_t inner = es;
+    for (size_t i = 1; i < t.shape.size(); ++i) inner *= t.shape[i];
+    if (dim == 0) {
+      if (start < 0 || stop > t.shape[0] || start > stop) throw std::out_of_range("copy_slice: bad range");
+      parallel_copy(out, src + start * inner, (stop - start) * inner, threads);
+      return;
+    }
+    if (dim != 1 || t.shape.size() < 2) throw std::invalid_argument("copy_slice: dim must be 0 or 1");
+    int64_t inner2 = es;
+    for (size_t i = 2; i < t.shape.size(); ++i) inner2 *= t.shape[i];
+    if (start < 0 || stop > t.shape[1] || start > stop) throw std::out_of_range("copy_slice: bad range");
+    const int64_t rows = t.shape[0], row_bytes = t.shape[1] * inner2, seg = (stop - start) * inner2;
+    const int nt = std::max(1, std::min<int>(threads, (int)rows));
+    std::vector<std::thread> pool;
+    for (int w = 0; w < nt; ++w) {
+      pool.emplace_back([=]() {
+        for (int64_t r = w; r < rows; r += nt) std::memcpy(out + r * seg, src + r * row_bytes + start * inner2, seg);
+      });
+    }
+    for (auto& th : pool) th.join();
+  }
+  int64_t nbytes(const std::string& name) const {
+    const auto& t = at(name);
+    return t.end - t.begin;
+  }
+
+ private:
+  static void parallel_copy(char* dst, const char* src, int64_t n, int threads) {
+    const int64_t chunk = 8 << 20;
+    if (threads <= 1 || n < 2 * chunk) {
+      std::memcpy(dst, src, n);
+      return;
+    }
+    const int nt = std::min<int64_t>(threads, (n + chunk - 1) / chunk);
+    std::vector<std::thread> pool;
+    const int64_t per = (n + nt - 1) / nt;
+    for (int w = 0; w < nt; ++w) {
+      const int64_t b = w * per, e = std::min(n, b + per);
+      if (b >= e) break;
+      pool.emplace_back([=]() { std::memcpy(dst + b, src + b, e - b); });
+    }
+    for (auto& th : pool) th.join();
+  }
+  const TensorInfo& at(const std::string& name) const {
+    auto it = tensors_.find(name);
+    if (it == tensors_.end()) throw std::out_of_range("safetensors: no tensor " + name);
+    return it->second;
+  }
+  void parse(const std::string& h) {
+    JsonCursor c(h);
+    c.expect('{');
+    if (c.peek() == '}') return;
+    while (true) {
+      std::string key = c.str();
+      c.expect(':');
+      if (key == "__metadata__") {
+        c.expect('{');
+        if (c.peek() != '}') {
+          while (true) {
+            std::string k = c.str();
+            c.expect(':');
+            if (c.peek() == '"') meta_[k] = c.str();
+            else c.skip_value();
+            if (c.peek() == ',') { c.advance(); continue; }
+            break;
+          }
+        }
+        c.expect('}');
+      } else {
+        TensorInfo t;
+        c.expect('{');
+        while (true) {
+          std::string f = c.str();
+          c.expect(':');
+          if (f == "dtype") {
+            t.dtype = c.str();
+          } else if (f == "shape") {
+            c.expect('[');
+            if (c.peek() != ']') {
+              while (true) {
+                t.shape.push_back(c.integer());
+                if (c.peek() == ',') { c.advance(); continue; }
+                break;
+              }
+            }
+            c.expect(']');
+          } else if (f == "data_offsets") {
+            c.expect('[');
+            t.begin = c.integer();
+            c.expect(',');
+            t.end = c.integer();
+            c.expect(']');
+          } else {
+            c.skip_value();
+          }
+          if (c.peek() == ',') { c.advance(); continue; }
+          break;
+        }
+        c.expect('}');
+        if (t.end < t.begin || (int64_t)(data_ - map_) + t.end > size_)
+          throw std::runtime_error("safetensors: tensor " + key + " out of file bounds");
+        tensors_[key] = t;
+      }
+      if (c.peek() == ',') { c.advance(); continue; }
+      break;
+    }
+    c.expect('}');
+  }
+
+  std::string path_;
+  int fd_ = -1;
+  int64_t size_ = 0;
+  const char* map_ = nullptr;
+  const char* data_ = nullptr;
+  std::map<std::string, TensorInfo> tensors_;
+  std::map<std::string, std::string> meta_;
+};
+
+// ============================================================================ bindings
+template <typename T>
+static py::array_t<T> to_np(const std::vector<T>& v) {
+  py::array_t<T> a(v.size());
+  if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
+  return a;
+}
+
+void register_runtime(py::module_& m) {
+  py::class_<BlockAllocator>(m, "BlockAllocator")
+      .def(py::init<int, int>(), py::arg("num_blocks"), py::arg("block_size"))
+      .def("num_free", &BlockAllocator::num_free)
+      .def("num_blocks", &BlockAllocator::num_blocks)
+      .def("block_size", &BlockAllocator::block_size)
+      .def("can_allocate", &BlockAllocator::can_allocate)
+      .def("allocate", &BlockAllocator::allocate)
+      .def("allocate_n", &BlockAllocator::allocate_n)
+      .def("fork", &BlockAllocator::fork)
+      .def("free", &BlockAllocator::free)
+      .def("free_all", &BlockAllocator::free_all)
+      .def("ref_count", &BlockAllocator::ref_count);
+
+  py::class_<StepBatch>(m, "StepBatch")
+      .def_readonly("kind", &StepBatch::kind)
+      .def_readonly("max_blocks", &StepBatch::max_blocks)
+      .def_property_readonly("ids", [](const StepBatch& b) { return to_np(b.ids); })
+      .def_property_readonly("query_lens", [](const StepBatch& b) { return to_np(b.query_lens); })
+      .def_property_readonly("ctx_lens", [](const StepBatch& b) { return to_np(b.ctx_lens); })
+      .def_property_readonly("positions", [](const StepBatch& b) { return to_np(b.positions); })
+      .def_property_readonly("slots", [](const StepBatch& b) { return to_np(b.slots); })
+      .def_property_readonly("block_table",
+                             [](const StepBatch& b) {
+                               auto a = to_np(b.block_table);
+                               const ssize_t B = (ssize_t)b.ids.size();
+                               a.resize({B, (ssize_t)b.max_blocks});
+                               return a;
+                             })
+      .def_property_readonly("preempted", [](const StepBatch& b) { return to_np(b.preempted); });
+
+  py::class_<Scheduler>(m, "Scheduler")
+      .def(py::init<int, int, int, int, int>(), py::arg("num_blocks"), py::arg("block_size"), py::arg("max_num_seqs"),
+           py::arg("max_batched_tokens"), py::arg("max_model_len"))
+      .def("add", &Scheduler::add)
+      .def("on_token", &Scheduler::on_token)
+      .def("finish", &Scheduler::finish)
+      .def("abort", &Scheduler::abort)
+      .def("schedule", &Scheduler::schedule)
+      .def("num_waiting", &Scheduler::num_waiting)
+      .def("num_running", &Scheduler::num_running)
+      .def("num_free_blocks", &Scheduler::num_free_blocks)
+      .def("max_blocks_per_seq", &Scheduler::max_blocks_per_seq)
+      .def("has_work", &Scheduler::has_work)
+      .def("num_tokens", &Scheduler::num_tokens)
+      .def("blocks", &Scheduler::blocks)
+      .def("contains", &Scheduler::contains);
+
+  py::class_<SafetensorsFile>(m, "SafetensorsFile")
+      .def(py::init<const std::string&>())
+      .def("keys", &SafetensorsFile::keys)
+      .def("info", &SafetensorsFile::info)
+      .def("metadata", &SafetensorsFile::metadata)
+      .def("nbytes", &SafetensorsFile::nbytes)
+      .def("copy_slice", &SafetensorsFile::copy_slice, py::arg("name"), py::arg("dim"), py::arg("start"),
+           py::arg("stop"), py::arg("dst"), py::arg("threads") = 8);
+}

@@ -1,0 +1,124 @@
+"""Family-agnostic tensor-parallel decoder forward over a paged KV cache.
+
+Replaces the per-family modeling files of the reference (``gptj_modeling.py`` 648 lines,
+``gpt_bigcode_modeling.py`` 926 lines, HF ``PreTrainedModel`` glue) with one forward that
+covers GPT-2, GPT-J (parallel block), GPT-BigCode (MQA/MHA) and Llama (RMSNorm/SwiGLU/GQA):
+
+    per layer (sequential):  y = norm1(x + delta)          fused residual add + norm (K3/K17)
+                             qkv = y @ Wqkv (+b)            column-parallel GEMM (K4)
+                             rope + paged KV write          in place (K8/K10)
+                             a = attention(q, cache)        prefill flash / split-K decode (K11-14)
+                             o = a @ Wo (+b rank 0)         row-parallel GEMM (K6) -> all-reduce
+                             y2 = norm2(x + o)
+                             m = act(y2 @ Wup (+b))         GEMM with fused GELU / SwiGLU epilogue
+                             delta = m @ Wdown -> all-reduce
+    GPT-J (parallel):        delta = (a @ Wo) + mlp(y) -> ONE all-reduce per layer (the reference
+                             all-reduces twice per layer)
+
+Tokens of all sequences in a step are flattened ([T, H]); the LM head runs on the last token of
+each sequence only (the reference runs it on every prompt position, K7) and is vocab-parallel
+followed by an all-gather of [B, V/tp] logits.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import torch
+
+from .. import ops
+from ..parallel.dist import TPGroup
+from .config import ModelConfig
+from .weights import ModelWeights, ShardPlan, shard_plan
+
+
+@dataclass
+class StepInput:
+    kind: str  # "prefill" | "decode"
+    input_ids: torch.Tensor  # [T] int64
+    positions: torch.Tensor  # [T] int64
+    slots: torch.Tensor  # [T] int64 physical KV slots (-1 = do not cache)
+    cu_seqlens: Optional[torch.Tensor] = None  # prefill: [B+1] int32
+    max_seqlen: int = 0
+    block_tables: Optional[torch.Tensor] = None  # decode: [B, maxb] int32
+    ctx_lens: Optional[torch.Tensor] = None  # decode: [B] int32
+    max_ctx: int = 0
+    decode_splits: Optional[Tuple[int, int]] = None
+    last_idx: Optional[torch.Tensor] = None  # rows feeding the LM head ([B] int64); None = all rows
+
+
+class DecoderLM:
+    def __init__(self, cfg: ModelConfig, weights: ModelWeights, tp: Optional[TPGroup] = None):
+        self.cfg = cfg
+        self.w = weights
+        self.tp = tp or TPGroup()
+        self.plan: ShardPlan = shard_plan(cfg, self.tp.size, self.tp.rank)
+        self.scale = cfg.head_dim ** -0.5
+        self.rms = cfg.norm == "rmsnorm"
+        self.act = "none" if cfg.gated_mlp else cfg.activation
+
+    @property
+    def device(self):
+        return self.w.wte.device
+
+    @property
+    def dtype(self):
+        return self.w.wte.dtype
+
+    # --------------------------------------------------------------------------------- KV
+    def kv_cache_shape(self, num_blocks: int, block_size: int):
+        return (num_blocks, self.plan.nkv_l, block_size, self.cfg.head_dim)
+
+    def kv_bytes_per_block(self, block_size: int) -> int:
+        return 2 * self.cfg.num_layers * self.plan.nkv_l * block_size * self.cfg.head_dim * 2
+
+    def allocate_kv_cache(self, num_blocks: int, block_size: int):
+        shp = self.kv_cache_shape(num_blocks, block_size)
+        return [(torch.zeros(shp, dtype=self.dtype, device=self.device),
+                 torch.zeros(shp, dtype=self.dtype, device=self.device)) for _ in range(self.cfg.num_layers)]
+
+    # ---------------------------------------------------------------------------- forward
+    def _attention(self, qkv, inp: StepInput, kc, vc):
+        cfg, p = self.cfg, self.plan
+        D = cfg.head_dim
+        ops.rope_cache(qkv, inp.positions, self.w.cos, self.w.sin, kc, vc, inp.slots, p.nh_l, p.nkv_l, D,
+                       cfg.rotary_dim, cfg.rope_style, do_rope=cfg.position == "rope")
+        if inp.kind == "prefill":
+            return ops.attn_prefill(qkv, inp.cu_seqlens, inp.max_seqlen, p.nh_l, p.nkv_l, D, self.scale)
+        return ops.attn_decode(qkv, kc, vc, inp.block_tables, inp.ctx_lens, p.nh_l, p.nkv_l, D, self.scale,
+                               inp.max_ctx, splits=inp.decode_splits)
+
+    def hidden_states(self, inp: StepInput, kv_caches) -> torch.Tensor:
+        cfg, w = self.cfg, self.w
+        eps, rms = cfg.norm_eps, self.rms
+        x = ops.embed(inp.input_ids, w.wte, inp.positions if w.wpe is not None else None, w.wpe)
+        residual = None
+        delta = x
+        for i, L in enumerate(w.layers):
+            kc, vc = kv_caches[i]
+            y, residual = ops.add_norm(delta, L.ln1_w, L.ln1_b, eps, rms, residual)
+            a = self._attention(L.qkv(y), inp, kc, vc)
+            o = L.o(a)
+            if cfg.parallel_block:
+                m = L.down(L.up(y, self.act))
+                o.add_(m)
+                delta = self.tp.all_reduce(o)
+            else:
+                o = self.tp.all_reduce(o)
+                y2, residual = ops.add_norm(o, L.ln2_w, L.ln2_b, eps, rms, residual)
+                delta = self.tp.all_reduce(L.down(L.up(y2, self.act)))
+        h, _ = ops.add_norm(delta, w.lnf_w, w.lnf_b, eps, rms, residual)
+        return h
+
+    def logits(self, h: torch.Tensor) -> torch.Tensor:
+        """[B, H] -> full-vocab logits [B, Vpadded] (all-gathered across TP ranks)."""
+        local = self.w.head(h)
+        return self.tp.all_gather_last_dim(local)
+
+    def forward(self, inp: StepInput, kv_caches) -> torch.Tensor:
+        h = self.hidden_states(inp, kv_caches)
+        if inp.last_idx is not None:
+            h = h.index_select(0, inp.last_idx)
+        return self.logits(h)
+
+    __call__ = forward

@@ -1,0 +1,75 @@
+"""Op API used by the models. Routing is by tensor device only:
+
+* CUDA (HIP) tensors -> the hand-written gfx950 kernels (``ops/hip.py`` -> ``llmss_amd._C``);
+  a missing extension raises, it never falls back to PyTorch.
+* CPU tensors -> the PyTorch definitions in ``ops/reference.py`` (CPU plumbing path / oracle).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+
+__all__ = ["add_norm", "embed", "rope_cache", "attn_prefill", "attn_decode", "linear", "sample", "quant_fp8_rows",
+           "rope_tables", "glu_interleave", "glu_split"]
+
+rope_tables = ref.rope_tables
+glu_interleave = ref.glu_interleave
+glu_split = ref.glu_split
+
+
+def _hip():
+    from . import hip
+    return hip
+
+
+def add_norm(x, weight, bias, eps, rms, residual=None):
+    if x.is_cuda:
+        return _hip().add_norm(x, weight, bias, eps, rms, residual)
+    return ref.add_norm(x, weight, bias, eps, rms, residual)
+
+
+def embed(ids, wte, positions=None, wpe=None):
+    if wte.is_cuda:
+        return _hip().embed(ids, wte, positions, wpe)
+    return ref.embed(ids, wte, positions, wpe)
+
+
+def rope_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, rot, style, do_rope=True):
+    if qkv.is_cuda:
+        return _hip().rope_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, rot, style, do_rope)
+    return ref.rope_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, rot, style, do_rope)
+
+
+def attn_prefill(qkv, cu_seqlens, max_seqlen, nh, nkv, D, scale):
+    if qkv.is_cuda:
+        return _hip().attn_prefill(qkv, cu_seqlens, max_seqlen, nh, nkv, D, scale)
+    return ref.attn_prefill(qkv, cu_seqlens, nh, nkv, D, scale)
+
+
+def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale, max_ctx, splits=None):
+    if q.is_cuda:
+        return _hip().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale, max_ctx,
+                                  splits=splits)
+    return ref.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale)
+
+
+def linear(x, w, bias=None, act="none", glu=False, w_scale: Optional[torch.Tensor] = None):
+    if x.is_cuda:
+        return _hip().linear(x, w, bias, act, glu, w_scale)
+    return ref.linear(x, w, bias, act, glu, w_scale)
+
+
+def sample(logits, temperature, top_k, top_p, seeds, vocab=None):
+    if logits.is_cuda:
+        return _hip().sample(logits, temperature, top_k, top_p, seeds, vocab)
+    lg = logits if vocab is None else logits[:, :vocab]
+    return ref.sample(lg, temperature, top_k, top_p, seeds)
+
+
+def quant_fp8_rows(w):
+    if w.is_cuda:
+        return _hip().quant_fp8_rows(w)
+    return ref.quant_fp8_rows(w)

@@ -1,0 +1,262 @@
+"""Validated launchers for the gfx950 kernels in ``llmss_amd/csrc`` (module ``llmss_amd._C``).
+
+Every wrapper checks dtype, device, contiguity/strides and the shape relations the kernel grid
+assumes *before* launching, so a malformed call raises here instead of faulting the GPU.
+Kernels run on the caller's current HIP stream (``torch.cuda.current_stream()``), which makes
+them capturable into HIP graphs together with RCCL collectives.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+_C = None
+_ERR = None
+
+
+def lib():
+    """The native module; raises loudly if it is missing (no silent eager fallback on GPU)."""
+    global _C, _ERR
+    if _C is None:
+        try:
+            from .. import _native
+            _C = _native()
+        except Exception as e:  # pragma: no cover - exercised only on broken installs
+            _ERR = e
+            raise RuntimeError(
+                "llmss_amd._C is not available: run `python -m llmss_amd._build` (hipcc --offload-arch=gfx950)"
+            ) from e
+    return _C
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _check(cond: bool, msg: str):
+    if not cond:
+        raise ValueError(msg)
+
+
+def _bf16_rows(t: torch.Tensor, name: str, cols: Optional[int] = None):
+    _check(t.is_cuda, f"{name} must be on the GPU")
+    _check(t.dtype == torch.bfloat16, f"{name} must be bfloat16, got {t.dtype}")
+    _check(t.dim() == 2, f"{name} must be 2-D")
+    _check(t.stride(1) == 1, f"{name} rows must be contiguous")
+    _check(t.data_ptr() % 16 == 0 and (t.stride(0) * 2) % 16 == 0, f"{name} must be 16-byte aligned")
+    if cols is not None:
+        _check(t.shape[1] == cols, f"{name} has {t.shape[1]} columns, expected {cols}")
+
+
+# ------------------------------------------------------------------------------------- norm
+def add_norm(x, weight, bias, eps, rms, residual=None, out=None, residual_out=None):
+    T, H = x.shape
+    _bf16_rows(x, "x")
+    _check(H % 8 == 0, "hidden must be a multiple of 8")
+    _check(weight.is_contiguous() and weight.numel() == H and weight.dtype == torch.bfloat16, "norm weight")
+    if bias is not None:
+        _check(bias.is_contiguous() and bias.numel() == H and bias.dtype == torch.bfloat16, "norm bias")
+    y = out if out is not None else torch.empty(T, H, dtype=x.dtype, device=x.device)
+    _bf16_rows(y, "out", H)
+    if residual is not None:
+        _check(residual.is_contiguous() and residual.shape == (T, H) and residual.dtype == torch.bfloat16, "residual")
+        ro = residual_out if residual_out is not None else residual
+        _check(ro.is_contiguous() and ro.shape == (T, H), "residual_out")
+    else:
+        ro = None
+    lib().add_norm(x.data_ptr(), x.stride(0), _ptr(residual), _ptr(ro), weight.data_ptr(), _ptr(bias),
+                   y.data_ptr(), y.stride(0), T, H, float(eps), bool(rms), _stream())
+    return y, (ro if residual is not None else x)
+
+
+# ------------------------------------------------------------------------------------ embed
+def embed(ids, wte, positions=None, wpe=None, out=None):
+    T = ids.numel()
+    V, H = wte.shape
+    _check(ids.dtype == torch.int64 and ids.is_contiguous() and ids.is_cuda, "ids must be contiguous int64 cuda")
+    _bf16_rows(wte, "wte")
+    _check(wte.is_contiguous(), "wte contiguous")
+    if wpe is not None:
+        _check(positions is not None and positions.dtype == torch.int64 and positions.numel() == T, "positions")
+        _check(wpe.is_contiguous() and wpe.shape[1] == H and wpe.dtype == torch.bfloat16, "wpe")
+    y = out if out is not None else torch.empty(T, H, dtype=wte.dtype, device=wte.device)
+    lib().embed(ids.data_ptr(), _ptr(positions), wte.data_ptr(), _ptr(wpe), y.data_ptr(), T, H, V, _stream())
+    return y
+
+
+# ------------------------------------------------------------------------------ rope + cache
+def rope_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, rot, style, do_rope=True):
+    T = qkv.shape[0]
+    _bf16_rows(qkv, "qkv")
+    _check(qkv.shape[1] >= (nh + 2 * nkv) * D, "qkv too narrow")
+    _check(D % 8 == 0 and rot % 2 == 0 and rot <= D, "head_dim / rotary_dim")
+    _check(positions.dtype == torch.int64 and positions.numel() == T and positions.is_contiguous(), "positions")
+    if do_rope and rot > 0:
+        _check(cos.dtype == torch.float32 and cos.is_contiguous() and cos.shape[1] == rot // 2, "cos table")
+        _check(sin.shape == cos.shape and sin.is_contiguous(), "sin table")
+    if k_cache is not None:
+        _check(k_cache.dtype == torch.bfloat16 and k_cache.is_contiguous() and k_cache.dim() == 4, "k_cache")
+        _check(k_cache.shape[1] == nkv and k_cache.shape[3] == D, "k_cache shape [nb, nkv, bs, D]")
+        _check(v_cache.shape == k_cache.shape and v_cache.is_contiguous(), "v_cache")
+        _check(slots is not None and slots.dtype == torch.int64 and slots.numel() == T, "slots")
+        bs = k_cache.shape[2]
+    else:
+        bs = 1
+    lib().rope_cache(qkv.data_ptr(), qkv.stride(0), positions.data_ptr(), _ptr(cos) if do_rope else 0,
+                     _ptr(sin) if do_rope else 0, _ptr(k_cache), _ptr(v_cache),
+                     _ptr(slots) if k_cache is not None else 0, T, nh, nkv, D, rot,
+                     bs, nh * D, (nh + nkv) * D, 1 if style == "gptj" else 0, bool(do_rope and rot > 0), _stream())
+
+
+# -------------------------------------------------------------------------------- attention
+def attn_prefill(qkv, cu_seqlens, max_seqlen, nh, nkv, D, scale, out=None):
+    T = qkv.shape[0]
+    _bf16_rows(qkv, "qkv")
+    _check(qkv.shape[1] >= (nh + 2 * nkv) * D, "qkv too narrow")
+    _check(D in (64, 128, 256), "prefill attention supports head_dim 64/128/256")
+    _check(cu_seqlens.dtype == torch.int32 and cu_seqlens.is_contiguous() and cu_seqlens.is_cuda, "cu_seqlens int32")
+    B = cu_seqlens.numel() - 1
+    y = out if out is not None else torch.empty(T, nh * D, dtype=qkv.dtype, device=qkv.device)
+    _bf16_rows(y, "out")
+    lib().attn_prefill(qkv.data_ptr(), qkv.stride(0), cu_seqlens.data_ptr(), y.data_ptr(), y.stride(0), B,
+                       int(max_seqlen), nh, nkv, D, nh * D, (nh + nkv) * D, float(scale), _stream())
+    return y
+
+
+class DecodeWorkspace:
+    """Split-K partial buffers for decode attention (allocated once; graph-capture safe)."""
+
+    def __init__(self):
+        self.po = None
+        self.pml = None
+
+    def get(self, B, nh, nsplit, D, device):
+        need = B * nh * nsplit
+        if self.po is None or self.po.numel() < need * D or self.po.device != device:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("decode workspace must be allocated before graph capture")
+            self.po = torch.empty(need * D, dtype=torch.float32, device=device)
+            self.pml = torch.empty(need * 2, dtype=torch.float32, device=device)
+        return self.po, self.pml
+
+
+_DECODE_WS = DecodeWorkspace()
+
+
+def decode_splits(B: int, nkv: int, max_ctx: int, block_size: int) -> tuple:
+    """(num_splits, partition_size): enough workgroups for 256 CUs, partitions >= 256 tokens."""
+    wgs = max(1, B * nkv)
+    want = max(1, math.ceil(512 / wgs))
+    nsplit = max(1, min(want, math.ceil(max_ctx / 256)))
+    psize = math.ceil(max_ctx / nsplit)
+    psize = math.ceil(psize / block_size) * block_size
+    nsplit = math.ceil(max_ctx / psize)
+    return nsplit, psize
+
+
+def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale, max_ctx, out=None, splits=None):
+    B = q.shape[0]
+    _check(q.is_cuda and q.dtype == torch.bfloat16 and q.stride(-1) == 1 and q.dim() == 2, "q [B, >=nh*D]")
+    _check(q.shape[1] >= nh * D, "q too narrow")
+    _check(D in (64, 128, 256), "decode attention supports head_dim 64/128/256")
+    _check(k_cache.dtype == torch.bfloat16 and k_cache.is_contiguous() and k_cache.shape[1] == nkv
+           and k_cache.shape[3] == D, "k_cache [nb, nkv, bs, D]")
+    _check(v_cache.shape == k_cache.shape and v_cache.is_contiguous(), "v_cache")
+    _check(block_tables.dtype == torch.int32 and block_tables.dim() == 2 and block_tables.shape[0] >= B
+           and block_tables.stride(1) == 1, "block_tables int32 [B, maxb]")
+    _check(ctx_lens.dtype == torch.int32 and ctx_lens.numel() >= B and ctx_lens.is_contiguous(), "ctx_lens int32")
+    bs = k_cache.shape[2]
+    _check(block_tables.shape[1] * bs >= max_ctx, "block table too short for max_ctx")
+    nsplit, psize = splits if splits is not None else decode_splits(B, nkv, max_ctx, bs)
+    _check(nsplit * psize >= max_ctx, "splits do not cover max_ctx")
+    y = out if out is not None else torch.empty(B, nh * D, dtype=q.dtype, device=q.device)
+    po, pml = _DECODE_WS.get(B, nh, nsplit, D, q.device) if nsplit > 1 else (None, None)
+    lib().attn_decode(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
+                      block_tables.stride(0), ctx_lens.data_ptr(), y.data_ptr(), y.stride(0), _ptr(po), _ptr(pml),
+                      B, nh, nkv, D, bs, nsplit, psize, float(scale), _stream())
+    return y
+
+
+# ------------------------------------------------------------------------------------- GEMM
+class GemmWorkspace:
+    def __init__(self):
+        self.buf = None
+
+    def get(self, nbytes, device):
+        if self.buf is None or self.buf.numel() * 4 < nbytes or self.buf.device != device:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("gemm workspace must be allocated before graph capture")
+            self.buf = torch.empty((max(nbytes, 1 << 20) + 3) // 4, dtype=torch.float32, device=device)
+        return self.buf
+
+
+_GEMM_WS = GemmWorkspace()
+
+
+def reserve_workspace(device, gemm_bytes: int = 64 << 20, decode_rows: int = 0, nh: int = 0, D: int = 128,
+                      nsplit: int = 1):
+    _GEMM_WS.get(gemm_bytes, device)
+    if decode_rows and nsplit > 1:
+        _DECODE_WS.get(decode_rows, nh, nsplit, D, device)
+
+
+_ACT = {"none": 0, None: 0, "gelu_tanh": 1, "gelu": 2, "relu": 3}
+
+
+def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None):
+    M, K = x.shape
+    _bf16_rows(x, "x")
+    fp8 = w_scale is not None
+    if fp8:
+        _check(w.dtype == torch.uint8 and w.is_contiguous() and w.is_cuda, "fp8 weight stored as uint8 [N, K]")
+        _check(w_scale.dtype == torch.float32 and w_scale.numel() == w.shape[0], "w_scale [N] fp32")
+    else:
+        _bf16_rows(w, "w")
+        _check(w.is_contiguous(), "w contiguous")
+    N = w.shape[0]
+    _check(w.shape[1] == K, f"weight K={w.shape[1]} != x K={K}")
+    _check(K % 16 == 0, "K must be a multiple of 16")
+    if glu:
+        _check(N % 32 == 0, "glu needs N % 32 == 0")
+    if bias is not None:
+        _check(bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.numel() == N, "bias [N] bf16")
+    nout = N // 2 if glu else N
+    y = out if out is not None else torch.empty(M, nout, dtype=x.dtype, device=x.device)
+    _bf16_rows(y, "out", nout)
+    ws = _GEMM_WS.get(64 << 20, x.device)
+    lib().gemm(x.data_ptr(), x.stride(0), w.data_ptr(), K, fp8, _ptr(w_scale), _ptr(bias), y.data_ptr(), y.stride(0),
+               M, N, K, _ACT[act], bool(glu), ws.data_ptr(), ws.numel() * 4, _stream())
+    return y
+
+
+def quant_fp8_rows(w):
+    _bf16_rows(w, "w")
+    _check(w.is_contiguous(), "w contiguous")
+    N, K = w.shape
+    q = torch.empty(N, K, dtype=torch.uint8, device=w.device)
+    s = torch.empty(N, dtype=torch.float32, device=w.device)
+    lib().quant_fp8_rows(w.data_ptr(), q.data_ptr(), s.data_ptr(), N, K, _stream())
+    return q, s
+
+
+# ---------------------------------------------------------------------------------- sampler
+def sample(logits, temperature, top_k, top_p, seeds, vocab: Optional[int] = None, out=None, out2=None):
+    _check(logits.is_cuda and logits.dim() == 2 and logits.stride(1) == 1, "logits [B, V]")
+    _check(logits.dtype in (torch.bfloat16, torch.float32), "logits bf16/fp32")
+    B = logits.shape[0]
+    V = vocab or logits.shape[1]
+    _check(V <= logits.shape[1], "vocab > logits width")
+    for t, dt, nm in ((temperature, torch.float32, "temperature"), (top_k, torch.int32, "top_k"),
+                      (top_p, torch.float32, "top_p"), (seeds, torch.int64, "seeds")):
+        if t is not None:
+            _check(t.dtype == dt and t.numel() >= B and t.is_contiguous() and t.is_cuda, f"{nm} must be {dt}")
+    y = out if out is not None else torch.empty(B, dtype=torch.int64, device=logits.device)
+    lib().sample(logits.data_ptr(), logits.stride(0), logits.dtype == torch.float32, B, V, _ptr(temperature),
+                 _ptr(top_k), _ptr(top_p), _ptr(seeds), y.data_ptr(), _ptr(out2), _stream())
+    return y

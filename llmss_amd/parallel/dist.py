@@ -1,0 +1,130 @@
+"""Process-group bootstrap and the tensor-parallel communicator.
+
+Reference: ``src/llmss/server/models/utils/dist.py:40-77`` (``initialize_torch_distributed``)
+and ``FakeGroup`` (``dist.py:14-37``). Differences, by design:
+
+* One process per GPU; the device is chosen from ``LOCAL_RANK`` (not ``RANK % count``) so the
+  same code runs on one node or several.
+* ``world_size == 1`` is a first-class case: :class:`TPGroup` with ``size == 1`` turns every
+  collective into the identity and *never* needs a default process group (the reference's
+  single-GPU ``generate.py`` crashes on an un-grouped ``dist.broadcast`` — SURVEY Q2).
+* On GPUs the backend is ``nccl`` which, on ROCm, is RCCL over xGMI. The data-plane collectives
+  are issued on the caller's current HIP stream so they can be captured into HIP graphs with
+  the rest of the decode step.
+* ``DEBUG=1`` keeps the reference's "fake" semantics: every rank computes with its own shard and
+  no communication happens (shape/loader debugging only, numerically wrong by construction).
+"""
+from __future__ import annotations
+
+import os
+from datetime import timedelta
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..utils.logging import get_logger
+
+log = get_logger(__name__)
+
+
+class TPGroup:
+    """Tensor-parallel communicator (size 1, real, or fake)."""
+
+    def __init__(self, rank: int = 0, size: int = 1, group=None, fake: bool = False):
+        self.rank = rank
+        self.size = size
+        self.group = group
+        self.fake = fake
+
+    # reference-compatible accessors (FakeGroup.size()/rank())
+    def world_size(self) -> int:
+        return self.size
+
+    @property
+    def is_real(self) -> bool:
+        return self.size > 1 and not self.fake
+
+    # ------------------------------------------------------------ data plane
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        if self.is_real:
+            dist.all_reduce(t, group=self.group)
+        return t
+
+    def all_gather_last_dim(self, t: torch.Tensor) -> torch.Tensor:
+        """Gather shards along the last dim: [..., n] -> [..., size*n]."""
+        if not self.is_real:
+            return t
+        t = t.contiguous()
+        out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t, group=self.group)
+        return out.movedim(0, -2).reshape(*t.shape[:-1], self.size * t.shape[-1])
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.is_real:
+            dist.broadcast(t, src=src, group=self.group)
+        return t
+
+    def broadcast_object(self, obj, src: int = 0):
+        if not self.is_real:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=src, group=self.group)
+        return box[0]
+
+    def all_gather_object(self, obj) -> List:
+        if not self.is_real:
+            return [obj]
+        out = [None] * self.size
+        dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+    def barrier(self):
+        if self.is_real:
+            dist.barrier(group=self.group)
+
+    def __repr__(self):
+        kind = "fake" if self.fake else ("local" if self.size == 1 else "rccl/gloo")
+        return f"TPGroup(rank={self.rank}, size={self.size}, {kind})"
+
+
+def _env_int(name: str, default: int) -> int:
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
+
+
+def initialize_distributed(timeout_s: int = 120, backend: Optional[str] = None):
+    """Initialise torch.distributed from torchrun env vars.
+
+    Returns ``(tp_group, rank, world_size)`` like the reference
+    (``dist.py:40``); ``tp_group`` is a :class:`TPGroup`.
+    """
+    rank = _env_int("RANK", 0)
+    world_size = _env_int("WORLD_SIZE", 1)
+    local_rank = _env_int("LOCAL_RANK", rank)
+
+    use_cuda = torch.cuda.is_available()
+    if use_cuda:
+        n = torch.cuda.device_count()
+        torch.cuda.set_device(local_rank % n)
+    if backend is None:
+        backend = "nccl" if use_cuda else "gloo"
+
+    if world_size == 1:
+        return TPGroup(0, 1), rank, world_size
+    if os.environ.get("DEBUG") == "1":
+        log.warning("DEBUG=1: fake process group, no collectives (numerically wrong by design)")
+        return TPGroup(rank, world_size, fake=True), rank, world_size
+
+    if not dist.is_initialized():
+        kwargs = dict(backend=backend, world_size=world_size, rank=rank, timeout=timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kwargs["device_id"] = torch.device("cuda", torch.cuda.current_device())
+        dist.init_process_group(**kwargs)
+    log.info("rank %d/%d initialised backend=%s", rank, world_size, backend)
+    return TPGroup(rank, world_size, group=dist.group.WORLD), rank, world_size
+
+
+# Reference-compatible alias (dist.py:40).
+def initialize_torch_distributed():
+    return initialize_distributed()

@@ -1,0 +1,104 @@
+"""End-to-end model/engine checks on the GPU: HIP forward vs the CPU fp32 reference forward,
+HIP-graph decode vs eager decode, and continuous batching determinism."""
+import pytest
+import torch
+
+from llmss_amd.engine import LLMEngine, SamplingParams
+from llmss_amd.models.config import get_preset
+from llmss_amd.models.decoder import DecoderLM, StepInput
+from llmss_amd.models.weights import random_weights
+
+pytestmark = pytest.mark.gpu
+
+
+def _to_gpu(w):
+    from llmss_amd.models.weights import Linear, LayerWeights, ModelWeights
+
+    def t(x, keep32=False):
+        if x is None:
+            return None
+        return x.to("cuda", torch.float32 if keep32 else torch.bfloat16).contiguous()
+
+    def lin(l):
+        return Linear(t(l.w), t(l.b), None, l.glu)
+
+    layers = [LayerWeights(t(L.ln1_w), t(L.ln1_b), t(L.ln2_w), t(L.ln2_b), lin(L.qkv), lin(L.o), lin(L.up), lin(L.down))
+              for L in w.layers]
+    return ModelWeights(t(w.wte), t(w.wpe), layers, t(w.lnf_w), t(w.lnf_b), lin(w.head),
+                        t(w.cos, True), t(w.sin, True))
+
+
+@pytest.mark.parametrize("name", ["tiny-gpt2", "tiny-gptj", "tiny-bigcode", "tiny-llama"])
+def test_forward_matches_reference(name):
+    over = {}
+    if name == "tiny-gptj":
+        over = dict(head_dim=64, hidden_size=256, num_heads=4, num_kv_heads=4, rotary_dim=16)
+    else:
+        over = dict(head_dim=64, hidden_size=256, num_heads=4, num_kv_heads=4 if name != "tiny-llama" else 2,
+                    rotary_dim=64 if name == "tiny-llama" else 0)
+        if name == "tiny-bigcode":
+            over["num_kv_heads"] = 1
+    cfg = get_preset(name, **over)
+    wc = random_weights(cfg, device="cpu", dtype=torch.float32, seed=1, std=0.05)
+    m_cpu = DecoderLM(cfg, wc)
+    m_gpu = DecoderLM(cfg, _to_gpu(wc))
+    T = 40
+    ids = torch.randint(0, cfg.vocab_size, (T,))
+    cu = torch.tensor([0, 25, T], dtype=torch.int32)
+    pos = torch.cat([torch.arange(25), torch.arange(T - 25)])
+    last = torch.tensor([24, T - 1])
+    kv_c = m_cpu.allocate_kv_cache(16, 16)
+    kv_g = m_gpu.allocate_kv_cache(16, 16)
+    slots = torch.arange(T)
+    ref = m_cpu(StepInput("prefill", ids, pos, slots, cu_seqlens=cu, max_seqlen=25, last_idx=last), kv_c)
+    out = m_gpu(StepInput("prefill", ids.cuda(), pos.cuda(), slots.cuda(), cu_seqlens=cu.cuda(), max_seqlen=25,
+                          last_idx=last.cuda()), kv_g)
+    V = cfg.vocab_size
+    err = (out[:, :V].float().cpu() - ref[:, :V]).abs().max().item()
+    assert err < 0.05 * max(1.0, ref.abs().max().item()), err
+    # single-sequence decode step after a prefill of 25 tokens
+    dec_ids = torch.randint(0, V, (1,))
+    kv_c = m_cpu.allocate_kv_cache(16, 16)
+    kv_g = m_gpu.allocate_kv_cache(16, 16)
+    ids1 = ids[:25]
+    m_cpu(StepInput("prefill", ids1, torch.arange(25), torch.arange(25), cu_seqlens=torch.tensor([0, 25], dtype=torch.int32),
+                    max_seqlen=25), kv_c)
+    m_gpu(StepInput("prefill", ids1.cuda(), torch.arange(25).cuda(), torch.arange(25).cuda(),
+                    cu_seqlens=torch.tensor([0, 25], dtype=torch.int32).cuda(), max_seqlen=25), kv_g)
+    bt = torch.tensor([[0, 1]], dtype=torch.int32)
+    ctx = torch.tensor([26], dtype=torch.int32)
+    d_in = dict(kind="decode", input_ids=dec_ids[:1], positions=torch.tensor([25]), slots=torch.tensor([25]),
+                block_tables=bt, ctx_lens=ctx, max_ctx=32)
+    ref = m_cpu(StepInput(**d_in), kv_c)
+    d_g = {k: (v.cuda() if torch.is_tensor(v) else v) for k, v in d_in.items()}
+    out = m_gpu(StepInput(**d_g), kv_g)
+    err = (out[:, :V].float().cpu() - ref[:, :V]).abs().max().item()
+    assert err < 0.05 * max(1.0, ref.abs().max().item()), err
+
+
+def test_engine_graph_vs_eager_and_batching():
+    cfg = get_preset("tiny-llama", hidden_size=256, num_heads=4, num_kv_heads=2, head_dim=64, rotary_dim=64,
+                     intermediate_size=512, max_position_embeddings=256)
+    w = random_weights(cfg, device="cuda", dtype=torch.bfloat16, seed=3, std=0.05)
+    m = DecoderLM(cfg, w)
+    prompts = [[int(x) for x in torch.randint(0, cfg.vocab_size, (n,))] for n in (5, 17, 33, 2, 60)]
+    sp = SamplingParams(max_new_tokens=24, is_greedy=True, ignore_eos=True)
+    e_graph = LLMEngine(m, max_num_seqs=8, block_size=16, use_graphs=True)
+    out_g = e_graph.generate(prompts, sp)
+    del e_graph
+    e_eager = LLMEngine(m, max_num_seqs=8, block_size=16, use_graphs=False)
+    out_e = e_eager.generate(prompts, sp)
+    assert out_g == out_e
+    # one-at-a-time == batched (continuous batching must not change greedy results)
+    # (prefill may use a different GEMM kernel for a lone prompt, so allow rare bf16 argmax flips)
+    singles = [e_eager.generate([p], sp)[0] for p in prompts]
+    agree = sum(a == b for s1, s2 in zip(singles, out_e) for a, b in zip(s1, s2)) / sum(len(s) for s in out_e)
+    assert agree > 0.8, agree
+    # sampled decoding is reproducible with fixed seeds
+    sps = [SamplingParams(max_new_tokens=16, temperature=0.8, top_k=20, top_p=0.9, seed=11 + i, ignore_eos=True)
+           for i in range(len(prompts))]
+    a = e_eager.generate(prompts, sps)
+    sps = [SamplingParams(max_new_tokens=16, temperature=0.8, top_k=20, top_p=0.9, seed=11 + i, ignore_eos=True)
+           for i in range(len(prompts))]
+    b = e_eager.generate(prompts, sps)
+    assert a == b

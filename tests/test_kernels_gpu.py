@@ -1,0 +1,174 @@
+"""Numerics of every gfx950 HIP kernel against the plain-PyTorch fp32 definitions
+(``llmss_amd/ops/reference.py``). Also asserts the native extension is what actually runs."""
+import math
+
+import pytest
+import torch
+
+from llmss_amd.ops import hip as H
+from llmss_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def rnd(*s, scale=1.0, dtype=torch.bfloat16):
+    return (torch.randn(*s, device=dev) * scale).to(dtype)
+
+
+def close(a, b, atol, rtol=0.02):
+    a, b = a.float(), b.float()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    assert bool((err <= tol).all()), f"max err {err.max().item():.4g} (max |ref| {b.abs().max().item():.3g})"
+
+
+def test_native_loaded():
+    lib = H.lib()
+    import llmss_amd
+
+    assert lib.__file__.startswith(llmss_amd.__path__[0])
+
+
+@pytest.mark.parametrize("T,Hd", [(1, 64), (7, 1600), (33, 4096), (5, 8192)])
+@pytest.mark.parametrize("rms", [False, True])
+def test_add_norm(T, Hd, rms):
+    torch.manual_seed(0)
+    x, r = rnd(T, Hd), rnd(T, Hd)
+    w, b = rnd(Hd, scale=0.5) + 1, (None if rms else rnd(Hd, scale=0.1))
+    r_ref = r.clone()
+    y, ro = H.add_norm(x, w, b, 1e-5, rms, residual=r)
+    y_ref, ro_ref = R.add_norm(x, w, b, 1e-5, rms, r_ref)
+    close(ro, ro_ref, 1e-2)
+    close(y, y_ref, 3e-2)
+    y2, _ = H.add_norm(x, w, b, 1e-5, rms)
+    y2_ref, _ = R.add_norm(x, w, b, 1e-5, rms)
+    close(y2, y2_ref, 3e-2)
+
+
+def test_embed():
+    torch.manual_seed(0)
+    wte, wpe = rnd(1000, 256), rnd(64, 256)
+    ids = torch.randint(0, 1000, (37,), device=dev)
+    pos = torch.randint(0, 64, (37,), device=dev)
+    close(H.embed(ids, wte), R.embed(ids, wte), 0)
+    close(H.embed(ids, wte, pos, wpe), R.embed(ids, wte, pos, wpe), 1e-2)
+
+
+@pytest.mark.parametrize("style,D,rot,nh,nkv", [("neox", 128, 128, 8, 2), ("gptj", 256, 64, 4, 4), ("neox", 64, 64, 4, 1)])
+def test_rope_cache(style, D, rot, nh, nkv):
+    torch.manual_seed(0)
+    T, bs, nb = 19, 16, 8
+    qkv = rnd(T, (nh + 2 * nkv) * D)
+    pos = torch.randint(0, 100, (T,), device=dev)
+    cos, sin = R.rope_tables(128, rot, 10000.0, dev)
+    kc = torch.zeros(nb, nkv, bs, D, dtype=torch.bfloat16, device=dev)
+    vc = torch.zeros_like(kc)
+    slots = torch.randperm(nb * bs, device=dev)[:T]
+    slots[3] = -1
+    q1, kc1, vc1 = qkv.clone(), kc.clone(), vc.clone()
+    H.rope_cache(q1, pos, cos, sin, kc1, vc1, slots, nh, nkv, D, rot, style)
+    q2, kc2, vc2 = qkv.clone(), kc.clone(), vc.clone()
+    R.rope_cache(q2, pos, cos, sin, kc2, vc2, slots, nh, nkv, D, rot, style)
+    close(q1, q2, 2e-2)
+    close(kc1, kc2, 2e-2)
+    close(vc1, vc2, 0)
+
+
+@pytest.mark.parametrize("D,nh,nkv", [(64, 4, 4), (128, 8, 2), (128, 16, 1), (256, 4, 4)])
+def test_attn_prefill(D, nh, nkv):
+    torch.manual_seed(0)
+    lens = [1, 70, 129, 5]
+    T = sum(lens)
+    qkv = rnd(T, (nh + 2 * nkv) * D)
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=dev)
+    sc = 1 / math.sqrt(D)
+    out = H.attn_prefill(qkv, cu, max(lens), nh, nkv, D, sc)
+    ref = R.attn_prefill(qkv.float(), cu.cpu(), nh, nkv, D, sc)
+    close(out, ref, 2e-2)
+
+
+@pytest.mark.parametrize("D,nh,nkv", [(64, 25, 25), (128, 32, 32), (128, 8, 1), (128, 64, 8), (256, 16, 16)])
+@pytest.mark.parametrize("B,maxctx", [(1, 1000), (6, 300)])
+def test_attn_decode(D, nh, nkv, B, maxctx):
+    torch.manual_seed(0)
+    bs = 16
+    maxb = (maxctx + bs - 1) // bs
+    nb = B * maxb + 3
+    kc, vc = rnd(nb, nkv, bs, D), rnd(nb, nkv, bs, D)
+    perm = torch.randperm(nb, device=dev)[: B * maxb].view(B, maxb).to(torch.int32)
+    ctx = torch.randint(1, maxctx + 1, (B,), device=dev, dtype=torch.int32)
+    ctx[0] = maxctx
+    q = rnd(B, (nh + 2 * nkv) * D)
+    sc = 1 / math.sqrt(D)
+    out = H.attn_decode(q, kc, vc, perm, ctx, nh, nkv, D, sc, maxctx)
+    ref = R.attn_decode(q.float(), kc.float(), vc.float(), perm, ctx, nh, nkv, D, sc)
+    close(out, ref, 2e-2)
+    out1 = H.attn_decode(q, kc, vc, perm, ctx, nh, nkv, D, sc, maxctx, splits=(1, maxb * bs))
+    close(out1, ref, 2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 33, 64, 65, 200, 512])
+@pytest.mark.parametrize("N,K", [(4800, 1600), (1376 * 2, 4096), (4096, 1376), (256, 64)])
+def test_gemm(M, N, K):
+    torch.manual_seed(0)
+    x, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
+    b = rnd(N, scale=0.1)
+    ref = R.linear(x.float(), w.float(), b.float())
+    close(H.linear(x, w, b), ref, 2e-2)
+    close(H.linear(x, w, b, act="gelu_tanh"), R.linear(x.float(), w.float(), b.float(), act="gelu_tanh"), 2e-2)
+    if N % 32 == 0:
+        close(H.linear(x, w, None, glu=True), R.linear(x.float(), w.float(), None, glu=True), 2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 8, 64, 100])
+def test_gemm_fp8(M):
+    torch.manual_seed(0)
+    N, K = 1024, 2048
+    x, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
+    q, s = H.quant_fp8_rows(w)
+    q_ref, s_ref = R.quant_fp8_rows(w)
+    close(s, s_ref, 1e-6)
+    assert (q.cpu().view(torch.float8_e4m3fn).float() - q_ref.cpu().view(torch.float8_e4m3fn).float()).abs().max() <= 0.0626 * 448
+    ref = R.linear(x.float(), q, None, w_scale=s)
+    close(H.linear(x, q, None, w_scale=s), ref, 2e-2)
+
+
+def test_sample_greedy_and_filters():
+    torch.manual_seed(0)
+    B, V = 8, 50257
+    logits = rnd(B, V + 15, scale=3.0)
+    temp = torch.zeros(B, device=dev)
+    topk = torch.zeros(B, dtype=torch.int32, device=dev)
+    topp = torch.ones(B, device=dev)
+    seeds = torch.arange(B, dtype=torch.int64, device=dev)
+    out = H.sample(logits, temp, topk, topp, seeds, vocab=V)
+    assert torch.equal(out, logits[:, :V].float().argmax(-1))
+    # top-k = 3: samples must lie in the top-3 set
+    temp.fill_(1.0)
+    topk.fill_(3)
+    top3 = logits[:, :V].float().topk(3, -1).indices
+    for s in range(20):
+        seeds.fill_(s * 7919)
+        o = H.sample(logits, temp, topk, topp, seeds + torch.arange(B, device=dev), vocab=V)
+        assert bool((top3 == o[:, None]).any(-1).all())
+    # top-p tiny -> argmax
+    topk.fill_(0)
+    topp.fill_(1e-6)
+    o = H.sample(logits, temp, topk, topp, seeds, vocab=V)
+    assert torch.equal(o, logits[:, :V].float().argmax(-1))
+
+
+def test_sample_distribution():
+    torch.manual_seed(0)
+    V = 8
+    base = torch.tensor([[2.0, 1.0, 0.5, 0.0, -1.0, -2.0, -3.0, 0.2]], device=dev)
+    logits = base.repeat(4096, 1).to(torch.bfloat16)
+    temp = torch.full((4096,), 0.7, device=dev)
+    topk = torch.zeros(4096, dtype=torch.int32, device=dev)
+    topp = torch.ones(4096, device=dev)
+    seeds = torch.arange(4096, dtype=torch.int64, device=dev) * 1000003
+    o = H.sample(logits, temp, topk, topp, seeds)
+    freq = torch.bincount(o, minlength=V).float() / 4096
+    p = torch.softmax(logits[0].float() / 0.7, -1)
+    assert (freq - p).abs().max() < 0.03, (freq, p)
