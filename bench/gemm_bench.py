@@ -1,0 +1,96 @@
+"""GEMM microbenchmark on decode/prefill shapes: our gfx950 kernels vs torch.matmul (hipBLASLt).
+
+Weights are rotated through enough copies (> 2x the 256 MiB Infinity Cache) that every call
+streams its weights from HBM, as in a real decode step. Reports time per call and the effective
+weight bandwidth (weight bytes / time) or TFLOP/s for large M.
+
+usage: python bench/gemm_bench.py [--sweep] [--m 1,16,64] [--shapes llama7b]
+"""
+import argparse
+import itertools
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from llmss_amd.ops import hip as H  # noqa: E402
+
+SHAPES = {
+    "llama7b": [("qkv", 12288, 4096), ("o", 4096, 4096), ("gate_up", 22016, 4096), ("down", 4096, 11008),
+                ("head", 32000, 4096)],
+    "llama7b_tp8": [("qkv", 1536, 4096), ("o", 4096, 512), ("gate_up", 2752, 4096), ("down", 4096, 1376)],
+    "gpt2xl": [("qkv", 4800, 1600), ("o", 1600, 1600), ("up", 6400, 1600), ("down", 1600, 6400)],
+    "llama70b_tp8": [("qkv", 1280, 8192), ("o", 8192, 1024), ("gate_up", 7168, 8192), ("down", 8192, 3584)],
+}
+
+
+def timeit(fn, iters=50):
+    for _ in range(5):
+        fn(0)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for i in range(iters):
+        fn(i)
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", default="1,16,32,64,128,256,2048")
+    ap.add_argument("--shapes", default="llama7b")
+    ap.add_argument("--sweep", action="store_true")
+    ap.add_argument("--fp8", action="store_true")
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    out = []
+    for sname in a.shapes.split(","):
+        for name, N, K in SHAPES[sname]:
+            wbytes = N * K * (1 if a.fp8 else 2)
+            ncopy = max(2, int(600e6 // wbytes) + 1)
+            ws = [(torch.randn(N, K, device=dev) * K ** -0.5).to(torch.bfloat16) for _ in range(ncopy)]
+            scales = None
+            if a.fp8:
+                qs = [H.quant_fp8_rows(w) for w in ws]
+                ws = [q for q, _ in qs]
+                scales = [s for _, s in qs]
+            for M in [int(m) for m in a.m.split(",")]:
+                x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+                y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+                res = {"shape": sname, "layer": name, "M": M, "N": N, "K": K}
+                if not a.fp8:
+                    t = timeit(lambda i: torch.matmul(x, ws[i % ncopy].t(), out=y))
+                    res["hipblaslt_us"] = round(t, 2)
+                cfgs = [(0, 0)]
+                if a.sweep and M <= 128:
+                    cfgs += list(itertools.product([1, 2, 4], [1, 2, 4, 8]))
+                best = None
+                for nt, sp in cfgs:
+                    try:
+                        t = timeit(lambda i: H.linear(x, ws[i % ncopy], None, w_scale=scales[i % ncopy] if scales else None,
+                                                      out=y, nt_hint=nt, split_hint=sp))
+                    except Exception as e:  # noqa: BLE001
+                        continue
+                    key = "ours_us" if (nt, sp) == (0, 0) else f"nt{nt}_s{sp}_us"
+                    res[key] = round(t, 2)
+                    if best is None or t < best[0]:
+                        best = (t, nt, sp)
+                res["best"] = {"us": round(best[0], 2), "nt": best[1], "split": best[2]}
+                t = res["ours_us"]
+                res["ours_TBps"] = round(wbytes / t / 1e6, 3)
+                res["ours_TFLOPs"] = round(2 * M * N * K / t / 1e6, 1)
+                if "hipblaslt_us" in res:
+                    res["hipblaslt_TBps"] = round(wbytes / res["hipblaslt_us"] / 1e6, 3)
+                    res["hipblaslt_TFLOPs"] = round(2 * M * N * K / res["hipblaslt_us"] / 1e6, 1)
+                print(json.dumps(res), flush=True)
+                out.append(res)
+            del ws
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

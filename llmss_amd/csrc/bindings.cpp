@@ -26,7 +26,7 @@ void launch_attn_prefill(const void* qkv, int64_t row_stride, const void* cu_seq
                          hipStream_t st);
 void launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_fp8, const void* w_scale,
                  const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace,
-                 int64_t ws_bytes, hipStream_t st);
+                 int64_t ws_bytes, int nt_hint, int split_hint, hipStream_t st);
 int gemm_skinny_splitk(int M, int N, int K);
 void launch_sample(const void* logits, int64_t ld, bool fp32_logits, int B, int V, const void* temperature,
                    const void* top_k, const void* top_p, const void* seeds, void* out, void* out2, hipStream_t st);
@@ -66,8 +66,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("gemm", [](uintptr_t x, int64_t ldx, uintptr_t w, int64_t ldw, bool fp8, uintptr_t ws, uintptr_t bias,
                    uintptr_t y, int64_t ldy, int M, int N, int K, int act, bool glu, uintptr_t work, int64_t wbytes,
-                   uintptr_t st) {
-    launch_gemm(CP(x), ldx, CP(w), ldw, fp8, CP(ws), CP(bias), P(y), ldy, M, N, K, act, glu, P(work), wbytes, S(st));
+                   int nt_hint, int split_hint, uintptr_t st) {
+    launch_gemm(CP(x), ldx, CP(w), ldw, fp8, CP(ws), CP(bias), P(y), ldy, M, N, K, act, glu, P(work), wbytes, nt_hint,
+                split_hint, S(st));
   });
   m.def("gemm_skinny_splitk", &gemm_skinny_splitk);
   m.def("sample", [](uintptr_t logits, int64_t ld, bool fp32, int B, int V, uintptr_t temp, uintptr_t topk,

@@ -47,24 +47,114 @@ __device__ __forceinline__ float epi_value(float v, int n, const float* wscale, 
 }
 
 // -------------------------------------------------------------------------------------------
-// skinny GEMM (M <= 64)
-// grid (ceil(N / (16*NT)), SPLITK), block 256 = 4 waves splitting the workgroup's K range.
+// weight-streaming GEMM (M <= 128: decode / small batches)
+// grid (ceil(N / (64*NT)), SPLITK), block 256 = 4 waves; wave w owns NT 16-column tiles.
+// Per K-chunk of KC: X[0:16*MT, chunk] is staged ONCE per workgroup into LDS by 16-byte
+// global_load_lds (lane-linear image, XOR swizzle applied on the source address: rule 21), and
+// shared by the 4 waves; each wave streams its W rows straight into VGPRs (non-temporal: read
+// once per step), 32 B per lane = a full 128-B line per 4 lanes. W for chunk c+1 and X for chunk
+// c+1 are issued before the MFMAs of chunk c (register ring of 2 named buffers, static indexing).
 // -------------------------------------------------------------------------------------------
-template <int MT, int NT, int U, bool FP8W>
-__global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restrict__ X, int64_t ldx,
-                                                          const void* __restrict__ Wv, int64_t ldw,
-                                                          const float* __restrict__ wscale,
-                                                          const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
-                                                          int64_t ldy, float* __restrict__ part, int M, int N, int K,
-                                                          int act, int glu) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+template <int MT, int NT, int KC, bool FP8W>
+struct StreamCfg {
+  static constexpr int ROWS = MT * 16;
+  static constexpr int RB = KC * 2;                     // LDS row bytes
+  static constexpr int XBYTES = ROWS * RB;              // one X chunk
+  static constexpr int NG = KC / 64;                    // 64-k groups per chunk
+  static constexpr int WV = FP8W ? 1 : 2;               // u32x4 per lane per (nt, group)
+  static constexpr int SW = (KC / 8 - 1) < 15 ? (KC / 8 - 1) : 15;  // swizzle mask (chunks)
+  static constexpr int XINST = XBYTES / 1024 / 4;       // glds per wave per chunk
+  static_assert(XBYTES % 4096 == 0, "X chunk must be a multiple of 4 KiB (4 waves x 1 KiB)");
+};
+
+template <int MT, int NT, int KC, bool FP8W>
+__device__ __forceinline__ void stream_stage_x(const bf16_t* __restrict__ X, int64_t ldx, int M, int K, int kc0,
+                                               char* xbuf, int w, int lane) {
+  using C = StreamCfg<MT, NT, KC, FP8W>;
+#pragma unroll
+  for (int i = 0; i < C::XINST; ++i) {
+    const int inst = i * 4 + w;
+    const int o = inst * 1024 + lane * 16;
+    const int row = o / C::RB;
+    const int pc = (o % C::RB) >> 4;
+    const int gc = pc ^ (row & C::SW);
+    const int k = min(kc0 + gc * 8, K - 8);
+    const bf16_t* src = X + (int64_t)min(row, M - 1) * ldx + k;
+    __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(xbuf + inst * 1024), 16, 0, 0);
+  }
+}
+
+template <int MT, int NT, int KC, bool FP8W>
+__device__ __forceinline__ void stream_load_w(const char* const (&wrow)[NT], int kc0, int K, int g,
+                                              u32x4 (&wr)[NT][KC / 64][FP8W ? 1 : 2]) {
+  constexpr int WB = FP8W ? 1 : 2;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int q = 0; q < KC / 64; ++q) {
+      int k = kc0 + 64 * q + 16 * g;
+      k = k < K ? k : 0;  // tail lanes read a valid address; their fragments are zeroed at use
+      const u32x4* p = reinterpret_cast<const u32x4*>(wrow[nt] + (int64_t)k * WB);
+      wr[nt][q][0] = __builtin_nontemporal_load(p);
+      if constexpr (!FP8W) wr[nt][q][1] = __builtin_nontemporal_load(p + 1);
+    }
+}
+
+// 8 fp8-e4m3 (two dwords) -> one bf16x8 fragment
+__device__ __forceinline__ s16x8 fp8x8_to_bf16(unsigned w0, unsigned w1) {
+  const f32x2 a = __builtin_amdgcn_cvt_pk_f32_fp8(w0, false), b = __builtin_amdgcn_cvt_pk_f32_fp8(w0, true);
+  const f32x2 c = __builtin_amdgcn_cvt_pk_f32_fp8(w1, false), d = __builtin_amdgcn_cvt_pk_f32_fp8(w1, true);
+  return s16x8{(short)f2bf(a[0]), (short)f2bf(a[1]), (short)f2bf(b[0]), (short)f2bf(b[1]),
+               (short)f2bf(c[0]), (short)f2bf(c[1]), (short)f2bf(d[0]), (short)f2bf(d[1])};
+}
+
+template <int MT, int NT, int KC, bool FP8W, bool TAIL>
+__device__ __forceinline__ void stream_compute(const char* xbuf, const u32x4 (&wr)[NT][KC / 64][FP8W ? 1 : 2],
+                                               f32x4 (&acc)[MT][NT], int kc0, int K, int li, int g) {
+  using C = StreamCfg<MT, NT, KC, FP8W>;
+  const s16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int q = 0; q < C::NG; ++q) {
+    const bool ok = !TAIL || (kc0 + 64 * q + 16 * g < K);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      s16x8 b[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        if constexpr (FP8W) b[nt] = fp8x8_to_bf16(wr[nt][q][0][2 * s], wr[nt][q][0][2 * s + 1]);
+        else b[nt] = *reinterpret_cast<const s16x8*>(&wr[nt][q][s]);
+        if (TAIL && !ok) b[nt] = z;
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int r = mt * 16 + li;
+        const int c = 8 * q + 2 * g + s;
+        s16x8 a = *reinterpret_cast<const s16x8*>(xbuf + r * C::RB + ((c ^ (r & C::SW)) << 4));
+        if (TAIL && !ok) a = z;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[nt], acc[mt][nt], 0, 0, 0);
+      }
+    }
+  }
+}
+
+template <int MT, int NT, int KC, bool FP8W>
+__global__ __launch_bounds__(256, 2) void gemm_stream_kernel(const bf16_t* __restrict__ X, int64_t ldx,
+                                                             const void* __restrict__ Wv, int64_t ldw,
+                                                             const float* __restrict__ wscale,
+                                                             const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
+                                                             int64_t ldy, float* __restrict__ part, int M, int N, int K,
+                                                             int act, int glu) {
+  using C = StreamCfg<MT, NT, KC, FP8W>;
+  __shared__ __attribute__((aligned(16))) char xs[2 * C::XBYTES];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int li = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * (16 * NT);
+  const int n0 = blockIdx.x * (64 * NT) + w * (16 * NT);
   const int split = blockIdx.y, nsplit = gridDim.y;
-  // K in groups of 64; slices = nsplit * 4 waves
-  const int ngrp = (K + 63) >> 6;
-  const int nslice = nsplit * 4, sl = split * 4 + w;
-  const int gb = (int)((int64_t)ngrp * sl / nslice), ge = (int)((int64_t)ngrp * (sl + 1) / nslice);
+  const int nck = (K + KC - 1) / KC;
+  const int cb = (int)((int64_t)nck * split / nsplit), ce = (int)((int64_t)nck * (split + 1) / nsplit);
 
   f32x4 acc[MT][NT];
 #pragma unroll
@@ -72,84 +162,43 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const bf16_t* __restri
 #pragma unroll
     for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // per-lane row pointers
-  const bf16_t* xrow[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) xrow[mt] = X + (int64_t)min(mt * 16 + li, M - 1) * ldx;
+  constexpr int WB = FP8W ? 1 : 2;
   const char* wrow[NT];
-  constexpr int WB = FP8W ? 1 : 2;  // bytes per weight element
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
-    wrow[nt] = (const char*)Wv + ((int64_t)min(n0 + nt * 16 + li, N - 1) * ldw) * WB;
+    wrow[nt] = (const char*)Wv + ((int64_t)min(n0 + nt * 16 + li, N - 1) * ldw + 16 * g) * WB;
 
-  for (int gi = gb; gi < ge; gi += U) {
-    u16x8 xa[U][MT][2];
-    u32x4 wa[U][NT][FP8W ? 1 : 2];
-    bool kok[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int gg = gi + u;
-      // k < K is uniform per 16-lane group (K % 16 == 0); gg < ge is wave-uniform
-      kok[u] = (gg < ge) && (gg * 64 + 16 * g < K);
-      const int ko = kok[u] ? gg * 64 + 16 * g : 0;  // masked lanes read k 0..15 (K >= 16)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        xa[u][mt][0] = *reinterpret_cast<const u16x8*>(xrow[mt] + ko);
-        xa[u][mt][1] = *reinterpret_cast<const u16x8*>(xrow[mt] + ko + 8);
-      }
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const u32x4* p = reinterpret_cast<const u32x4*>(wrow[nt] + (int64_t)ko * WB);
-        wa[u][nt][0] = __builtin_nontemporal_load(p);
-        if constexpr (!FP8W) wa[u][nt][1] = __builtin_nontemporal_load(p + 1);
-      }
+  u32x4 wA[NT][KC / 64][FP8W ? 1 : 2], wB[NT][KC / 64][FP8W ? 1 : 2];
+  const bool tail_k = (K % KC) != 0;
+  if (cb < ce) {
+    stream_stage_x<MT, NT, KC, FP8W>(X, ldx, M, K, cb * KC, xs, w, lane);
+    stream_load_w<MT, NT, KC, FP8W>(wrow, cb * KC, K, g, wA);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int c = cb; c < ce; c += 2) {
+    // ---- even chunk: compute from wA / buffer 0, prefetch chunk c+1 into wB / buffer 1
+    if (c + 1 < ce) {
+      stream_stage_x<MT, NT, KC, FP8W>(X, ldx, M, K, (c + 1) * KC, xs + C::XBYTES, w, lane);
+      stream_load_w<MT, NT, KC, FP8W>(wrow, (c + 1) * KC, K, g, wB);
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (gi + u >= ge) break;  // wave-uniform
-      const s16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        s16x8 b0, b1;
-        if constexpr (FP8W) {
-          fp8x16_to_bf16(wa[u][nt][0], b0, b1);
-        } else {
-          b0 = *reinterpret_cast<const s16x8*>(&wa[u][nt][0]);
-          b1 = *reinterpret_cast<const s16x8*>(&wa[u][nt][1]);
-        }
-        b0 = kok[u] ? b0 : z;
-        b1 = kok[u] ? b1 : z;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          s16x8 a0 = *reinterpret_cast<const s16x8*>(&xa[u][mt][0]);
-          s16x8 a1 = *reinterpret_cast<const s16x8*>(&xa[u][mt][1]);
-          a0 = kok[u] ? a0 : z;
-          a1 = kok[u] ? a1 : z;
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc[mt][nt], 0, 0, 0);
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc[mt][nt], 0, 0, 0);
-        }
-      }
+    if (tail_k && c == nck - 1) stream_compute<MT, NT, KC, FP8W, true>(xs, wA, acc, c * KC, K, li, g);
+    else stream_compute<MT, NT, KC, FP8W, false>(xs, wA, acc, c * KC, K, li, g);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (c + 1 >= ce) break;
+    // ---- odd chunk: compute from wB / buffer 1, prefetch chunk c+2 into wA / buffer 0
+    if (c + 2 < ce) {
+      stream_stage_x<MT, NT, KC, FP8W>(X, ldx, M, K, (c + 2) * KC, xs, w, lane);
+      stream_load_w<MT, NT, KC, FP8W>(wrow, (c + 2) * KC, K, g, wA);
     }
+    if (tail_k && c + 1 == nck - 1) stream_compute<MT, NT, KC, FP8W, true>(xs + C::XBYTES, wB, acc, (c + 1) * KC, K, li, g);
+    else stream_compute<MT, NT, KC, FP8W, false>(xs + C::XBYTES, wB, acc, (c + 1) * KC, K, li, g);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
 
-  // ---- reduce the 4 K-slices of the workgroup through LDS --------------------------------
-  __shared__ f32x4 red[3][MT][NT][64];
-  if (w > 0) {
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) red[w - 1][mt][nt][lane] = acc[mt][nt];
-  }
-  __syncthreads();
-  if (w != 0) return;
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-      for (int r = 0; r < 3; ++r) acc[mt][nt] += red[r][mt][nt][lane];
-
-  // ---- epilogue --------------------------------------------------------------------------
+  // ---- epilogue (C layout: col = lane&15 -> n, row = 4*(lane>>4)+i -> m) --------------------
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
@@ -321,35 +370,62 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
 // -------------------------------------------------------------------------------------------
 // host dispatch
 // -------------------------------------------------------------------------------------------
-template <int MT, int NT, int U, bool FP8W>
-static void launch_skinny_t(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const float* ws, const bf16_t* bias,
+template <int MT, int NT, int KC, bool FP8W>
+static void launch_stream_t(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const float* ws, const bf16_t* bias,
                             bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu, int splitk,
                             hipStream_t st) {
-  dim3 grid((N + 16 * NT - 1) / (16 * NT), splitk);
-  gemm_skinny_kernel<MT, NT, U, FP8W><<<grid, 256, 0, st>>>(X, ldx, W, ldw, ws, bias, Y, ldy, part, M, N, K, act, glu);
+  dim3 grid((N + 64 * NT - 1) / (64 * NT), splitk);
+  gemm_stream_kernel<MT, NT, KC, FP8W><<<grid, 256, 0, st>>>(X, ldx, W, ldw, ws, bias, Y, ldy, part, M, N, K, act, glu);
   HIP_CHECK_LAUNCH();
 }
 
-template <int MT, bool FP8W>
-static void launch_skinny_m(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const float* ws,
-                            const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act,
-                            int glu, int splitk, hipStream_t st) {
-  constexpr int U = MT <= 1 ? 4 : 2;
-  launch_skinny_t<MT, 2, U, FP8W>(X, ldx, W, ldw, ws, bias, Y, ldy, part, M, N, K, act, glu, splitk, st);
+template <bool FP8W>
+static void launch_stream(int mt, int nt, const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const float* ws,
+                          const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
+                          int splitk, hipStream_t st) {
+#define LS(MT_, NT_, KC_) \
+  launch_stream_t<MT_, NT_, KC_, FP8W>(X, ldx, W, ldw, ws, bias, Y, ldy, part, M, N, K, act, glu, splitk, st)
+  // only register-feasible (spill-free at 2 waves/SIMD) instantiations
+  if constexpr (FP8W) {
+    if (nt >= 2) {
+      if (mt == 1) LS(1, 2, 256); else if (mt == 2) LS(2, 2, 128); else if (mt <= 4) LS(4, 2, 128); else LS(8, 2, 64);
+    } else {
+      if (mt == 1) LS(1, 1, 256); else if (mt == 2) LS(2, 1, 256); else if (mt <= 4) LS(4, 1, 256); else LS(8, 1, 128);
+    }
+  } else {
+    if (nt >= 4 && mt <= 2) {
+      if (mt == 1) LS(1, 4, 128); else LS(2, 4, 128);
+    } else if (nt >= 2) {
+      if (mt == 1) LS(1, 2, 256); else if (mt == 2) LS(2, 2, 256); else if (mt <= 4) LS(4, 2, 256); else LS(8, 2, 64);
+    } else {
+      if (mt == 1) LS(1, 1, 256); else if (mt == 2) LS(2, 1, 256); else if (mt <= 4) LS(4, 1, 256); else LS(8, 1, 128);
+    }
+  }
+#undef LS
 }
 
-// Number of K-splits across workgroups: enough workgroups to put >= 2 on every CU.
-int gemm_skinny_splitk(int M, int N, int K) {
-  const int nblk = (N + 31) / 32;
+// Tile/split choice for the streaming kernel: columns per workgroup and K splits such that the
+// grid reaches ~2 workgroups per CU (256 CUs) without splitting K below 4 chunks per slice.
+void gemm_stream_plan(int M, int N, int K, int* nt_out, int* splitk_out) {
+  int nt = (N >= 16384) ? 2 : 1;
+  const int nblk = (N + 64 * nt - 1) / (64 * nt);
+  const int kc = M > 64 ? 128 : 256;
+  const int nck = (K + kc - 1) / kc;
   int s = 1;
-  while (nblk * s < 512 && s < 16 && (K / 64) / (8 * s) >= 2) s *= 2;
-  (void)M;
+  while (nblk * s < 512 && s < 16 && nck / (2 * s) >= 4) s *= 2;
+  *nt_out = nt;
+  *splitk_out = s;
+}
+
+int gemm_skinny_splitk(int M, int N, int K) {
+  int nt, s;
+  gemm_stream_plan(M, N, K, &nt, &s);
   return s;
 }
 
 void launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_fp8, const void* w_scale,
                  const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace,
-                 int64_t ws_bytes, hipStream_t st) {
+                 int64_t ws_bytes, int nt_hint, int split_hint, hipStream_t st) {
   if (M == 0 || N == 0) return;
   if (K % 16) throw std::runtime_error("gemm: K must be a multiple of 16");
   if (glu && (N % 32)) throw std::runtime_error("gemm: glu needs N % 32 == 0");
@@ -358,29 +434,27 @@ void launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_
   auto Y = (bf16_t*)y;
   auto WS = (const float*)w_scale;
   const int g = glu ? 1 : 0;
-  if (M <= 64 || w_fp8) {
-    if (M > 64) {  // fp8 weights with many rows: loop over 64-row panels (prefill with fp8 weights)
-      for (int m0 = 0; m0 < M; m0 += 64) {
-        const int mm = std::min(64, M - m0);
-        launch_gemm((const bf16_t*)x + m0 * ldx, ldx, w, ldw, w_fp8, w_scale, bias,
-                    (bf16_t*)y + m0 * ldy, ldy, mm, N, K, act, glu, workspace, ws_bytes, st);
+  const bool stream = M <= 128 || w_fp8;
+  if (stream) {
+    if (M > 128) {  // fp8 weights with many rows (prefill): 128-row panels through the streaming kernel
+      for (int m0 = 0; m0 < M; m0 += 128) {
+        const int mm = std::min(128, M - m0);
+        launch_gemm((const bf16_t*)x + m0 * ldx, ldx, w, ldw, w_fp8, w_scale, bias, (bf16_t*)y + m0 * ldy, ldy, mm, N,
+                    K, act, glu, workspace, ws_bytes, nt_hint, split_hint, st);
       }
       return;
     }
-    int splitk = gemm_skinny_splitk(M, N, K);
+    int nt, splitk;
+    gemm_stream_plan(M, N, K, &nt, &splitk);
+    if (nt_hint > 0) nt = nt_hint;
+    if (split_hint > 0) splitk = split_hint;
+    if (glu && nt < 2) nt = 2;  // the SwiGLU epilogue pairs (gate, up) 16-column tiles inside a wave
     if ((int64_t)splitk * M * N * 4 > ws_bytes) splitk = 1;
     float* part = splitk > 1 ? (float*)workspace : nullptr;
     const int mt = (M + 15) / 16;
     const int act_k = splitk > 1 ? 0 : act, glu_k = splitk > 1 ? 0 : g;
-    if (w_fp8) {
-      if (mt == 1) launch_skinny_m<1, true>(X, ldx, w, ldw, WS, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
-      else if (mt == 2) launch_skinny_m<2, true>(X, ldx, w, ldw, WS, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
-      else launch_skinny_m<4, true>(X, ldx, w, ldw, WS, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
-    } else {
-      if (mt == 1) launch_skinny_m<1, false>(X, ldx, w, ldw, nullptr, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
-      else if (mt == 2) launch_skinny_m<2, false>(X, ldx, w, ldw, nullptr, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
-      else launch_skinny_m<4, false>(X, ldx, w, ldw, nullptr, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
-    }
+    if (w_fp8) launch_stream<true>(mt, nt, X, ldx, w, ldw, WS, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
+    else launch_stream<false>(mt, nt, X, ldx, w, ldw, nullptr, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
     if (splitk > 1) {
       const int nout = glu ? N / 2 : N;
       dim3 grid(std::min((nout + 255) / 256, 64), M);

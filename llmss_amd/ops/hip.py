@@ -138,11 +138,14 @@ class DecodeWorkspace:
 
     def get(self, B, nh, nsplit, D, device):
         need = B * nh * nsplit
-        if self.po is None or self.po.numel() < need * D or self.po.device != device:
+        if (self.po is None or self.po.numel() < need * D or self.pml.numel() < need * 2
+                or self.po.device != device):
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("decode workspace must be allocated before graph capture")
-            self.po = torch.empty(need * D, dtype=torch.float32, device=device)
-            self.pml = torch.empty(need * 2, dtype=torch.float32, device=device)
+            n_o = max(need * D, 0 if self.po is None else self.po.numel())
+            n_ml = max(need * 2, 0 if self.pml is None else self.pml.numel())
+            self.po = torch.empty(n_o, dtype=torch.float32, device=device)
+            self.pml = torch.empty(n_ml, dtype=torch.float32, device=device)
         return self.po, self.pml
 
 
@@ -209,7 +212,7 @@ def reserve_workspace(device, gemm_bytes: int = 64 << 20, decode_rows: int = 0, 
 _ACT = {"none": 0, None: 0, "gelu_tanh": 1, "gelu": 2, "relu": 3}
 
 
-def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None):
+def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hint=0, split_hint=0):
     M, K = x.shape
     _bf16_rows(x, "x")
     fp8 = w_scale is not None
@@ -231,7 +234,7 @@ def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None):
     _bf16_rows(y, "out", nout)
     ws = _GEMM_WS.get(64 << 20, x.device)
     lib().gemm(x.data_ptr(), x.stride(0), w.data_ptr(), K, fp8, _ptr(w_scale), _ptr(bias), y.data_ptr(), y.stride(0),
-               M, N, K, _ACT[act], bool(glu), ws.data_ptr(), ws.numel() * 4, _stream())
+               M, N, K, _ACT[act], bool(glu), ws.data_ptr(), ws.numel() * 4, int(nt_hint), int(split_hint), _stream())
     return y
 
 

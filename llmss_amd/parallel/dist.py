@@ -56,8 +56,9 @@ class TPGroup:
         if not self.is_real:
             return t
         t = t.contiguous()
-        out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        out = torch.empty((self.size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(out, t, group=self.group)
+        out = out.view((self.size,) + tuple(t.shape))
         return out.movedim(0, -2).reshape(*t.shape[:-1], self.size * t.shape[-1])
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:

@@ -19,6 +19,7 @@ for s in $STAGES; do
     kernels) step kernels 900 python -m pytest tests/test_kernels_gpu.py -q -rf --timeout 300; rc=$? ;;
     engine) step engine 900 python -m pytest tests/test_engine_gpu.py -q -rf --timeout 300; rc=$? ;;
     gputests) step gputests 1200 python -m pytest tests -m gpu -q -rf --timeout 600; rc=$? ;;
+    gemm) step gemm 900 python bench/gemm_bench.py ${GEMM_ARGS:-}; rc=$? ;;
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()"; rc=$? ;;
     bench) step bench 900 python bench.py ${BENCH_ARGS:-}; rc=$? ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null;

@@ -129,7 +129,8 @@ def test_gemm_fp8(M):
     q, s = H.quant_fp8_rows(w)
     q_ref, s_ref = R.quant_fp8_rows(w)
     close(s, s_ref, 1e-6)
-    assert (q.cpu().view(torch.float8_e4m3fn).float() - q_ref.cpu().view(torch.float8_e4m3fn).float()).abs().max() <= 0.0626 * 448
+    a, b = q.cpu().view(torch.float8_e4m3fn).float(), q_ref.cpu().view(torch.float8_e4m3fn).float()
+    assert ((a - b).abs() <= 0.125 * b.abs() + 2 ** -9).all()  # at most one e4m3 ulp of rounding difference
     ref = R.linear(x.float(), q, None, w_scale=s)
     close(H.linear(x, q, None, w_scale=s), ref, 2e-2)
 
@@ -156,7 +157,8 @@ def test_sample_greedy_and_filters():
     topk.fill_(0)
     topp.fill_(1e-6)
     o = H.sample(logits, temp, topk, topp, seeds, vocab=V)
-    assert torch.equal(o, logits[:, :V].float().argmax(-1))
+    lf = logits[:, :V].float()
+    assert torch.equal(lf.gather(1, o[:, None])[:, 0], lf.max(-1).values)  # a max-logit token (bf16 ties)
 
 
 def test_sample_distribution():

@@ -1,0 +1,89 @@
+"""Native C++ runtime: block allocator, continuous-batching scheduler, safetensors reader."""
+import numpy as np
+import pytest
+import torch
+
+
+def test_block_allocator(native):
+    a = native.BlockAllocator(8, 16)
+    bs = a.allocate_n(5)
+    assert len(set(bs)) == 5 and a.num_free() == 3
+    a.fork(bs[0])
+    a.free(bs[0])
+    assert a.ref_count(bs[0]) == 1 and a.num_free() == 3
+    a.free_all(bs)
+    assert a.num_free() == 8
+    with pytest.raises(RuntimeError):
+        a.free(bs[1])
+    with pytest.raises(RuntimeError):
+        a.allocate_n(9)
+
+
+def test_scheduler_prefill_then_decode(native):
+    s = native.Scheduler(num_blocks=64, block_size=4, max_num_seqs=8, max_batched_tokens=64, max_model_len=64)
+    s.add(10, 5, 3)
+    s.add(11, 9, 3)
+    b = s.schedule()
+    assert b.kind == 1 and b.ids.tolist() == [10, 11] and b.query_lens.tolist() == [5, 9]
+    assert b.positions.tolist() == list(range(5)) + list(range(9))
+    bt = b.block_table
+    slots = b.slots.tolist()
+    # slots follow the block table
+    assert slots[:5] == [bt[0, p // 4] * 4 + p % 4 for p in range(5)]
+    s.on_token(10, False)
+    s.on_token(11, False)
+    b = s.schedule()
+    assert b.kind == 2 and b.ctx_lens.tolist() == [6, 10] and b.positions.tolist() == [5, 9]
+    s.on_token(10, True)  # finished early (eos)
+    s.on_token(11, False)
+    b = s.schedule()
+    assert b.ids.tolist() == [11]
+    s.on_token(11, False)  # third token -> length limit
+    assert not s.has_work()
+    assert s.num_free_blocks() == 64
+
+
+def test_scheduler_budget_and_preemption(native):
+    s = native.Scheduler(num_blocks=6, block_size=4, max_num_seqs=4, max_batched_tokens=16, max_model_len=32)
+    s.add(1, 8, 16)
+    s.add(2, 8, 16)
+    s.add(3, 8, 16)
+    b = s.schedule()
+    assert b.ids.tolist() == [1, 2]  # token budget 16
+    for i in b.ids.tolist():
+        s.on_token(i, False)
+    b = s.schedule()  # 3 waits: only 2 free blocks, needs 2 -> admitted
+    assert b.kind == 1 and b.ids.tolist() == [3]
+    s.on_token(3, False)
+    # all 6 blocks used; each needs a new block at token 9 -> preemption of the newest
+    b = s.schedule()
+    assert b.kind == 2
+    assert 3 in b.preempted.tolist()
+    assert sorted(b.ids.tolist()) == [1, 2]
+
+
+def test_scheduler_rejects_too_long(native):
+    s = native.Scheduler(16, 4, 4, 64, 16)
+    with pytest.raises(ValueError):
+        s.add(1, 10, 10)
+
+
+def test_safetensors_reader(native, tmp_path):
+    from safetensors.torch import save_file
+
+    t = {"a": torch.randn(7, 5), "b.c": torch.arange(24, dtype=torch.int64).view(2, 3, 4),
+         "h": torch.randn(6, 9).to(torch.bfloat16)}
+    p = str(tmp_path / "x.safetensors")
+    save_file(t, p, metadata={"format": "pt"})
+    f = native.SafetensorsFile(p)
+    assert sorted(f.keys()) == ["a", "b.c", "h"]
+    assert f.metadata()["format"] == "pt"
+    from llmss_amd.utils.checkpoint import CheckpointReader
+
+    r = CheckpointReader([p])
+    assert torch.equal(r.get("a"), t["a"])
+    assert torch.equal(r.rows("a", 2, 5), t["a"][2:5])
+    assert torch.equal(r.cols("a", 1, 4), t["a"][:, 1:4])
+    assert torch.equal(r.cols("b.c", 1, 3), t["b.c"][:, 1:3])
+    assert torch.equal(r.cols("h", 3, 9), t["h"][:, 3:9])
+    assert r.shape("b.c") == [2, 3, 4]
