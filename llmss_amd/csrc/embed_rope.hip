@@ -41,13 +41,17 @@ void launch_embed(const void* ids, const void* pos, const void* wte, const void*
 
 // ---------------------------------------------------------------------------------------------
 // RoPE + KV-cache write.
-//   qkv      [T, row_stride] bf16: q at col 0 (nh*D), k at q_off_k (nkv*D), v at q_off_v (nkv*D)
+//   qkv      [T, row_stride] bf16: q at col 0 (nh*D), k at k_off (nkv*D), v at v_off (nkv*D)
 //   cos_sin  [max_pos, rot/2] fp32 each (host-precomputed table; no on-device trig, guide App. B)
 //   k_cache / v_cache [num_blocks, nkv, block_size, D] bf16 (paged)
 //   slot[t] = physical slot (block*block_size + offset), < 0 = do not cache (padding)
 // q and k are rotated IN PLACE in qkv (prefill attention reads them from there); rotated k and
 // raw v are also written to the paged cache. Styles: 0 = neox half-rotate, 1 = gptj interleaved.
-// One thread per (head, rotation pair); launches one workgroup per token.
+// One thread per 16-byte "octet" of the token's q|k|v row (4 rotation pairs):
+//   neox  octet j < rot/8 of a head: elements [4j, 4j+4) and [rot/2 + 4j, +4) (two 8-B accesses)
+//   gptj  octet j < rot/8 of a head: elements [8j, 8j+8) = pairs (8j+2i, 8j+2i+1) (one 16-B access)
+//   j >= rot/8: pass-through octet [rot + 8(j - rot/8), +8); v octets: copied to the cache.
+// grid (T, ceil(octets / 256)): all octets of all tokens in flight at once.
 // ---------------------------------------------------------------------------------------------
 template <int STYLE>
 __global__ __launch_bounds__(256) void rope_cache_kernel(bf16_t* __restrict__ qkv, int64_t row_stride,
@@ -57,51 +61,65 @@ __global__ __launch_bounds__(256) void rope_cache_kernel(bf16_t* __restrict__ qk
                                                          int nh, int nkv, int D, int rot, int block_size, int k_off,
                                                          int v_off, int do_rope) {
   const int t = blockIdx.x;
-  const int64_t p = do_rope ? pos[t] : 0;
+  const int oct = blockIdx.y * blockDim.x + threadIdx.x;
+  const int OPH = D >> 3;  // octets per head
+  const int nqk = (nh + nkv) * OPH;
+  if (oct >= nqk + nkv * OPH) return;
   const int64_t s = slot ? slot[t] : -1;
   bf16_t* row = qkv + t * row_stride;
-  const int half = D >> 1, rh = rot >> 1;
-  const int total = (nh + nkv) * half;
   int64_t cbase = 0;
   if (s >= 0) {
     const int64_t blk = s / block_size, off = s % block_size;
-    cbase = (blk * nkv) * (int64_t)block_size * D + off * (int64_t)D;  // + h*block_size*D + d
+    cbase = blk * nkv * (int64_t)block_size * D + off * (int64_t)D;  // + head*block_size*D + d
   }
-  for (int i = threadIdx.x; i < total; i += blockDim.x) {
-    const int h = i / half, pi = i - h * half;
-    const bool is_k = h >= nh;
-    const int hk = h - nh;
-    bf16_t* base = is_k ? row + k_off + hk * D : row + h * D;
-    int d0, d1;
-    bool rotate;
-    if (STYLE == 1) {  // gptj: pairs (2i, 2i+1) over the first rot dims
-      d0 = 2 * pi; d1 = d0 + 1; rotate = d0 < rot;
-    } else {  // neox: pairs (i, i+rot/2) for i < rot/2, then pass-through pairs
-      if (pi < rh) { d0 = pi; d1 = pi + rh; rotate = true; }
-      else { d0 = rot + 2 * (pi - rh); d1 = d0 + 1; rotate = false; }
-    }
-    float x0 = bf2f(base[d0]), x1 = bf2f(base[d1]);
-    if (rotate && do_rope) {
-      const int fi = STYLE == 1 ? pi : pi;  // frequency index
-      const float c = cos_t[p * rh + fi], sn = sin_t[p * rh + fi];
-      const float y0 = x0 * c - x1 * sn, y1 = x1 * c + x0 * sn;
-      x0 = y0; x1 = y1;
-      base[d0] = f2bf(x0);
-      base[d1] = f2bf(x1);
-    }
-    if (is_k && s >= 0) {
-      bf16_t* kdst = kc + cbase + (int64_t)hk * block_size * D;
-      kdst[d0] = f2bf(x0);
-      kdst[d1] = f2bf(x1);
-    }
+  if (oct >= nqk) {  // v octet -> cache
+    if (s < 0) return;
+    const int v = oct - nqk, h = v / OPH, j = v % OPH;
+    *reinterpret_cast<u16x8*>(vc + cbase + (int64_t)h * block_size * D + j * 8) =
+        *reinterpret_cast<const u16x8*>(row + v_off + h * D + j * 8);
+    return;
   }
-  // V copy into the cache: 16 B per lane
-  if (s >= 0) {
-    const int vchunks = nkv * (D / 8);
-    for (int i = threadIdx.x; i < vchunks; i += blockDim.x) {
-      const int h = i / (D / 8), c = i - h * (D / 8);
-      u16x8 v = *reinterpret_cast<const u16x8*>(row + v_off + h * D + c * 8);
-      *reinterpret_cast<u16x8*>(vc + cbase + (int64_t)h * block_size * D + c * 8) = v;
+  const int h = oct / OPH, j = oct % OPH;
+  const bool is_k = h >= nh;
+  const int hk = h - nh;
+  bf16_t* base = is_k ? row + k_off + hk * D : row + h * D;
+  bf16_t* kdst = (is_k && s >= 0) ? kc + cbase + (int64_t)hk * block_size * D : nullptr;
+  const int r8 = rot >> 3;
+  if (j >= r8 || !do_rope) {  // pass-through octet (only k needs a cache copy)
+    if (kdst) {
+      const int e = do_rope ? rot + 8 * (j - r8) : 8 * j;
+      *reinterpret_cast<u16x8*>(kdst + e) = *reinterpret_cast<const u16x8*>(base + e);
+    }
+    return;
+  }
+  const int64_t p = pos[t];
+  const int rh = rot >> 1;
+  const f32x4 c = *reinterpret_cast<const f32x4*>(cos_t + p * rh + 4 * j);
+  const f32x4 sn = *reinterpret_cast<const f32x4*>(sin_t + p * rh + 4 * j);
+  if (STYLE == 1) {
+    u16x8 x = *reinterpret_cast<const u16x8*>(base + 8 * j);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x0 = bf2f(x[2 * i]), x1 = bf2f(x[2 * i + 1]);
+      x[2 * i] = f2bf(x0 * c[i] - x1 * sn[i]);
+      x[2 * i + 1] = f2bf(x1 * c[i] + x0 * sn[i]);
+    }
+    *reinterpret_cast<u16x8*>(base + 8 * j) = x;
+    if (kdst) *reinterpret_cast<u16x8*>(kdst + 8 * j) = x;
+  } else {
+    u16x4 a = *reinterpret_cast<const u16x4*>(base + 4 * j);
+    u16x4 b = *reinterpret_cast<const u16x4*>(base + rh + 4 * j);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x0 = bf2f(a[i]), x1 = bf2f(b[i]);
+      a[i] = f2bf(x0 * c[i] - x1 * sn[i]);
+      b[i] = f2bf(x1 * c[i] + x0 * sn[i]);
+    }
+    *reinterpret_cast<u16x4*>(base + 4 * j) = a;
+    *reinterpret_cast<u16x4*>(base + rh + 4 * j) = b;
+    if (kdst) {
+      *reinterpret_cast<u16x4*>(kdst + 4 * j) = a;
+      *reinterpret_cast<u16x4*>(kdst + rh + 4 * j) = b;
     }
   }
 }
@@ -110,17 +128,17 @@ void launch_rope_cache(void* qkv, int64_t row_stride, const void* pos, const voi
                        void* kc, void* vc, const void* slot, int T, int nh, int nkv, int D, int rot, int block_size,
                        int k_off, int v_off, int style, bool do_rope, hipStream_t st) {
   if (D % 8) throw std::runtime_error("rope_cache: head_dim must be a multiple of 8");
-  if (rot % 2 || rot > D) throw std::runtime_error("rope_cache: bad rotary_dim");
+  if (do_rope && (rot % 8 || rot > D)) throw std::runtime_error("rope_cache: rotary_dim must be a multiple of 8");
   if (T == 0) return;
-  const int total = (nh + nkv) * (D / 2);
-  const int threads = std::min(256, ((total + 63) / 64) * 64);
+  const int octets = (nh + 2 * nkv) * (D / 8);
+  dim3 grid(T, (octets + 255) / 256);
   if (style == 1)
-    rope_cache_kernel<1><<<T, threads, 0, st>>>((bf16_t*)qkv, row_stride, (const int64_t*)pos, (const float*)cos_t,
-                                                (const float*)sin_t, (bf16_t*)kc, (bf16_t*)vc, (const int64_t*)slot, nh,
-                                                nkv, D, rot, block_size, k_off, v_off, do_rope ? 1 : 0);
+    rope_cache_kernel<1><<<grid, 256, 0, st>>>((bf16_t*)qkv, row_stride, (const int64_t*)pos, (const float*)cos_t,
+                                               (const float*)sin_t, (bf16_t*)kc, (bf16_t*)vc, (const int64_t*)slot, nh,
+                                               nkv, D, rot, block_size, k_off, v_off, do_rope ? 1 : 0);
   else
-    rope_cache_kernel<0><<<T, threads, 0, st>>>((bf16_t*)qkv, row_stride, (const int64_t*)pos, (const float*)cos_t,
-                                                (const float*)sin_t, (bf16_t*)kc, (bf16_t*)vc, (const int64_t*)slot, nh,
-                                                nkv, D, rot, block_size, k_off, v_off, do_rope ? 1 : 0);
+    rope_cache_kernel<0><<<grid, 256, 0, st>>>((bf16_t*)qkv, row_stride, (const int64_t*)pos, (const float*)cos_t,
+                                               (const float*)sin_t, (bf16_t*)kc, (bf16_t*)vc, (const int64_t*)slot, nh,
+                                               nkv, D, rot, block_size, k_off, v_off, do_rope ? 1 : 0);
   HIP_CHECK_LAUNCH();
 }

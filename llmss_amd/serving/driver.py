@@ -1,0 +1,188 @@
+"""Tensor-parallel serving driver: the engine step loop on every rank + a CPU control plane.
+
+Reference: the consumer broadcasts a pickled payload with ``dist.broadcast_object_list`` over the
+NCCL world group on EVERY idle poll iteration (a spinning GPU collective, consumer_server.py:75-111,
+quirk Q11), then runs one request at a time and broadcasts each sampled token (``:165``).
+
+Here the leader (rank 0) owns admission; per engine step it sends the followers only the *new*
+requests / aborts over a dedicated gloo (CPU/TCP) group, and all ranks then run an identical
+``engine.step()`` (same scheduler decisions, same all-gathered logits, same Philox keys => same
+tokens, no token broadcast). When there is no work the leader blocks on its inbox and followers
+block in a CPU receive - nothing spins on the GPU.
+"""
+from __future__ import annotations
+
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+from datetime import timedelta
+from typing import Callable, Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..engine.engine import LLMEngine
+from ..engine.sampling import SamplingParams
+from ..utils.logging import get_logger
+
+log = get_logger(__name__)
+
+
+@dataclass
+class Handle:
+    rid: int
+    prompt_ids: List[int]
+    params: SamplingParams
+    tokens: "queue.Queue[Optional[int]]" = field(default_factory=queue.Queue)
+    done: threading.Event = field(default_factory=threading.Event)
+    output_ids: List[int] = field(default_factory=list)
+    finish_reason: str = ""
+    metrics: Dict[str, float] = field(default_factory=dict)
+    on_done: Optional[Callable[["Handle"], None]] = None
+    t_submit: float = field(default_factory=time.perf_counter)
+
+    def wait(self, timeout: Optional[float] = None) -> bool:
+        return self.done.wait(timeout)
+
+    def stream(self):
+        while True:
+            t = self.tokens.get()
+            if t is None:
+                return
+            yield t
+
+
+class EngineDriver:
+    def __init__(self, engine: LLMEngine, control_group=None):
+        self.engine = engine
+        self.tp = engine.tp
+        self.rank = self.tp.rank
+        self.leader = self.rank == 0
+        self.cg = control_group
+        if self.tp.is_real and self.cg is None:
+            self.cg = dist.new_group(backend="gloo", timeout=timedelta(days=30))
+        self.inbox: "queue.Queue" = queue.Queue()
+        self.handles: Dict[int, Handle] = {}
+        self._next = 0
+        self._stop = False
+        self._thread: Optional[threading.Thread] = None
+        self._lock = threading.Lock()
+        self.idle_wait_s = 0.05
+
+    # --------------------------------------------------------------------- leader API
+    def submit(self, prompt_ids: List[int], params: SamplingParams,
+               on_done: Optional[Callable[[Handle], None]] = None) -> Handle:
+        if not self.leader:
+            raise RuntimeError("submit() is only valid on rank 0")
+        params.resolved_seed()  # fix the seed on the leader so every rank uses the same one
+        with self._lock:
+            rid = self._next
+            self._next += 1
+        h = Handle(rid, list(prompt_ids), params, on_done=on_done)
+        self.handles[rid] = h
+        self.inbox.put(("new", h))
+        return h
+
+    def abort(self, rid: int):
+        self.inbox.put(("abort", rid))
+
+    def stop(self):
+        self._stop = True
+        self.inbox.put(("stop", None))
+        if self._thread is not None:
+            self._thread.join(timeout=60)
+
+    def start(self):
+        self._thread = threading.Thread(target=self.run, daemon=True, name=f"engine-driver-r{self.rank}")
+        self._thread.start()
+        return self
+
+    # --------------------------------------------------------------------- loop
+    def _bcast(self, msg):
+        if not self.tp.is_real:
+            return msg
+        box = [msg]
+        dist.broadcast_object_list(box, src=0, group=self.cg)
+        return box[0]
+
+    def _collect(self, block: bool):
+        """Leader: drain the inbox (blocking when idle). Returns a control message."""
+        new, aborts, stop = [], [], False
+        try:
+            item = self.inbox.get(timeout=self.idle_wait_s) if block else self.inbox.get_nowait()
+            while True:
+                kind, v = item
+                if kind == "new":
+                    new.append((v.rid, v.prompt_ids, v.params.__dict__.copy()))
+                elif kind == "abort":
+                    aborts.append(v)
+                elif kind == "stop":
+                    stop = True
+                item = self.inbox.get_nowait()
+        except queue.Empty:
+            pass
+        return {"new": new, "abort": aborts, "stop": stop}
+
+    def run(self):
+        eng = self.engine
+        dev_ok = eng.is_gpu
+        if dev_ok:
+            torch.cuda.set_device(eng.device)
+        while True:
+            if self.leader:
+                idle = not eng.has_unfinished()
+                msg = self._collect(block=idle)
+                if idle and not msg["new"] and not msg["abort"] and not msg["stop"] and not self._stop:
+                    continue  # nothing to do, nothing to tell the followers
+            else:
+                msg = None
+            msg = self._bcast(msg)
+            for rid, prompt, pd in msg["new"]:
+                eng.add_request(prompt, SamplingParams(**pd), req_id=rid)
+            for rid in msg["abort"]:
+                eng.abort(rid)
+                self._finish_abort(rid)
+            if msg["stop"]:
+                break
+            if not eng.has_unfinished():
+                continue
+            events = eng.step()
+            if self.leader:
+                for ev in events:
+                    h = self.handles.get(ev.req_id)
+                    if h is None:
+                        continue
+                    h.output_ids.append(ev.token)
+                    h.tokens.put(ev.token)
+                    if ev.finished:
+                        self._complete(h, ev.finish_reason)
+            for r in eng.pop_finished():
+                pass
+
+    def _complete(self, h: Handle, reason: str):
+        req = self.engine.requests.get(h.rid)
+        h.finish_reason = reason
+        if req is not None:
+            h.metrics = req.metrics()
+        h.tokens.put(None)
+        h.done.set()
+        self.handles.pop(h.rid, None)
+        if h.on_done is not None:
+            try:
+                h.on_done(h)
+            except Exception:  # noqa: BLE001
+                log.exception("on_done callback failed")
+
+    def _finish_abort(self, rid):
+        h = self.handles.get(rid)
+        if h is not None:
+            self._complete(h, "abort")
+
+    # --------------------------------------------------------------------- convenience
+    def generate(self, prompt_ids: List[int], params: SamplingParams, timeout: Optional[float] = None) -> Handle:
+        h = self.submit(prompt_ids, params)
+        if not h.wait(timeout):
+            self.abort(h.rid)
+            raise TimeoutError(f"request {h.rid} timed out")
+        return h

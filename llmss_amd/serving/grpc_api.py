@@ -1,0 +1,197 @@
+"""gRPC ``llmss.Generate`` service (``proto/generate.proto``). The reference advertises gRPC in its
+README tagline (README.md:2) but ships none; this is new API surface (BASELINE north star).
+
+``grpc_tools``/``protoc`` are not available, so the message classes are built at import time from
+a ``FileDescriptorProto`` that mirrors ``proto/generate.proto`` field for field, and the service
+is registered with generic method handlers. Any standard gRPC client generated from the .proto
+file interoperates (same package, service, method and field numbers).
+
+Two servicers:
+* :class:`EngineServicer` - in-process on the TP leader, feeding :class:`EngineDriver` directly
+  (lowest latency; config "GPT-2-XL TP=1 served over gRPC").
+* :class:`BrokerServicer` - a front-end that enqueues to the pub/sub broker and waits for the
+  correlated reply (config "pub/sub producer/consumer under concurrent gRPC clients").
+"""
+from __future__ import annotations
+
+import json
+import time
+from concurrent import futures
+from typing import Optional
+
+import grpc
+from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+
+_F = descriptor_pb2.FieldDescriptorProto
+
+
+def _build_pool():
+    fd = descriptor_pb2.FileDescriptorProto(name="llmss/generate.proto", package="llmss", syntax="proto3")
+
+    def msg(name, fields):
+        m = fd.message_type.add(name=name)
+        for num, (fname, ftype, rep) in enumerate(fields, 1):
+            m.field.add(name=fname, number=num, type=ftype,
+                        label=_F.LABEL_REPEATED if rep else _F.LABEL_OPTIONAL)
+
+    S, I32, I64, B, FL = _F.TYPE_STRING, _F.TYPE_INT32, _F.TYPE_INT64, _F.TYPE_BOOL, _F.TYPE_FLOAT
+    msg("GenerateRequest", [("prompt", S, 0), ("max_new_tokens", I32, 0), ("is_greedy", B, 0), ("temperature", FL, 0),
+                            ("top_p", FL, 0), ("top_k", I32, 0), ("request_id", S, 0), ("seed", I64, 0),
+                            ("prompt_token_ids", I32, 1)])
+    msg("GenerateResponse", [("prompt", S, 0), ("continuation", S, 0), ("request_id", S, 0), ("token_ids", I32, 1),
+                             ("finish_reason", S, 0), ("ttft_s", FL, 0), ("e2e_s", FL, 0)])
+    msg("Token", [("token_id", I32, 0), ("text", S, 0), ("finished", B, 0), ("finish_reason", S, 0)])
+    msg("StatsRequest", [])
+    msg("StatsResponse", [("json", S, 0)])
+    svc = fd.service.add(name="Generate")
+    svc.method.add(name="Generate", input_type=".llmss.GenerateRequest", output_type=".llmss.GenerateResponse")
+    svc.method.add(name="GenerateStream", input_type=".llmss.GenerateRequest", output_type=".llmss.Token",
+                   server_streaming=True)
+    svc.method.add(name="Stats", input_type=".llmss.StatsRequest", output_type=".llmss.StatsResponse")
+    pool = descriptor_pool.DescriptorPool()
+    pool.Add(fd)
+    return pool
+
+
+_POOL = _build_pool()
+GenerateRequest = message_factory.GetMessageClass(_POOL.FindMessageTypeByName("llmss.GenerateRequest"))
+GenerateResponse = message_factory.GetMessageClass(_POOL.FindMessageTypeByName("llmss.GenerateResponse"))
+Token = message_factory.GetMessageClass(_POOL.FindMessageTypeByName("llmss.Token"))
+StatsRequest = message_factory.GetMessageClass(_POOL.FindMessageTypeByName("llmss.StatsRequest"))
+StatsResponse = message_factory.GetMessageClass(_POOL.FindMessageTypeByName("llmss.StatsResponse"))
+
+SERVICE = "llmss.Generate"
+
+
+def _params(req):
+    from ..engine.sampling import SamplingParams
+
+    # proto3 scalars default to 0: 0 means "reference default" for max_new_tokens/temperature/top_p
+    # (0 is invalid for them) and "disabled" for top_k (as in the reference CLI, generate.py:30).
+    return SamplingParams(max_new_tokens=req.max_new_tokens or 20, is_greedy=req.is_greedy,
+                          temperature=req.temperature or 1.0, top_p=req.top_p or 0.95, top_k=req.top_k,
+                          seed=req.seed or None).validate()
+
+
+def add_servicer(server: grpc.Server, servicer) -> None:
+    handlers = {
+        "Generate": grpc.unary_unary_rpc_method_handler(
+            servicer.Generate, request_deserializer=GenerateRequest.FromString,
+            response_serializer=GenerateResponse.SerializeToString),
+        "GenerateStream": grpc.unary_stream_rpc_method_handler(
+            servicer.GenerateStream, request_deserializer=GenerateRequest.FromString,
+            response_serializer=Token.SerializeToString),
+        "Stats": grpc.unary_unary_rpc_method_handler(
+            servicer.Stats, request_deserializer=StatsRequest.FromString,
+            response_serializer=StatsResponse.SerializeToString),
+    }
+    server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(SERVICE, handlers),))
+
+
+def serve(servicer, port: int = 50051, host: str = "0.0.0.0", max_workers: int = 64) -> grpc.Server:
+    server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers),
+                         options=[("grpc.max_receive_message_length", 64 << 20)])
+    add_servicer(server, servicer)
+    bound = server.add_insecure_port(f"{host}:{port}")
+    server.start()
+    server.bound_port = bound
+    return server
+
+
+class Stub:
+    """Client stub (what grpc_tools would generate)."""
+
+    def __init__(self, channel: grpc.Channel):
+        self.Generate = channel.unary_unary(f"/{SERVICE}/Generate", request_serializer=GenerateRequest.SerializeToString,
+                                            response_deserializer=GenerateResponse.FromString)
+        self.GenerateStream = channel.unary_stream(f"/{SERVICE}/GenerateStream",
+                                                   request_serializer=GenerateRequest.SerializeToString,
+                                                   response_deserializer=Token.FromString)
+        self.Stats = channel.unary_unary(f"/{SERVICE}/Stats", request_serializer=StatsRequest.SerializeToString,
+                                         response_deserializer=StatsResponse.FromString)
+
+
+# ------------------------------------------------------------------------------ servicers
+class EngineServicer:
+    """Direct servicer on the TP leader."""
+
+    def __init__(self, driver, tokenizer):
+        self.driver = driver
+        self.tok = tokenizer
+
+    def _prompt_ids(self, req):
+        from ..utils.tokenizer import encode
+
+        if len(req.prompt_token_ids):
+            return list(req.prompt_token_ids)
+        return encode(self.tok, req.prompt)
+
+    def Generate(self, req, ctx):
+        try:
+            params = _params(req)
+        except ValueError as e:
+            ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        h = self.driver.submit(self._prompt_ids(req), params)
+        remaining = ctx.time_remaining()
+        if not h.wait(remaining if remaining is not None else None):
+            self.driver.abort(h.rid)
+            ctx.abort(grpc.StatusCode.DEADLINE_EXCEEDED, "generation deadline exceeded")
+        m = h.metrics or {}
+        return GenerateResponse(prompt=req.prompt, continuation=self.tok.decode(h.output_ids), request_id=req.request_id,
+                                token_ids=h.output_ids, finish_reason=h.finish_reason,
+                                ttft_s=float(m.get("ttft_s", 0.0) or 0.0), e2e_s=float(m.get("e2e_s", 0.0) or 0.0))
+
+    def GenerateStream(self, req, ctx):
+        try:
+            params = _params(req)
+        except ValueError as e:
+            ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        h = self.driver.submit(self._prompt_ids(req), params)
+        ctx.add_callback(lambda: (not h.done.is_set()) and self.driver.abort(h.rid))
+        ids, prev = [], ""
+        for t in h.stream():
+            ids.append(t)
+            text = self.tok.decode(ids)
+            yield Token(token_id=t, text=text[len(prev):], finished=False)
+            prev = text
+        yield Token(token_id=-1, text="", finished=True, finish_reason=h.finish_reason)
+
+    def Stats(self, req, ctx):
+        return StatsResponse(json=json.dumps(self.driver.engine.stats))
+
+
+class BrokerServicer:
+    """gRPC front-end of the pub/sub path: enqueue on the broker, wait for the correlated reply."""
+
+    def __init__(self, broker, default_timeout: float = 600.0):
+        self.broker = broker
+        self.timeout = default_timeout
+        self.stats = {"requests": 0, "timeouts": 0}
+
+    def Generate(self, req, ctx):
+        from .broker import PQUEUE, reply_key
+        from .protocol import Request, new_request_id
+
+        rid = req.request_id or new_request_id()
+        body = Request(prompt=req.prompt, max_new_tokens=req.max_new_tokens or 20, is_greedy=req.is_greedy,
+                       temperature=req.temperature or 1.0, top_p=req.top_p or 0.95, top_k=req.top_k or 50,
+                       request_id=rid, seed=req.seed or None)
+        t0 = time.perf_counter()
+        self.broker.lpush(PQUEUE, body.model_dump_json())
+        self.stats["requests"] += 1
+        remaining = ctx.time_remaining()
+        msg = self.broker.brpop(reply_key(rid), timeout=remaining if remaining else self.timeout)
+        if msg is None:
+            self.stats["timeouts"] += 1
+            ctx.abort(grpc.StatusCode.DEADLINE_EXCEEDED, "no reply from consumer")
+        d = json.loads(msg)
+        return GenerateResponse(prompt=d.get("prompt", ""), continuation=d.get("continuation", ""), request_id=rid,
+                                finish_reason=d.get("finish_reason", ""), ttft_s=float(d.get("ttft_s") or 0.0),
+                                e2e_s=float(time.perf_counter() - t0))
+
+    def GenerateStream(self, req, ctx):
+        r = self.Generate(req, ctx)
+        yield Token(token_id=-1, text=r.continuation, finished=True, finish_reason=r.finish_reason)
+
+    def Stats(self, req, ctx):
+        return StatsResponse(json=json.dumps(self.stats))

@@ -1,0 +1,160 @@
+"""Serving path on CPU: broker semantics (in-memory and RESP over TCP), the HTTP producer, the
+TP driver + consumer, gRPC (direct and via the broker), request/response correlation under
+concurrent clients (reference quirk Q11), and reference-format interoperability."""
+import concurrent.futures as cf
+import json
+import threading
+import time
+
+import grpc
+import pytest
+import torch
+
+from helpers import save_hf_model
+from llmss_amd.engine import LLMEngine, build_model
+from llmss_amd.engine.sampling import SamplingParams
+from llmss_amd.serving.broker import PQUEUE, SQUEUE, MemoryBroker, MiniRedisServer, RedisBroker, reply_key
+from llmss_amd.serving.consumer import Consumer
+from llmss_amd.serving.driver import EngineDriver
+from llmss_amd.serving.grpc_api import BrokerServicer, EngineServicer, GenerateRequest, Stub, serve
+from llmss_amd.utils.tokenizer import load_tokenizer
+
+
+@pytest.mark.parametrize("kind", ["memory", "resp"])
+def test_broker_list_semantics(kind):
+    srv = None
+    if kind == "memory":
+        b = MemoryBroker()
+    else:
+        srv = MiniRedisServer().start()
+        b = RedisBroker(srv.host, srv.port)
+        assert b.ping() == "PONG"
+    assert b.llen("q") == 0 and b.rpop("q") is None
+    b.lpush("q", "a")
+    b.lpush("q", "b")
+    b.lpush("q", "ü-unicode")
+    assert b.llen("q") == 3
+    assert b.rpop("q") == "a"  # LPUSH + RPOP = FIFO like the reference queues
+    assert b.brpop("q", 1) == "b"
+    assert b.rpop("q") == "ü-unicode"
+    t0 = time.time()
+    assert b.brpop("q", 0.3) is None and time.time() - t0 >= 0.25
+    threading.Timer(0.2, lambda: b.lpush("q", "late")).start()
+    assert b.brpop("q", 5) == "late"
+    if srv:
+        b.close()
+        srv.stop()
+
+
+@pytest.fixture(scope="module")
+def model_dir(tmp_path_factory):
+    d = str(tmp_path_factory.mktemp("gpt2tok"))
+    save_hf_model("gpt2", d, vocab=101, with_tokenizer=True)
+    return d
+
+
+@pytest.fixture(scope="module")
+def driver(model_dir):
+    m = build_model(model_dir, None, "fp32", "cpu")
+    tok = load_tokenizer(model_dir, m.cfg.vocab_size)
+    eng = LLMEngine(m, max_num_seqs=8, block_size=4, num_blocks=256, eos_token_id=None)
+    drv = EngineDriver(eng).start()
+    yield drv, tok, m
+    drv.stop()
+
+
+def _offline(m, tok, prompt, n):
+    from llmss_amd.utils.tokenizer import encode
+
+    eng = LLMEngine(m, max_num_seqs=4, block_size=4, num_blocks=128, eos_token_id=None)
+    return tok.decode(eng.generate([encode(tok, prompt)], SamplingParams(max_new_tokens=n, is_greedy=True))[0])
+
+
+def test_driver_concurrent_requests(driver):
+    drv, tok, m = driver
+    from llmss_amd.utils.tokenizer import encode
+
+    prompts = ["hello world", "this is", "tiny corpus for", "an offline tokenizer", "hello"]
+    hs = [drv.submit(encode(tok, p), SamplingParams(max_new_tokens=6 + i, is_greedy=True)) for i, p in enumerate(prompts)]
+    for i, (h, p) in enumerate(zip(hs, prompts)):
+        assert h.wait(60)
+        assert len(h.output_ids) == 6 + i
+        assert tok.decode(h.output_ids) == _offline(m, tok, p, 6 + i)
+
+
+def test_producer_consumer_http(driver):
+    from fastapi.testclient import TestClient
+
+    from llmss_amd.serving.producer import create_app
+
+    drv, tok, m = driver
+    srv = MiniRedisServer().start()
+    consumer = Consumer(drv, tok, RedisBroker(srv.host, srv.port), poll_timeout=0.2).start()
+    client = TestClient(create_app(RedisBroker(srv.host, srv.port), timeout_s=60))
+    prompts = [f"hello world {i}" for i in range(6)]
+
+    def call(p):
+        r = client.post("/generate", json={"prompt": p, "max_new_tokens": 5, "is_greedy": True, "temperature": 1.0,
+                                            "top_p": 0.95, "top_k": 50})
+        assert r.status_code == 200
+        return p, r.json()
+
+    with cf.ThreadPoolExecutor(6) as ex:
+        results = list(ex.map(call, prompts))
+    for p, body in results:
+        assert body["prompt"] == p  # correlation: every client gets its own reply
+        assert body["continuation"] == _offline(m, tok, p, 5)
+    assert client.get("/health").json() == {"status": "ok"}
+    assert "llmss_producer_completed 6" in client.get("/metrics").text
+    consumer.stop()
+    srv.stop()
+
+
+def test_reference_format_interop(driver):
+    """A reference producer pushes a request without request_id and pops plain 'squeue'."""
+    drv, tok, m = driver
+    b = MemoryBroker()
+    consumer = Consumer(drv, tok, b, poll_timeout=0.2).start()
+    b.lpush(PQUEUE, json.dumps({"prompt": "hello", "max_new_tokens": 4, "is_greedy": True, "temperature": 1.0,
+                                "top_p": 0.95, "top_k": 50}))
+    msg = b.brpop(SQUEUE, 30)
+    assert msg is not None
+    d = json.loads(msg)
+    assert set(d) == {"prompt", "continuation"} and d["prompt"] == "hello"
+    # invalid request -> error reply, consumer keeps serving
+    b.lpush(PQUEUE, json.dumps({"prompt": "x", "max_new_tokens": 0, "is_greedy": True, "temperature": 1.0,
+                                "top_p": 0.95, "top_k": 50, "request_id": "bad"}))
+    assert "error" in json.loads(b.brpop(reply_key("bad"), 30))
+    consumer.stop()
+
+
+def test_grpc_direct_and_broker(driver):
+    drv, tok, m = driver
+    server = serve(EngineServicer(drv, tok), port=0, host="127.0.0.1")
+    ch = grpc.insecure_channel(f"127.0.0.1:{server.bound_port}")
+    stub = Stub(ch)
+    r = stub.Generate(GenerateRequest(prompt="hello world", max_new_tokens=5, is_greedy=True), timeout=60)
+    assert r.continuation == _offline(m, tok, "hello world", 5) and len(r.token_ids) == 5
+    toks = list(stub.GenerateStream(GenerateRequest(prompt="hello world", max_new_tokens=5, is_greedy=True),
+                                    timeout=60))
+    assert toks[-1].finished and "".join(t.text for t in toks[:-1]) == r.continuation
+    with pytest.raises(grpc.RpcError) as e:
+        stub.Generate(GenerateRequest(prompt="x", max_new_tokens=5, temperature=1.5), timeout=10)
+    assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+    assert json.loads(stub.Stats(__import__("llmss_amd.serving.grpc_api", fromlist=["StatsRequest"]).StatsRequest(),
+                                 timeout=10).json)["tokens"] > 0
+
+    # gRPC front-end on the pub/sub broker, concurrent clients
+    b = MemoryBroker()
+    consumer = Consumer(drv, tok, b, poll_timeout=0.2).start()
+    fe = serve(BrokerServicer(b), port=0, host="127.0.0.1")
+    stub2 = Stub(grpc.insecure_channel(f"127.0.0.1:{fe.bound_port}"))
+    prompts = [f"tiny {i}" for i in range(8)]
+    with cf.ThreadPoolExecutor(8) as ex:
+        outs = list(ex.map(lambda p: stub2.Generate(GenerateRequest(prompt=p, max_new_tokens=4, is_greedy=True),
+                                                    timeout=60), prompts))
+    for p, o in zip(prompts, outs):
+        assert o.prompt == p and o.continuation == _offline(m, tok, p, 4)
+    consumer.stop()
+    fe.stop(0)
+    server.stop(0)
