@@ -71,16 +71,25 @@ def main():
         reqs = eng.pop_finished()
         return n, [r.metrics() for r in reqs]
 
-    for _ in range(args.warmup):
+    def progress(msg):
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+    progress(f"engine ready: {model.cfg.model_type} tp={world} batch={batch} kv_blocks={eng.num_blocks} "
+             f"graphs={sorted(eng.graphs)}")
+    for i in range(args.warmup):
+        t = time.perf_counter()
         one_step()
+        progress(f"warmup {i}: {time.perf_counter() - t:.3f}s")
     tp.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     total, mets = 0, []
-    for _ in range(args.steps):
+    for i in range(args.steps):
         n, m = one_step()
         total += n
         mets.extend(m)
+        progress(f"step {i}: {n} tokens, {time.perf_counter() - t0:.3f}s elapsed")
     torch.cuda.synchronize()
     tp.barrier()
     el = time.perf_counter() - t0

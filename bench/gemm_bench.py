@@ -73,12 +73,15 @@ def main():
                     try:
                         t = timeit(lambda i: H.linear(x, ws[i % ncopy], None, w_scale=scales[i % ncopy] if scales else None,
                                                       out=y, nt_hint=nt, split_hint=sp))
-                    except Exception as e:  # noqa: BLE001
+                    except ValueError:  # config rejected by validation; GPU faults propagate
                         continue
                     key = "ours_us" if (nt, sp) == (0, 0) else f"nt{nt}_s{sp}_us"
                     res[key] = round(t, 2)
                     if best is None or t < best[0]:
                         best = (t, nt, sp)
+                if best is None:
+                    print(json.dumps({**res, "error": "no config ran"}), flush=True)
+                    continue
                 res["best"] = {"us": round(best[0], 2), "nt": best[1], "split": best[2]}
                 t = res["ours_us"]
                 res["ours_TBps"] = round(wbytes / t / 1e6, 3)

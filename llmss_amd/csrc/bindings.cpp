@@ -24,15 +24,16 @@ void launch_attn_decode(const void* q, int64_t q_stride, const void* kc, const v
 void launch_attn_prefill(const void* qkv, int64_t row_stride, const void* cu_seqlens, void* out, int64_t out_stride,
                          int B, int max_seqlen, int nh, int nkv, int D, int k_off, int v_off, float scale,
                          hipStream_t st);
-void launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_fp8, const void* w_scale,
-                 const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace,
-                 int64_t ws_bytes, int nt_hint, int split_hint, hipStream_t st);
-int gemm_skinny_splitk(int M, int N, int K);
+int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_fp8, const void* w_scale,
+                const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace,
+                int64_t ws_bytes, int nt_hint, int split_hint, bool partial_out, hipStream_t st);
+void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk);
+void launch_add_norm_partial(const void* part, int S, int64_t slab, const void* xbias, const void* res_in,
+                             void* res_out, const void* w, const void* b, void* y, int64_t y_stride, int T, int H,
+                             float eps, bool rms, hipStream_t st);
 void launch_sample(const void* logits, int64_t ld, bool fp32_logits, int B, int V, const void* temperature,
                    const void* top_k, const void* top_p, const void* seeds, void* out, void* out2, hipStream_t st);
 void launch_quant_fp8_rows(const void* w, void* q, void* scale, int64_t N, int64_t K, hipStream_t st);
-void launch_allreduce_p2p(void* const* bufs, int world, int rank, void* out, int64_t n_elems, void* flags,
-                          int epoch, hipStream_t st);
 
 void register_runtime(py::module_& m);  // host-side C++ runtime (runtime.cpp)
 
@@ -66,11 +67,20 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("gemm", [](uintptr_t x, int64_t ldx, uintptr_t w, int64_t ldw, bool fp8, uintptr_t ws, uintptr_t bias,
                    uintptr_t y, int64_t ldy, int M, int N, int K, int act, bool glu, uintptr_t work, int64_t wbytes,
-                   int nt_hint, int split_hint, uintptr_t st) {
-    launch_gemm(CP(x), ldx, CP(w), ldw, fp8, CP(ws), CP(bias), P(y), ldy, M, N, K, act, glu, P(work), wbytes, nt_hint,
-                split_hint, S(st));
+                   int nt_hint, int split_hint, bool partial_out, uintptr_t st) {
+    return launch_gemm(CP(x), ldx, CP(w), ldw, fp8, CP(ws), CP(bias), P(y), ldy, M, N, K, act, glu, P(work), wbytes,
+                       nt_hint, split_hint, partial_out, S(st));
   });
-  m.def("gemm_skinny_splitk", &gemm_skinny_splitk);
+  m.def("gemm_plan", [](int M, int N, int K, bool fp8) {
+    int nt, s;
+    gemm_plan(M, N, K, fp8, &nt, &s);
+    return py::make_tuple(nt, s);
+  });
+  m.def("add_norm_partial", [](uintptr_t part, int S, int64_t slab, uintptr_t xbias, uintptr_t ri, uintptr_t ro,
+                               uintptr_t w, uintptr_t b, uintptr_t y, int64_t ys, int T, int H, float eps, bool rms,
+                               uintptr_t st) {
+    launch_add_norm_partial(CP(part), S, slab, CP(xbias), CP(ri), P(ro), CP(w), CP(b), P(y), ys, T, H, eps, rms, S(st));
+  });
   m.def("sample", [](uintptr_t logits, int64_t ld, bool fp32, int B, int V, uintptr_t temp, uintptr_t topk,
                      uintptr_t topp, uintptr_t seeds, uintptr_t out, uintptr_t out2, uintptr_t st) {
     launch_sample(CP(logits), ld, fp32, B, V, CP(temp), CP(topk), CP(topp), CP(seeds), P(out), P(out2), S(st));

@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(const bf16_t* __res
   const char* wrow[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
-    wrow[nt] = (const char*)Wv + ((int64_t)min(n0 + nt * 16 + li, N - 1) * ldw + 16 * g) * WB;
+    wrow[nt] = (const char*)Wv + (int64_t)min(n0 + nt * 16 + li, N - 1) * ldw * WB;  // + k*WB per load
 
   u32x4 wA[NT][KC / 64][FP8W ? 1 : 2], wB[NT][KC / 64][FP8W ? 1 : 2];
   const bool tail_k = (K % KC) != 0;
@@ -423,10 +423,13 @@ int gemm_skinny_splitk(int M, int N, int K) {
   return s;
 }
 
-void launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_fp8, const void* w_scale,
-                 const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace,
-                 int64_t ws_bytes, int nt_hint, int split_hint, hipStream_t st) {
-  if (M == 0 || N == 0) return;
+// Returns the number of fp32 partial slabs [S, M, N] left in `workspace` (partial_out and the
+// planner chose split-K: the consumer - add_norm - reduces them and adds `bias`), or 0 when Y
+// holds the finished bf16 output.
+int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_fp8, const void* w_scale,
+                const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace,
+                int64_t ws_bytes, int nt_hint, int split_hint, bool partial_out, hipStream_t st) {
+  if (M == 0 || N == 0) return 0;
   if (K % 16) throw std::runtime_error("gemm: K must be a multiple of 16");
   if (glu && (N % 32)) throw std::runtime_error("gemm: glu needs N % 32 == 0");
   auto X = (const bf16_t*)x;
@@ -440,9 +443,9 @@ void launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_
       for (int m0 = 0; m0 < M; m0 += 128) {
         const int mm = std::min(128, M - m0);
         launch_gemm((const bf16_t*)x + m0 * ldx, ldx, w, ldw, w_fp8, w_scale, bias, (bf16_t*)y + m0 * ldy, ldy, mm, N,
-                    K, act, glu, workspace, ws_bytes, nt_hint, split_hint, st);
+                    K, act, glu, workspace, ws_bytes, nt_hint, split_hint, false, st);
       }
-      return;
+      return 0;
     }
     int nt, splitk;
     gemm_stream_plan(M, N, K, &nt, &splitk);
@@ -455,15 +458,26 @@ void launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_
     const int act_k = splitk > 1 ? 0 : act, glu_k = splitk > 1 ? 0 : g;
     if (w_fp8) launch_stream<true>(mt, nt, X, ldx, w, ldw, WS, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
     else launch_stream<false>(mt, nt, X, ldx, w, ldw, nullptr, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
+    if (splitk > 1 && partial_out && !glu && act == 0) return splitk;
     if (splitk > 1) {
       const int nout = glu ? N / 2 : N;
       dim3 grid(std::min((nout + 255) / 256, 64), M);
       splitk_reduce_kernel<<<grid, 256, 0, st>>>(part, splitk, M, N, B, Y, ldy, act, g);
       HIP_CHECK_LAUNCH();
     }
-    return;
+    return 0;
   }
   const int nwg = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
   gemm_tiled_kernel<<<nwg, 256, 0, st>>>(X, ldx, (const bf16_t*)w, ldw, B, Y, ldy, M, N, K, act, g);
   HIP_CHECK_LAUNCH();
+  return 0;
+}
+
+void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk) {
+  if (M <= 128 || w_fp8) {
+    gemm_stream_plan(std::min(M, 128), N, K, nt, splitk);
+  } else {
+    *nt = 0;
+    *splitk = 1;
+  }
 }

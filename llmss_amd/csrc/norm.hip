@@ -13,11 +13,15 @@
 #include <stdexcept>
 #include <string>
 
-template <int MAXC, bool RMS, bool HAS_RES, bool HAS_BIAS>
+// PART: x is not a bf16 tensor but S fp32 split-K partial slabs of the preceding GEMM
+// (part[s*slab + row*H + col]) plus an optional bf16 bias - the split-K reduction is fused here.
+template <int MAXC, bool RMS, bool HAS_RES, bool HAS_BIAS, bool PART>
 __global__ __launch_bounds__(256) void add_norm_kernel(const bf16_t* __restrict__ x, int64_t x_stride,
                                                        const bf16_t* res_in, bf16_t* res_out,
                                                        const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
-                                                       bf16_t* __restrict__ y, int64_t y_stride, int H, float eps) {
+                                                       bf16_t* __restrict__ y, int64_t y_stride, int H, float eps,
+                                                       const float* __restrict__ part, int S, int64_t slab,
+                                                       const bf16_t* __restrict__ xbias) {
   __shared__ float red[16];
   const int row = blockIdx.x;
   const int nchunk = H >> 3;
@@ -27,9 +31,28 @@ __global__ __launch_bounds__(256) void add_norm_kernel(const bf16_t* __restrict_
   for (int c = 0; c < MAXC; ++c) {
     const int ch = threadIdx.x + c * blockDim.x;
     if (ch < nchunk) {
-      u16x8 a = *reinterpret_cast<const u16x8*>(xr + ch * 8);
+      if constexpr (PART) {
+        const float* pr = part + (int64_t)row * H + ch * 8;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[c][j] = bf2f(a[j]);
+        for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+        for (int sp = 0; sp < S; ++sp) {
+          const f32x4 p0 = *reinterpret_cast<const f32x4*>(pr + sp * slab);
+          const f32x4 p1 = *reinterpret_cast<const f32x4*>(pr + sp * slab + 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { v[c][j] += p0[j]; v[c][4 + j] += p1[j]; }
+        }
+        if (xbias) {
+          u16x8 bb = *reinterpret_cast<const u16x8*>(xbias + ch * 8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[c][j] += bf2f(bb[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = bf2f(f2bf(v[c][j]));  // the GEMM output is bf16 in the unfused path
+      } else {
+        u16x8 a = *reinterpret_cast<const u16x8*>(xr + ch * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = bf2f(a[j]);
+      }
       if constexpr (HAS_RES) {
         u16x8 r = *reinterpret_cast<const u16x8*>(res_in + (int64_t)row * H + ch * 8);
         u16x8 o;
@@ -87,21 +110,22 @@ __global__ __launch_bounds__(256) void add_norm_kernel(const bf16_t* __restrict_
   }
 }
 
-template <bool RMS, bool HAS_RES, bool HAS_BIAS>
+template <bool RMS, bool HAS_RES, bool HAS_BIAS, bool PART = false>
 static void launch_norm_t(const bf16_t* x, int64_t xs, const bf16_t* ri, bf16_t* ro, const bf16_t* w,
-                          const bf16_t* b, bf16_t* y, int64_t ys, int T, int H, float eps, hipStream_t st) {
+                          const bf16_t* b, bf16_t* y, int64_t ys, int T, int H, float eps, hipStream_t st,
+                          const float* part = nullptr, int S = 0, int64_t slab = 0, const bf16_t* xbias = nullptr) {
   const int nchunk = H / 8;
   int threads = nchunk <= 256 ? ((nchunk + 63) / 64) * 64 : 256;
   const int maxc = (nchunk + threads - 1) / threads;
   dim3 grid(T), block(threads);
   if (maxc == 1)
-    add_norm_kernel<1, RMS, HAS_RES, HAS_BIAS><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps);
+    add_norm_kernel<1, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias);
   else if (maxc == 2)
-    add_norm_kernel<2, RMS, HAS_RES, HAS_BIAS><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps);
+    add_norm_kernel<2, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias);
   else if (maxc <= 4)
-    add_norm_kernel<4, RMS, HAS_RES, HAS_BIAS><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps);
+    add_norm_kernel<4, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias);
   else if (maxc <= 8)
-    add_norm_kernel<8, RMS, HAS_RES, HAS_BIAS><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps);
+    add_norm_kernel<8, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias);
   else
     throw std::runtime_error("add_norm: hidden size too large (max 16384)");
   HIP_CHECK_LAUNCH();
@@ -131,4 +155,23 @@ void launch_add_norm(const void* x, int64_t x_stride, const void* res_in, void* 
       else launch_norm_t<false, false, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st);
     }
   }
+}
+
+// residual-add + norm whose input is the split-K partial sum of the preceding row-parallel GEMM
+void launch_add_norm_partial(const void* part, int S, int64_t slab, const void* xbias, const void* res_in,
+                             void* res_out, const void* w, const void* b, void* y, int64_t y_stride, int T, int H,
+                             float eps, bool rms, hipStream_t st) {
+  if (H % 8 != 0) throw std::runtime_error("add_norm: hidden size must be a multiple of 8");
+  if (!res_in) throw std::runtime_error("add_norm_partial: needs a residual");
+  if (T == 0) return;
+  auto P = (const float*)part;
+  auto XB = (const bf16_t*)xbias;
+  auto RI = (const bf16_t*)res_in;
+  auto RO = (bf16_t*)res_out;
+  auto W = (const bf16_t*)w;
+  auto B = (const bf16_t*)b;
+  auto Y = (bf16_t*)y;
+  if (rms) launch_norm_t<true, true, false, true>(nullptr, 0, RI, RO, W, B, Y, y_stride, T, H, eps, st, P, S, slab, XB);
+  else if (b) launch_norm_t<false, true, true, true>(nullptr, 0, RI, RO, W, B, Y, y_stride, T, H, eps, st, P, S, slab, XB);
+  else launch_norm_t<false, true, false, true>(nullptr, 0, RI, RO, W, B, Y, y_stride, T, H, eps, st, P, S, slab, XB);
 }

@@ -94,11 +94,12 @@ class DecoderLM:
         x = ops.embed(inp.input_ids, w.wte, inp.positions if w.wpe is not None else None, w.wpe)
         residual = None
         delta = x
+        fuse = not self.tp.is_real  # split-K partials can skip their own reduce only without a TP all-reduce
         for i, L in enumerate(w.layers):
             kc, vc = kv_caches[i]
             y, residual = ops.add_norm(delta, L.ln1_w, L.ln1_b, eps, rms, residual)
             a = self._attention(L.qkv(y), inp, kc, vc)
-            o = L.o(a)
+            o = L.o(a, partial_ok=fuse and not cfg.parallel_block)
             if cfg.parallel_block:
                 m = L.down(L.up(y, self.act))
                 o.add_(m)
@@ -106,7 +107,8 @@ class DecoderLM:
             else:
                 o = self.tp.all_reduce(o)
                 y2, residual = ops.add_norm(o, L.ln2_w, L.ln2_b, eps, rms, residual)
-                delta = self.tp.all_reduce(L.down(L.up(y2, self.act)))
+                # TP=1: the down-projection's split-K partials are reduced inside the next add_norm
+                delta = self.tp.all_reduce(L.down(L.up(y2, self.act), partial_ok=fuse))
         h, _ = ops.add_norm(delta, w.lnf_w, w.lnf_b, eps, rms, residual)
         return h
 

@@ -74,8 +74,8 @@ class Linear:
     w_scale: Optional[torch.Tensor] = None
     glu: bool = False
 
-    def __call__(self, x, act="none"):
-        return ops.linear(x, self.w, self.b, act, self.glu, self.w_scale)
+    def __call__(self, x, act="none", partial_ok=False):
+        return ops.linear(x, self.w, self.b, act, self.glu, self.w_scale, partial_ok=partial_ok)
 
     @property
     def out_features(self):

@@ -56,9 +56,10 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale, 
     return ref.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale)
 
 
-def linear(x, w, bias=None, act="none", glu=False, w_scale: Optional[torch.Tensor] = None):
+def linear(x, w, bias=None, act="none", glu=False, w_scale: Optional[torch.Tensor] = None, partial_ok=False):
+    """partial_ok: on GPU the result may be a split-K PartialSum that only add_norm consumes."""
     if x.is_cuda:
-        return _hip().linear(x, w, bias, act, glu, w_scale)
+        return _hip().linear(x, w, bias, act, glu, w_scale, partial_ok=partial_ok)
     return ref.linear(x, w, bias, act, glu, w_scale)
 
 

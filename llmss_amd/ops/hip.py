@@ -56,6 +56,8 @@ def _bf16_rows(t: torch.Tensor, name: str, cols: Optional[int] = None):
 
 # ------------------------------------------------------------------------------------- norm
 def add_norm(x, weight, bias, eps, rms, residual=None, out=None, residual_out=None):
+    if isinstance(x, PartialSum):
+        return add_norm_partial(x, weight, bias, eps, rms, residual, out)
     T, H = x.shape
     _bf16_rows(x, "x")
     _check(H % 8 == 0, "hidden must be a multiple of 8")
@@ -95,7 +97,7 @@ def rope_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, ro
     T = qkv.shape[0]
     _bf16_rows(qkv, "qkv")
     _check(qkv.shape[1] >= (nh + 2 * nkv) * D, "qkv too narrow")
-    _check(D % 8 == 0 and rot % 2 == 0 and rot <= D, "head_dim / rotary_dim")
+    _check(D % 8 == 0 and rot <= D and (not do_rope or rot % 8 == 0), "head_dim / rotary_dim (multiple of 8)")
     _check(positions.dtype == torch.int64 and positions.numel() == T and positions.is_contiguous(), "positions")
     if do_rope and rot > 0:
         _check(cos.dtype == torch.float32 and cos.is_contiguous() and cos.shape[1] == rot // 2, "cos table")
@@ -212,7 +214,27 @@ def reserve_workspace(device, gemm_bytes: int = 64 << 20, decode_rows: int = 0, 
 _ACT = {"none": 0, None: 0, "gelu_tanh": 1, "gelu": 2, "relu": 3}
 
 
-def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hint=0, split_hint=0):
+class PartialSum:
+    """fp32 split-K partial slabs [S, M, N] of a GEMM left in the GEMM workspace; consumed (summed +
+    bias) by the next add_norm. Valid only until the next GEMM on the stream."""
+
+    __slots__ = ("buf", "S", "M", "N", "bias", "dtype", "device")
+
+    def __init__(self, buf, S, M, N, bias, device):
+        self.buf, self.S, self.M, self.N, self.bias, self.device = buf, S, M, N, bias, device
+        self.dtype = torch.bfloat16
+
+    @property
+    def shape(self):
+        return (self.M, self.N)
+
+    @property
+    def is_cuda(self):
+        return True
+
+
+def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hint=0, split_hint=0,
+           partial_ok=False):
     M, K = x.shape
     _bf16_rows(x, "x")
     fp8 = w_scale is not None
@@ -230,12 +252,36 @@ def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hi
     if bias is not None:
         _check(bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.numel() == N, "bias [N] bf16")
     nout = N // 2 if glu else N
-    y = out if out is not None else torch.empty(M, nout, dtype=x.dtype, device=x.device)
-    _bf16_rows(y, "out", nout)
     ws = _GEMM_WS.get(64 << 20, x.device)
-    lib().gemm(x.data_ptr(), x.stride(0), w.data_ptr(), K, fp8, _ptr(w_scale), _ptr(bias), y.data_ptr(), y.stride(0),
-               M, N, K, _ACT[act], bool(glu), ws.data_ptr(), ws.numel() * 4, int(nt_hint), int(split_hint), _stream())
+    partial_ok = partial_ok and not glu and act in ("none", None) and out is None
+    y = out if out is not None else (None if partial_ok else torch.empty(M, nout, dtype=x.dtype, device=x.device))
+    if partial_ok:
+        nt, s = lib().gemm_plan(M, N, K, fp8)
+        if split_hint:
+            s = split_hint
+        if s <= 1 or s * M * N * 4 > ws.numel() * 4:
+            y = torch.empty(M, nout, dtype=x.dtype, device=x.device)
+    if y is not None:
+        _bf16_rows(y, "out", nout)
+    S = lib().gemm(x.data_ptr(), x.stride(0), w.data_ptr(), K, fp8, _ptr(w_scale), _ptr(bias), _ptr(y),
+                   y.stride(0) if y is not None else nout, M, N, K, _ACT[act], bool(glu), ws.data_ptr(),
+                   ws.numel() * 4, int(nt_hint), int(split_hint), bool(y is None), _stream())
+    if y is None:
+        if S <= 1:
+            raise RuntimeError("internal: partial GEMM did not produce partial slabs")
+        return PartialSum(ws, S, M, N, bias, x.device)
     return y
+
+
+def add_norm_partial(p: PartialSum, weight, bias, eps, rms, residual, out=None):
+    T, H = p.M, p.N
+    _check(residual is not None and residual.is_contiguous() and residual.shape == (T, H), "residual [T, H]")
+    _check(weight.numel() == H and weight.dtype == torch.bfloat16 and weight.is_contiguous(), "norm weight")
+    y = out if out is not None else torch.empty(T, H, dtype=torch.bfloat16, device=residual.device)
+    lib().add_norm_partial(p.buf.data_ptr(), p.S, T * H, _ptr(p.bias), residual.data_ptr(), residual.data_ptr(),
+                           weight.data_ptr(), _ptr(bias), y.data_ptr(), y.stride(0), T, H, float(eps), bool(rms),
+                           _stream())
+    return y, residual
 
 
 def quant_fp8_rows(w):

@@ -174,3 +174,20 @@ def test_sample_distribution():
     freq = torch.bincount(o, minlength=V).float() / 4096
     p = torch.softmax(logits[0].float() / 0.7, -1)
     assert (freq - p).abs().max() < 0.03, (freq, p)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (64, 4096, 11008), (100, 1600, 6400)])
+@pytest.mark.parametrize("rms", [True, False])
+def test_splitk_partials_fused_into_add_norm(M, N, K, rms):
+    torch.manual_seed(0)
+    x, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
+    b = rnd(N, scale=0.1)
+    res = rnd(M, N)
+    nw, nb = rnd(N, scale=0.2) + 1, (None if rms else rnd(N, scale=0.1))
+    y_ref = H.linear(x, w, b)
+    out_ref, r_ref = H.add_norm(y_ref, nw, nb, 1e-5, rms, residual=res.clone())
+    p = H.linear(x, w, b, partial_ok=True)
+    r2 = res.clone()
+    out, r_out = H.add_norm(p, nw, nb, 1e-5, rms, residual=r2)
+    close(r_out, r_ref, 2e-2)
+    close(out, out_ref, 3e-2)
