@@ -66,8 +66,8 @@ def main():
                     t = timeit(lambda i: torch.matmul(x, ws[i % ncopy].t(), out=y))
                     res["hipblaslt_us"] = round(t, 2)
                 cfgs = [(0, 0)]
-                if a.sweep and M <= 128:
-                    cfgs += list(itertools.product([1, 2, 4], [1, 2, 4, 8]))
+                if a.sweep and M <= 128:  # nt_hint = nt + 16 * variant (1: LDS-DMA X, 2: register X + W ring)
+                    cfgs += [(nt + 16 * v, sp) for v, nt, sp in itertools.product([1, 2], [1, 2], [1, 2, 4, 8])]
                 best = None
                 for nt, sp in cfgs:
                     try:

@@ -232,6 +232,139 @@ __global__ __launch_bounds__(256, 2) void gemm_stream_kernel(const bf16_t* __res
   }
 }
 
+// -------------------------------------------------------------------------------------------
+// weight-streaming GEMM, v2: register-staged X + 3-deep W register ring (2 chunks in flight).
+// v1 stages X with global_load_lds; while an LDS-DMA is in flight hipcc drains vmcnt(0) at every
+// use of an ordinary load (guide §5 'Pipelining across barriers'), which caps v1 at ONE W chunk
+// in flight per wave. Here every load is an ordinary global_load, issued in the order
+// X(c+1), W(c+2) before the MFMAs of chunk c, so the compiler's counted vmcnt waits only for what
+// each consumer needs: the ds_write of X(c+1) waits for X(c+1), not for W(c+2).
+// Same tile/K mapping as v1 (verified by tests/test_kernel_emulation.py), same epilogue.
+// -------------------------------------------------------------------------------------------
+template <int MT, int NT, int KC, bool FP8W>
+struct Stream2Cfg {
+  static constexpr int ROWS = MT * 16;
+  static constexpr int RB = KC * 2;
+  static constexpr int XBYTES = ROWS * RB;
+  static constexpr int CPR = KC / 8;                      // 16-B chunks per X row
+  static constexpr int XPT = ROWS * CPR / 256;            // X chunks per thread per K-chunk
+  static constexpr int SW = (CPR - 1) < 15 ? (CPR - 1) : 15;
+  static_assert((ROWS * CPR) % 256 == 0, "X chunk must split evenly over 256 threads");
+};
+
+template <int MT, int NT, int KC, bool FP8W>
+__device__ __forceinline__ void stream2_load_x(const bf16_t* __restrict__ X, int64_t ldx, int M, int K, int kc0,
+                                               u32x4 (&xr)[Stream2Cfg<MT, NT, KC, FP8W>::XPT]) {
+  using C = Stream2Cfg<MT, NT, KC, FP8W>;
+#pragma unroll
+  for (int i = 0; i < C::XPT; ++i) {
+    const int id = threadIdx.x + i * 256;
+    const int row = id / C::CPR, c = id % C::CPR;
+    const int k = min(kc0 + c * 8, K - 8);
+    xr[i] = *reinterpret_cast<const u32x4*>(X + (int64_t)min(row, M - 1) * ldx + k);
+  }
+}
+
+template <int MT, int NT, int KC, bool FP8W>
+__device__ __forceinline__ void stream2_store_x(char* xbuf, const u32x4 (&xr)[Stream2Cfg<MT, NT, KC, FP8W>::XPT]) {
+  using C = Stream2Cfg<MT, NT, KC, FP8W>;
+#pragma unroll
+  for (int i = 0; i < C::XPT; ++i) {
+    const int id = threadIdx.x + i * 256;
+    const int row = id / C::CPR, c = id % C::CPR;
+    *reinterpret_cast<u32x4*>(xbuf + row * C::RB + ((c ^ (row & C::SW)) << 4)) = xr[i];
+  }
+}
+
+template <int MT, int NT, int KC, bool FP8W>
+__global__ __launch_bounds__(256, 2) void gemm_stream2_kernel(const bf16_t* __restrict__ X, int64_t ldx,
+                                                              const void* __restrict__ Wv, int64_t ldw,
+                                                              const float* __restrict__ wscale,
+                                                              const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
+                                                              int64_t ldy, float* __restrict__ part, int M, int N,
+                                                              int K, int act, int glu) {
+  using C = Stream2Cfg<MT, NT, KC, FP8W>;
+  __shared__ __attribute__((aligned(16))) char xs[2 * C::XBYTES];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * (64 * NT) + w * (16 * NT);
+  const int split = blockIdx.y, nsplit = gridDim.y;
+  const int nck = (K + KC - 1) / KC;
+  const int cb = (int)((int64_t)nck * split / nsplit), ce = (int)((int64_t)nck * (split + 1) / nsplit);
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int WB = FP8W ? 1 : 2;
+  const char* wrow[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) wrow[nt] = (const char*)Wv + (int64_t)min(n0 + nt * 16 + li, N - 1) * ldw * WB;
+
+  u32x4 w0[NT][KC / 64][FP8W ? 1 : 2], w1[NT][KC / 64][FP8W ? 1 : 2], w2[NT][KC / 64][FP8W ? 1 : 2];
+  u32x4 xr[C::XPT];
+  const bool tail_k = (K % KC) != 0;
+  if (cb < ce) {
+    stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, cb * KC, xr);
+    stream_load_w<MT, NT, KC, FP8W>(wrow, cb * KC, K, g, w0);
+    if (cb + 1 < ce) stream_load_w<MT, NT, KC, FP8W>(wrow, (cb + 1) * KC, K, g, w1);
+    stream2_store_x<MT, NT, KC, FP8W>(xs, xr);
+    __syncthreads();
+  }
+#define STREAM2_STEP(CUR, NXT2)                                                                               \
+  {                                                                                                          \
+    const int cc = c;                                                                                        \
+    if (cc + 1 < ce) stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, (cc + 1) * KC, xr);                      \
+    if (cc + 2 < ce) stream_load_w<MT, NT, KC, FP8W>(wrow, (cc + 2) * KC, K, g, NXT2);                       \
+    const char* xb = xs + ((cc - cb) & 1) * C::XBYTES;                                                       \
+    if (tail_k && cc == nck - 1) stream_compute<MT, NT, KC, FP8W, true>(xb, CUR, acc, cc * KC, K, li, g);    \
+    else stream_compute<MT, NT, KC, FP8W, false>(xb, CUR, acc, cc * KC, K, li, g);                           \
+    if (cc + 1 < ce) stream2_store_x<MT, NT, KC, FP8W>(xs + ((cc + 1 - cb) & 1) * C::XBYTES, xr);            \
+    __syncthreads();                                                                                         \
+    if (++c >= ce) break;                                                                                    \
+  }
+  for (int c = cb; c < ce;) {
+    STREAM2_STEP(w0, w2)
+    STREAM2_STEP(w1, w0)
+    STREAM2_STEP(w2, w1)
+  }
+#undef STREAM2_STEP
+
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = mt * 16 + 4 * g + i;
+      if (m >= M) continue;
+      if (nsplit > 1) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const int n = n0 + nt * 16 + li;
+          if (n < N) part[((int64_t)split * M + m) * N + n] = acc[mt][nt][i] * (wscale ? wscale[n] : 1.f);
+        }
+      } else if (glu) {
+#pragma unroll
+        for (int p = 0; p < NT / 2; ++p) {
+          const int ng = n0 + 2 * p * 16 + li, nu = ng + 16;
+          if (nu < N) {
+            const float gv = epi_value(acc[mt][2 * p][i], ng, wscale, bias, ACT_NONE);
+            const float uv = epi_value(acc[mt][2 * p + 1][i], nu, wscale, bias, ACT_NONE);
+            Y[(int64_t)m * ldy + n0 / 2 + p * 16 + li] = f2bf(silu(gv) * uv);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const int n = n0 + nt * 16 + li;
+          if (n < N) Y[(int64_t)m * ldy + n] = f2bf(epi_value(acc[mt][nt][i], n, wscale, bias, act));
+        }
+      }
+    }
+  }
+}
+
 // split-K reduction + epilogue: part [S, M, N] fp32 (w_scale already applied)
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N,
                                                             const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
@@ -370,21 +503,35 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
 // -------------------------------------------------------------------------------------------
 // host dispatch
 // -------------------------------------------------------------------------------------------
-template <int MT, int NT, int KC, bool FP8W>
+template <int MT, int NT, int KC, bool FP8W, int VARIANT>
 static void launch_stream_t(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const float* ws, const bf16_t* bias,
                             bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu, int splitk,
                             hipStream_t st) {
   dim3 grid((N + 64 * NT - 1) / (64 * NT), splitk);
-  gemm_stream_kernel<MT, NT, KC, FP8W><<<grid, 256, 0, st>>>(X, ldx, W, ldw, ws, bias, Y, ldy, part, M, N, K, act, glu);
+  if constexpr (VARIANT == 2)
+    gemm_stream2_kernel<MT, NT, KC, FP8W><<<grid, 256, 0, st>>>(X, ldx, W, ldw, ws, bias, Y, ldy, part, M, N, K, act, glu);
+  else
+    gemm_stream_kernel<MT, NT, KC, FP8W><<<grid, 256, 0, st>>>(X, ldx, W, ldw, ws, bias, Y, ldy, part, M, N, K, act, glu);
   HIP_CHECK_LAUNCH();
 }
 
 template <bool FP8W>
-static void launch_stream(int mt, int nt, const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const float* ws,
-                          const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
-                          int splitk, hipStream_t st) {
+static void launch_stream(int variant, int mt, int nt, const bf16_t* X, int64_t ldx, const void* W, int64_t ldw,
+                          const float* ws, const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K,
+                          int act, int glu, int splitk, hipStream_t st) {
+  if (variant == 2) {  // v2 instantiations (3-deep W ring): NT <= 2, spill-free at 2 waves/SIMD
+#define LS2(MT_, NT_, KC_) \
+  launch_stream_t<MT_, NT_, KC_, FP8W, 2>(X, ldx, W, ldw, ws, bias, Y, ldy, part, M, N, K, act, glu, splitk, st)
+    if (nt >= 2) {
+      if (mt == 1) LS2(1, 2, 128); else if (mt == 2) LS2(2, 2, 128); else if (mt <= 4) LS2(4, 2, 128); else LS2(8, 2, 64);
+    } else {
+      if (mt == 1) LS2(1, 1, 256); else if (mt == 2) LS2(2, 1, 256); else if (mt <= 4) LS2(4, 1, 256); else LS2(8, 1, 128);
+    }
+#undef LS2
+    return;
+  }
 #define LS(MT_, NT_, KC_) \
-  launch_stream_t<MT_, NT_, KC_, FP8W>(X, ldx, W, ldw, ws, bias, Y, ldy, part, M, N, K, act, glu, splitk, st)
+  launch_stream_t<MT_, NT_, KC_, FP8W, 1>(X, ldx, W, ldw, ws, bias, Y, ldy, part, M, N, K, act, glu, splitk, st)
   // only register-feasible (spill-free at 2 waves/SIMD) instantiations
   if constexpr (FP8W) {
     if (nt >= 2) {
@@ -449,6 +596,9 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_f
     }
     int nt, splitk;
     gemm_stream_plan(M, N, K, &nt, &splitk);
+    // nt_hint = nt + 16 * variant (variant 1: LDS-DMA X staging, 2: register-staged X + W ring)
+    int variant = (nt_hint >> 4) ? (nt_hint >> 4) : 2;
+    nt_hint &= 15;
     if (nt_hint > 0) nt = nt_hint;
     if (split_hint > 0) splitk = split_hint;
     if (glu && nt < 2) nt = 2;  // the SwiGLU epilogue pairs (gate, up) 16-column tiles inside a wave
@@ -456,8 +606,8 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_f
     float* part = splitk > 1 ? (float*)workspace : nullptr;
     const int mt = (M + 15) / 16;
     const int act_k = splitk > 1 ? 0 : act, glu_k = splitk > 1 ? 0 : g;
-    if (w_fp8) launch_stream<true>(mt, nt, X, ldx, w, ldw, WS, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
-    else launch_stream<false>(mt, nt, X, ldx, w, ldw, nullptr, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
+    if (w_fp8) launch_stream<true>(variant, mt, nt, X, ldx, w, ldw, WS, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
+    else launch_stream<false>(variant, mt, nt, X, ldx, w, ldw, nullptr, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
     if (splitk > 1 && partial_out && !glu && act == 0) return splitk;
     if (splitk > 1) {
       const int nout = glu ? N / 2 : N;
