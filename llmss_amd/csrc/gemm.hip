@@ -313,24 +313,46 @@ __global__ __launch_bounds__(256, 2) void gemm_stream2_kernel(const bf16_t* __re
     stream2_store_x<MT, NT, KC, FP8W>(xs, xr);
     __syncthreads();
   }
-#define STREAM2_STEP(CUR, NXT2)                                                                               \
+  // Steady state: branch-free steps (every prefetch valid), so hipcc's vmcnt bookkeeping stays
+  // exact and it waits only for the chunk being consumed (a load under an `if` makes the counts
+  // path-dependent and the compiler then drains vmcnt(0) before re-issuing - measured).
+#define STREAM2_STEADY(CUR, NXT2)                                                                             \
   {                                                                                                          \
-    const int cc = c;                                                                                        \
-    if (cc + 1 < ce) stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, (cc + 1) * KC, xr);                      \
-    if (cc + 2 < ce) stream_load_w<MT, NT, KC, FP8W>(wrow, (cc + 2) * KC, K, g, NXT2);                       \
-    const char* xb = xs + ((cc - cb) & 1) * C::XBYTES;                                                       \
-    if (tail_k && cc == nck - 1) stream_compute<MT, NT, KC, FP8W, true>(xb, CUR, acc, cc * KC, K, li, g);    \
-    else stream_compute<MT, NT, KC, FP8W, false>(xb, CUR, acc, cc * KC, K, li, g);                           \
-    if (cc + 1 < ce) stream2_store_x<MT, NT, KC, FP8W>(xs + ((cc + 1 - cb) & 1) * C::XBYTES, xr);            \
+    stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, (c + 1) * KC, xr);                                        \
+    stream_load_w<MT, NT, KC, FP8W>(wrow, (c + 2) * KC, K, g, NXT2);                                         \
+    __builtin_amdgcn_sched_barrier(0); /* keep the prefetch ahead of the MFMAs (hipcc sinks it) */           \
+    stream_compute<MT, NT, KC, FP8W, false>(xs + ((c - cb) & 1) * C::XBYTES, CUR, acc, c * KC, K, li, g);    \
+    __builtin_amdgcn_sched_barrier(0);                                                                       \
+    stream2_store_x<MT, NT, KC, FP8W>(xs + ((c + 1 - cb) & 1) * C::XBYTES, xr);                              \
     __syncthreads();                                                                                         \
-    if (++c >= ce) break;                                                                                    \
+    ++c;                                                                                                     \
   }
-  for (int c = cb; c < ce;) {
-    STREAM2_STEP(w0, w2)
-    STREAM2_STEP(w1, w0)
-    STREAM2_STEP(w2, w1)
+#define STREAM2_REM(CUR, NXT2)                                                                                \
+  {                                                                                                          \
+    if (c >= ce) break;                                                                                      \
+    if (c + 1 < ce) stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, (c + 1) * KC, xr);                        \
+    if (c + 2 < ce) stream_load_w<MT, NT, KC, FP8W>(wrow, (c + 2) * KC, K, g, NXT2);                         \
+    const char* xb = xs + ((c - cb) & 1) * C::XBYTES;                                                        \
+    if (tail_k && c == nck - 1) stream_compute<MT, NT, KC, FP8W, true>(xb, CUR, acc, c * KC, K, li, g);      \
+    else stream_compute<MT, NT, KC, FP8W, false>(xb, CUR, acc, c * KC, K, li, g);                            \
+    if (c + 1 < ce) stream2_store_x<MT, NT, KC, FP8W>(xs + ((c + 1 - cb) & 1) * C::XBYTES, xr);              \
+    __syncthreads();                                                                                         \
+    ++c;                                                                                                     \
   }
-#undef STREAM2_STEP
+  int c = cb;
+  for (; c + 4 < ce;) {  // 3 chunks per iteration; chunks c+2..c+4 exist -> all prefetches valid
+    STREAM2_STEADY(w0, w2)
+    STREAM2_STEADY(w1, w0)
+    STREAM2_STEADY(w2, w1)
+  }
+  do {  // remaining <= 4 chunks (ring rotation continues at w0); also handles the K tail chunk
+    STREAM2_REM(w0, w2)
+    STREAM2_REM(w1, w0)
+    STREAM2_REM(w2, w1)
+    STREAM2_REM(w0, w2)
+  } while (0);
+#undef STREAM2_STEADY
+#undef STREAM2_REM
 
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -525,7 +547,7 @@ static void launch_stream(int variant, int mt, int nt, const bf16_t* X, int64_t 
     if (nt >= 2) {
       if (mt == 1) LS2(1, 2, 128); else if (mt == 2) LS2(2, 2, 128); else if (mt <= 4) LS2(4, 2, 128); else LS2(8, 2, 64);
     } else {
-      if (mt == 1) LS2(1, 1, 256); else if (mt == 2) LS2(2, 1, 256); else if (mt <= 4) LS2(4, 1, 256); else LS2(8, 1, 128);
+      if (mt == 1) LS2(1, 1, 256); else if (mt == 2) LS2(2, 1, 128); else if (mt <= 4) LS2(4, 1, 128); else LS2(8, 1, 128);
     }
 #undef LS2
     return;
