@@ -303,53 +303,61 @@ __global__ __launch_bounds__(256, 2) void gemm_stream2_kernel(const bf16_t* __re
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) wrow[nt] = (const char*)Wv + (int64_t)min(n0 + nt * 16 + li, N - 1) * ldw * WB;
 
+  // W and X both live in 3-slot register rings: chunk c+2 is loaded during step c, chunk c+1
+  // (loaded during step c-1) is written to LDS at the end of step c, chunk c is consumed.
   u32x4 w0[NT][KC / 64][FP8W ? 1 : 2], w1[NT][KC / 64][FP8W ? 1 : 2], w2[NT][KC / 64][FP8W ? 1 : 2];
-  u32x4 xr[C::XPT];
+  u32x4 x0[C::XPT], x1[C::XPT], x2[C::XPT];
   const bool tail_k = (K % KC) != 0;
   if (cb < ce) {
-    stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, cb * KC, xr);
+    stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, cb * KC, x0);
     stream_load_w<MT, NT, KC, FP8W>(wrow, cb * KC, K, g, w0);
-    if (cb + 1 < ce) stream_load_w<MT, NT, KC, FP8W>(wrow, (cb + 1) * KC, K, g, w1);
-    stream2_store_x<MT, NT, KC, FP8W>(xs, xr);
+    if (cb + 1 < ce) {
+      stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, (cb + 1) * KC, x1);
+      stream_load_w<MT, NT, KC, FP8W>(wrow, (cb + 1) * KC, K, g, w1);
+    }
+    stream2_store_x<MT, NT, KC, FP8W>(xs, x0);
     __syncthreads();
   }
   // Steady state: branch-free steps (every prefetch valid), so hipcc's vmcnt bookkeeping stays
   // exact and it waits only for the chunk being consumed (a load under an `if` makes the counts
   // path-dependent and the compiler then drains vmcnt(0) before re-issuing - measured).
-#define STREAM2_STEADY(CUR, NXT2)                                                                             \
+#define STREAM2_STEADY(WCUR, WNXT2, XNXT1, XNXT2)                                                             \
   {                                                                                                          \
-    stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, (c + 1) * KC, xr);                                        \
-    stream_load_w<MT, NT, KC, FP8W>(wrow, (c + 2) * KC, K, g, NXT2);                                         \
+    stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, (c + 2) * KC, XNXT2);                                     \
+    stream_load_w<MT, NT, KC, FP8W>(wrow, (c + 2) * KC, K, g, WNXT2);                                        \
     __builtin_amdgcn_sched_barrier(0); /* keep the prefetch ahead of the MFMAs (hipcc sinks it) */           \
-    stream_compute<MT, NT, KC, FP8W, false>(xs + ((c - cb) & 1) * C::XBYTES, CUR, acc, c * KC, K, li, g);    \
+    stream_compute<MT, NT, KC, FP8W, false>(xs + ((c - cb) & 1) * C::XBYTES, WCUR, acc, c * KC, K, li, g);   \
     __builtin_amdgcn_sched_barrier(0);                                                                       \
-    stream2_store_x<MT, NT, KC, FP8W>(xs + ((c + 1 - cb) & 1) * C::XBYTES, xr);                              \
+    stream2_store_x<MT, NT, KC, FP8W>(xs + ((c + 1 - cb) & 1) * C::XBYTES, XNXT1);                           \
     __syncthreads();                                                                                         \
     ++c;                                                                                                     \
   }
-#define STREAM2_REM(CUR, NXT2)                                                                                \
+#define STREAM2_REM(WCUR, WNXT2, XNXT1, XNXT2)                                                                \
   {                                                                                                          \
     if (c >= ce) break;                                                                                      \
-    if (c + 1 < ce) stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, (c + 1) * KC, xr);                        \
-    if (c + 2 < ce) stream_load_w<MT, NT, KC, FP8W>(wrow, (c + 2) * KC, K, g, NXT2);                         \
+    if (c + 2 < ce) {                                                                                        \
+      stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, (c + 2) * KC, XNXT2);                                   \
+      stream_load_w<MT, NT, KC, FP8W>(wrow, (c + 2) * KC, K, g, WNXT2);                                      \
+    }                                                                                                        \
     const char* xb = xs + ((c - cb) & 1) * C::XBYTES;                                                        \
-    if (tail_k && c == nck - 1) stream_compute<MT, NT, KC, FP8W, true>(xb, CUR, acc, c * KC, K, li, g);      \
-    else stream_compute<MT, NT, KC, FP8W, false>(xb, CUR, acc, c * KC, K, li, g);                            \
-    if (c + 1 < ce) stream2_store_x<MT, NT, KC, FP8W>(xs + ((c + 1 - cb) & 1) * C::XBYTES, xr);              \
+    if (tail_k && c == nck - 1) stream_compute<MT, NT, KC, FP8W, true>(xb, WCUR, acc, c * KC, K, li, g);     \
+    else stream_compute<MT, NT, KC, FP8W, false>(xb, WCUR, acc, c * KC, K, li, g);                           \
+    if (c + 1 < ce) stream2_store_x<MT, NT, KC, FP8W>(xs + ((c + 1 - cb) & 1) * C::XBYTES, XNXT1);           \
     __syncthreads();                                                                                         \
     ++c;                                                                                                     \
   }
+  // slot of chunk c = (c - cb) % 3 for both rings
   int c = cb;
   for (; c + 4 < ce;) {  // 3 chunks per iteration; chunks c+2..c+4 exist -> all prefetches valid
-    STREAM2_STEADY(w0, w2)
-    STREAM2_STEADY(w1, w0)
-    STREAM2_STEADY(w2, w1)
+    STREAM2_STEADY(w0, w2, x1, x2)
+    STREAM2_STEADY(w1, w0, x2, x0)
+    STREAM2_STEADY(w2, w1, x0, x1)
   }
-  do {  // remaining <= 4 chunks (ring rotation continues at w0); also handles the K tail chunk
-    STREAM2_REM(w0, w2)
-    STREAM2_REM(w1, w0)
-    STREAM2_REM(w2, w1)
-    STREAM2_REM(w0, w2)
+  do {  // remaining <= 4 chunks (ring rotation continues at slot 0); also the K tail chunk
+    STREAM2_REM(w0, w2, x1, x2)
+    STREAM2_REM(w1, w0, x2, x0)
+    STREAM2_REM(w2, w1, x0, x1)
+    STREAM2_REM(w0, w2, x1, x2)
   } while (0);
 #undef STREAM2_STEADY
 #undef STREAM2_REM
@@ -580,8 +588,11 @@ void gemm_stream_plan(int M, int N, int K, int* nt_out, int* splitk_out) {
   const int nblk = (N + 64 * nt - 1) / (64 * nt);
   const int kc = M > 64 ? 128 : 256;
   const int nck = (K + kc - 1) / kc;
+  // measured (bench/gemm_bench.py --sweep, Llama-2-7B shapes): M <= 16 likes ~3 workgroups per
+  // CU, larger M ~1 per CU (its X tile already costs LDS); N alone filling the chip -> no split
+  const int target = nblk >= 256 ? nblk : (M <= 16 ? 768 : 256);
   int s = 1;
-  while (nblk * s < 512 && s < 16 && nck / (2 * s) >= 4) s *= 2;
+  while (nblk * s < target && s < 16 && nck / (2 * s) >= 4) s *= 2;
   *nt_out = nt;
   *splitk_out = s;
 }

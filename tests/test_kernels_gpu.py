@@ -191,3 +191,33 @@ def test_splitk_partials_fused_into_add_norm(M, N, K, rms):
     out, r_out = H.add_norm(p, nw, nb, 1e-5, rms, residual=r2)
     close(r_out, r_ref, 2e-2)
     close(out, out_ref, 3e-2)
+
+
+@pytest.mark.parametrize("V", [32000, 50257, 1000])
+def test_sample_topk_topp_sets(V):
+    """Every sampled token must lie in the reference top-k -> top-p kept set."""
+    torch.manual_seed(1)
+    B = 16
+    logits = rnd(B, V, scale=2.0)
+    temp = torch.full((B,), 0.8, device=dev)
+    topk = torch.tensor([0, 1, 5, 50, 0, 50, 100, 0] * 2, dtype=torch.int32, device=dev)
+    topp = torch.tensor([0.9, 1.0, 1.0, 0.95, 0.5, 0.8, 1.0, 1.0] * 2, device=dev)
+    allowed = []
+    for b in range(B):
+        x = logits[b].float() / 0.8
+        keep = torch.ones(V, dtype=torch.bool, device=dev)
+        k = int(topk[b])
+        if 0 < k < V:
+            keep &= x >= torch.topk(x, k).values[-1]
+        if float(topp[b]) < 1.0:
+            pr = torch.softmax(x.masked_fill(~keep, float("-inf")), -1)
+            sp, _ = pr.sort(descending=True)
+            cum = sp.cumsum(0)
+            n = int((cum - sp < float(topp[b])).sum())
+            keep &= pr >= sp[n - 1] * (1 - 1e-5)
+        allowed.append(keep)
+    for s in range(25):
+        seeds = torch.arange(B, dtype=torch.int64, device=dev) * 7777 + s
+        o = H.sample(logits, temp, topk, topp, seeds)
+        for b in range(B):
+            assert allowed[b][o[b]], (b, int(o[b]), int(topk[b]), float(topp[b]))
