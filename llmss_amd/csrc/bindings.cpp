@@ -31,8 +31,6 @@ void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk);
 void launch_add_norm_partial(const void* part, int S, int64_t slab, const void* xbias, const void* res_in,
                              void* res_out, const void* w, const void* b, void* y, int64_t y_stride, int T, int H,
                              float eps, bool rms, hipStream_t st);
-void launch_sample_fast(const void* logits, int64_t ld, bool fp32_logits, int B, int V, const void* temperature,
-                        const void* top_k, const void* top_p, const void* seeds, void* out, void* out2, hipStream_t st);
 void launch_sample(const void* logits, int64_t ld, bool fp32_logits, int B, int V, const void* temperature,
                    const void* top_k, const void* top_p, const void* seeds, void* out, void* out2, hipStream_t st);
 void launch_quant_fp8_rows(const void* w, void* q, void* scale, int64_t N, int64_t K, hipStream_t st);
@@ -85,7 +83,7 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("sample", [](uintptr_t logits, int64_t ld, bool fp32, int B, int V, uintptr_t temp, uintptr_t topk,
                      uintptr_t topp, uintptr_t seeds, uintptr_t out, uintptr_t out2, uintptr_t st) {
-    launch_sample_fast(CP(logits), ld, fp32, B, V, CP(temp), CP(topk), CP(topp), CP(seeds), P(out), P(out2), S(st));
+    launch_sample(CP(logits), ld, fp32, B, V, CP(temp), CP(topk), CP(topp), CP(seeds), P(out), P(out2), S(st));
   });
   m.def("quant_fp8_rows", [](uintptr_t w, uintptr_t q, uintptr_t scale, int64_t N, int64_t K, uintptr_t st) {
     launch_quant_fp8_rows(CP(w), P(q), P(scale), N, K, S(st));

@@ -303,61 +303,53 @@ __global__ __launch_bounds__(256, 2) void gemm_stream2_kernel(const bf16_t* __re
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) wrow[nt] = (const char*)Wv + (int64_t)min(n0 + nt * 16 + li, N - 1) * ldw * WB;
 
-  // W and X both live in 3-slot register rings: chunk c+2 is loaded during step c, chunk c+1
-  // (loaded during step c-1) is written to LDS at the end of step c, chunk c is consumed.
   u32x4 w0[NT][KC / 64][FP8W ? 1 : 2], w1[NT][KC / 64][FP8W ? 1 : 2], w2[NT][KC / 64][FP8W ? 1 : 2];
-  u32x4 x0[C::XPT], x1[C::XPT], x2[C::XPT];
+  u32x4 xr[C::XPT];
   const bool tail_k = (K % KC) != 0;
   if (cb < ce) {
-    stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, cb * KC, x0);
+    stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, cb * KC, xr);
     stream_load_w<MT, NT, KC, FP8W>(wrow, cb * KC, K, g, w0);
-    if (cb + 1 < ce) {
-      stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, (cb + 1) * KC, x1);
-      stream_load_w<MT, NT, KC, FP8W>(wrow, (cb + 1) * KC, K, g, w1);
-    }
-    stream2_store_x<MT, NT, KC, FP8W>(xs, x0);
+    if (cb + 1 < ce) stream_load_w<MT, NT, KC, FP8W>(wrow, (cb + 1) * KC, K, g, w1);
+    stream2_store_x<MT, NT, KC, FP8W>(xs, xr);
     __syncthreads();
   }
   // Steady state: branch-free steps (every prefetch valid), so hipcc's vmcnt bookkeeping stays
   // exact and it waits only for the chunk being consumed (a load under an `if` makes the counts
   // path-dependent and the compiler then drains vmcnt(0) before re-issuing - measured).
-#define STREAM2_STEADY(WCUR, WNXT2, XNXT1, XNXT2)                                                             \
+#define STREAM2_STEADY(CUR, NXT2)                                                                             \
   {                                                                                                          \
-    stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, (c + 2) * KC, XNXT2);                                     \
-    stream_load_w<MT, NT, KC, FP8W>(wrow, (c + 2) * KC, K, g, WNXT2);                                        \
+    stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, (c + 1) * KC, xr);                                        \
+    stream_load_w<MT, NT, KC, FP8W>(wrow, (c + 2) * KC, K, g, NXT2);                                         \
     __builtin_amdgcn_sched_barrier(0); /* keep the prefetch ahead of the MFMAs (hipcc sinks it) */           \
-    stream_compute<MT, NT, KC, FP8W, false>(xs + ((c - cb) & 1) * C::XBYTES, WCUR, acc, c * KC, K, li, g);   \
+    stream_compute<MT, NT, KC, FP8W, false>(xs + ((c - cb) & 1) * C::XBYTES, CUR, acc, c * KC, K, li, g);    \
     __builtin_amdgcn_sched_barrier(0);                                                                       \
-    stream2_store_x<MT, NT, KC, FP8W>(xs + ((c + 1 - cb) & 1) * C::XBYTES, XNXT1);                           \
+    stream2_store_x<MT, NT, KC, FP8W>(xs + ((c + 1 - cb) & 1) * C::XBYTES, xr);                              \
     __syncthreads();                                                                                         \
     ++c;                                                                                                     \
   }
-#define STREAM2_REM(WCUR, WNXT2, XNXT1, XNXT2)                                                                \
+#define STREAM2_REM(CUR, NXT2)                                                                                \
   {                                                                                                          \
     if (c >= ce) break;                                                                                      \
-    if (c + 2 < ce) {                                                                                        \
-      stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, (c + 2) * KC, XNXT2);                                   \
-      stream_load_w<MT, NT, KC, FP8W>(wrow, (c + 2) * KC, K, g, WNXT2);                                      \
-    }                                                                                                        \
+    if (c + 1 < ce) stream2_load_x<MT, NT, KC, FP8W>(X, ldx, M, K, (c + 1) * KC, xr);                        \
+    if (c + 2 < ce) stream_load_w<MT, NT, KC, FP8W>(wrow, (c + 2) * KC, K, g, NXT2);                         \
     const char* xb = xs + ((c - cb) & 1) * C::XBYTES;                                                        \
-    if (tail_k && c == nck - 1) stream_compute<MT, NT, KC, FP8W, true>(xb, WCUR, acc, c * KC, K, li, g);     \
-    else stream_compute<MT, NT, KC, FP8W, false>(xb, WCUR, acc, c * KC, K, li, g);                           \
-    if (c + 1 < ce) stream2_store_x<MT, NT, KC, FP8W>(xs + ((c + 1 - cb) & 1) * C::XBYTES, XNXT1);           \
+    if (tail_k && c == nck - 1) stream_compute<MT, NT, KC, FP8W, true>(xb, CUR, acc, c * KC, K, li, g);      \
+    else stream_compute<MT, NT, KC, FP8W, false>(xb, CUR, acc, c * KC, K, li, g);                            \
+    if (c + 1 < ce) stream2_store_x<MT, NT, KC, FP8W>(xs + ((c + 1 - cb) & 1) * C::XBYTES, xr);              \
     __syncthreads();                                                                                         \
     ++c;                                                                                                     \
   }
-  // slot of chunk c = (c - cb) % 3 for both rings
   int c = cb;
   for (; c + 4 < ce;) {  // 3 chunks per iteration; chunks c+2..c+4 exist -> all prefetches valid
-    STREAM2_STEADY(w0, w2, x1, x2)
-    STREAM2_STEADY(w1, w0, x2, x0)
-    STREAM2_STEADY(w2, w1, x0, x1)
+    STREAM2_STEADY(w0, w2)
+    STREAM2_STEADY(w1, w0)
+    STREAM2_STEADY(w2, w1)
   }
-  do {  // remaining <= 4 chunks (ring rotation continues at slot 0); also the K tail chunk
-    STREAM2_REM(w0, w2, x1, x2)
-    STREAM2_REM(w1, w0, x2, x0)
-    STREAM2_REM(w2, w1, x0, x1)
-    STREAM2_REM(w0, w2, x1, x2)
+  do {  // remaining <= 4 chunks (ring rotation continues at w0); also handles the K tail chunk
+    STREAM2_REM(w0, w2)
+    STREAM2_REM(w1, w0)
+    STREAM2_REM(w2, w1)
+    STREAM2_REM(w0, w2)
   } while (0);
 #undef STREAM2_STEADY
 #undef STREAM2_REM
@@ -422,103 +414,178 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 }
 
 // -------------------------------------------------------------------------------------------
-// tiled GEMM (M > 64), bf16 weights
+// tiled GEMM (prefill / large M), bf16 weights. Tile BM x BN x 64, 4 waves in 2x2, each wave
+// (BM/2) x (BN/2) = MTW x NTW mfma_f32_16x16x32 accumulators. Both operands staged by 16-byte
+// global_load_lds into an XOR-swizzled image (chunk ^= row & 7: conflict-free ds_read_b128),
+// double-buffered; XCD-aware tile order (T1). The tile is chosen per call so small-N tensor-
+// parallel shards still produce >= ~256 workgroups (128x128, 64x128 or 64x64).
 // -------------------------------------------------------------------------------------------
-constexpr int TBM = 128, TBN = 128, TBK = 64;
+constexpr int TBK = 64;
 
+template <int BM, int BN>
 __device__ __forceinline__ void tiled_stage(const bf16_t* __restrict__ A, int64_t lda, int M, const bf16_t* __restrict__ B,
                                             int64_t ldb, int N, int K, int m0, int n0, int k0, char* sA, char* sB,
                                             int w, int lane) {
+  // one wave-instruction = 1 KiB = 8 rows x 128 B; A needs BM/8 of them, B BN/8 (4 waves share)
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
+  for (int it = 0; it < BM / 32; ++it) {
     const int inst = it * 4 + w;
     const int row = inst * 8 + (lane >> 3);
     const int c = (lane & 7) ^ (row & 7);
     const int kc = min(k0 + c * 8, K - 8);
     const bf16_t* ga = A + (int64_t)min(m0 + row, M - 1) * lda + kc;
-    const bf16_t* gb = B + (int64_t)min(n0 + row, N - 1) * ldb + kc;
     __builtin_amdgcn_global_load_lds((const void*)ga, (LDS_AS void*)(sA + inst * 1024), 16, 0, 0);
+  }
+#pragma unroll
+  for (int it = 0; it < BN / 32; ++it) {
+    const int inst = it * 4 + w;
+    const int row = inst * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (row & 7);
+    const int kc = min(k0 + c * 8, K - 8);
+    const bf16_t* gb = B + (int64_t)min(n0 + row, N - 1) * ldb + kc;
     __builtin_amdgcn_global_load_lds((const void*)gb, (LDS_AS void*)(sB + inst * 1024), 16, 0, 0);
   }
 }
 
-template <bool MASK>
-__device__ __forceinline__ void tiled_compute(const char* sA, const char* sB, f32x4 (&acc)[4][4], int wr, int wc, int li,
-                                              int g, int k0, int K) {
+template <int MTW, int NTW, bool MASK>
+__device__ __forceinline__ void tiled_compute(const char* sA, const char* sB, f32x4 (&acc)[MTW][NTW], int wr, int wc,
+                                              int li, int g, int k0, int K) {
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const int c = 4 * s + g;
     const bool valid = !MASK || (k0 + c * 8 < K);
-    s16x8 a[4], b[4];
+    const s16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+    s16x8 a[MTW], b[NTW];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int ra = wr * 64 + t * 16 + li, rb = wc * 64 + t * 16 + li;
+    for (int t = 0; t < MTW; ++t) {
+      const int ra = wr * (MTW * 16) + t * 16 + li;
       a[t] = *reinterpret_cast<const s16x8*>(sA + ra * 128 + ((c ^ (ra & 7)) << 4));
-      b[t] = *reinterpret_cast<const s16x8*>(sB + rb * 128 + ((c ^ (rb & 7)) << 4));
-      if (MASK && !valid) { a[t] = s16x8{0, 0, 0, 0, 0, 0, 0, 0}; b[t] = a[t]; }
+      if (MASK && !valid) a[t] = z;
     }
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int t = 0; t < NTW; ++t) {
+      const int rb = wc * (NTW * 16) + t * 16 + li;
+      b[t] = *reinterpret_cast<const s16x8*>(sB + rb * 128 + ((c ^ (rb & 7)) << 4));
+      if (MASK && !valid) b[t] = z;
+    }
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+    for (int mt = 0; mt < MTW; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
   }
 }
 
+// s_waitcnt vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 encoding: vmcnt[3:0] + [15:14])
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Barrier that lets global_load_lds stay in flight across it: __syncthreads()' release fence
+// would emit vmcnt(0) and drain the prefetch (guide: "Pipelining across barriers").
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int BM, int BN, int NS>
 __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                          const bf16_t* __restrict__ B, int64_t ldb,
                                                          const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
-                                                         int64_t ldy, int M, int N, int K, int act, int glu) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TBM * TBK * 2];  // 64 KiB
+                                                         int64_t ldy, float* __restrict__ part, int M, int N, int K,
+                                                         int act, int glu) {
+  constexpr int MTW = BM / 32, NTW = BN / 32;  // 16x16 tiles per wave
+  constexpr int A_BYTES = BM * TBK * 2, B_BYTES = BN * TBK * 2, STAGE = A_BYTES + B_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int li = lane & 15, g = lane >> 4;
   const int wr = w >> 1, wc = w & 1;
-  const int ntn = (N + TBN - 1) / TBN, ntm = (M + TBM - 1) / TBM;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
   const int tile = xcd_remap(blockIdx.x, ntn * ntm);
-  const int m0 = (tile / ntn) * TBM, n0 = (tile % ntn) * TBN;
+  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
 
-  f32x4 acc[4][4];
+  f32x4 acc[MTW][NTW];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < MTW; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < NTW; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (K + TBK - 1) / TBK;
-  constexpr int TILE_BYTES = TBM * TBK * 2;  // one operand tile; buffer c: A at 2c, B at 2c+1
-  tiled_stage(A, lda, M, B, ldb, N, K, m0, n0, 0, smem, smem + TILE_BYTES, w, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int t = 0; t < nk; ++t) {
-    const int cur = t & 1;
-    char* nA = smem + (2 * (cur ^ 1)) * TILE_BYTES;
-    char* cA = smem + (2 * cur) * TILE_BYTES;
-    if (t + 1 < nk) tiled_stage(A, lda, M, B, ldb, N, K, m0, n0, (t + 1) * TBK, nA, nA + TILE_BYTES, w, lane);
-    if (t + 1 == nk && (K % TBK)) tiled_compute<true>(cA, cA + TILE_BYTES, acc, wr, wc, li, g, t * TBK, K);
-    else tiled_compute<false>(cA, cA + TILE_BYTES, acc, wr, wc, li, g, t * TBK, K);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  // split-K (grid.y): slice z covers k-tiles [t0, t1); partial sums go to part[z] (fp32)
+  const int nk_all = (K + TBK - 1) / TBK;
+  const int per = (nk_all + gridDim.y - 1) / gridDim.y;
+  const int t0 = blockIdx.y * per, t1 = min(nk_all, t0 + per);
+  if constexpr (NS == 2) {
+    if (t0 < t1) {
+      tiled_stage<BM, BN>(A, lda, M, B, ldb, N, K, m0, n0, t0 * TBK, smem, smem + A_BYTES, w, lane);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    for (int t = t0; t < t1; ++t) {
+      const int cur = (t - t0) & 1;
+      char* nA = smem + (cur ^ 1) * STAGE;
+      char* cA = smem + cur * STAGE;
+      if (t + 1 < t1) tiled_stage<BM, BN>(A, lda, M, B, ldb, N, K, m0, n0, (t + 1) * TBK, nA, nA + A_BYTES, w, lane);
+      if (t + 1 == nk_all && (K % TBK)) tiled_compute<MTW, NTW, true>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
+      else tiled_compute<MTW, NTW, false>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    // 3-stage ring: stage t+2 is issued while stage t is computed; the wait before compute only
+    // covers stage t (the younger stage's LOADS instructions stay in flight): no per-step drain.
+    constexpr int LOADS = BM / 32 + BN / 32;  // global_load_lds per wave per stage
+    if (t0 < t1) tiled_stage<BM, BN>(A, lda, M, B, ldb, N, K, m0, n0, t0 * TBK, smem, smem + A_BYTES, w, lane);
+    if (t0 + 1 < t1)
+      tiled_stage<BM, BN>(A, lda, M, B, ldb, N, K, m0, n0, (t0 + 1) * TBK, smem + STAGE, smem + STAGE + A_BYTES, w, lane);
+    int cur = 0;
+    for (int t = t0; t < t1; ++t) {
+      if (t + 1 < t1) wait_vmcnt<LOADS>();
+      else wait_vmcnt<0>();
+      lds_barrier();  // stage t visible; every wave is past compute(t-1), so its buffer is free
+      char* cA = smem + cur * STAGE;
+      const int nxt = cur == 0 ? 2 : cur - 1;  // (cur + 2) % 3
+      if (t + 2 < t1) {
+        char* nA = smem + nxt * STAGE;
+        tiled_stage<BM, BN>(A, lda, M, B, ldb, N, K, m0, n0, (t + 2) * TBK, nA, nA + A_BYTES, w, lane);
+      }
+      if (t + 1 == nk_all && (K % TBK)) tiled_compute<MTW, NTW, true>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
+      else tiled_compute<MTW, NTW, false>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
+      cur = cur == 2 ? 0 : cur + 1;
+    }
   }
-  // epilogue
+  // epilogue (C layout: col = lane&15 -> n, row = 4*(lane>>4)+i -> m)
+  const int wn0 = n0 + wc * (NTW * 16);
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
+  for (int mt = 0; mt < MTW; ++mt) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wr * 64 + mt * 16 + 4 * g + i;
+      const int m = m0 + wr * (MTW * 16) + mt * 16 + 4 * g + i;
       if (m >= M) continue;
-      if (glu) {
+      if (part) {
+        float* pr = part + ((int64_t)blockIdx.y * M + m) * N;
 #pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const int ng = n0 + wc * 64 + 2 * p * 16 + li, nu = ng + 16;
+        for (int nt = 0; nt < NTW; ++nt) {
+          const int n = wn0 + nt * 16 + li;
+          if (n < N) pr[n] = acc[mt][nt][i];
+        }
+      } else if (glu) {
+#pragma unroll
+        for (int p = 0; p < NTW / 2; ++p) {
+          const int ng = wn0 + 2 * p * 16 + li, nu = ng + 16;
           if (nu < N) {
             float gv = acc[mt][2 * p][i], uv = acc[mt][2 * p + 1][i];
             if (bias) { gv += bf2f(bias[ng]); uv += bf2f(bias[nu]); }
-            Y[(int64_t)m * ldy + (n0 + wc * 64) / 2 + p * 16 + li] = f2bf(silu(gv) * uv);
+            Y[(int64_t)m * ldy + wn0 / 2 + p * 16 + li] = f2bf(silu(gv) * uv);
           }
         }
       } else {
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          const int n = n0 + wc * 64 + nt * 16 + li;
+        for (int nt = 0; nt < NTW; ++nt) {
+          const int n = wn0 + nt * 16 + li;
           if (n < N) {
             float v = acc[mt][nt][i];
             if (bias) v += bf2f(bias[n]);
@@ -603,6 +670,10 @@ int gemm_skinny_splitk(int M, int N, int K) {
   return s;
 }
 
+int launch_tiled(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, const bf16_t* B, bf16_t* Y, int64_t ldy,
+                 int M, int N, int K, int act, int g, int tsel, int split_hint, void* workspace, int64_t ws_bytes,
+                 bool partial_out, hipStream_t st);
+
 // Returns the number of fp32 partial slabs [S, M, N] left in `workspace` (partial_out and the
 // planner chose split-K: the consumer - add_norm - reduces them and adds `bias`), or 0 when Y
 // holds the finished bf16 output.
@@ -617,7 +688,7 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_f
   auto Y = (bf16_t*)y;
   auto WS = (const float*)w_scale;
   const int g = glu ? 1 : 0;
-  const bool stream = M <= 128 || w_fp8;
+  const bool stream = w_fp8 || (M <= 16 && (nt_hint >> 8) == 0) || (nt_hint & 0xff);
   if (stream) {
     if (M > 128) {  // fp8 weights with many rows (prefill): 128-row panels through the streaming kernel
       for (int m0 = 0; m0 < M; m0 += 128) {
@@ -630,7 +701,7 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_f
     int nt, splitk;
     gemm_stream_plan(M, N, K, &nt, &splitk);
     // nt_hint = nt + 16 * variant (variant 1: LDS-DMA X staging, 2: register-staged X + W ring)
-    int variant = (nt_hint >> 4) ? (nt_hint >> 4) : 2;
+    int variant = ((nt_hint >> 4) & 15) ? ((nt_hint >> 4) & 15) : 2;
     nt_hint &= 15;
     if (nt_hint > 0) nt = nt_hint;
     if (split_hint > 0) splitk = split_hint;
@@ -650,17 +721,82 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_f
     }
     return 0;
   }
-  const int nwg = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
-  gemm_tiled_kernel<<<nwg, 256, 0, st>>>(X, ldx, (const bf16_t*)w, ldw, B, Y, ldy, M, N, K, act, g);
+  return launch_tiled(X, ldx, (const bf16_t*)w, ldw, B, Y, ldy, M, N, K, act, g, nt_hint >> 8, split_hint, workspace,
+                      ws_bytes, partial_out, st);
+}
+
+// Tiled-path plan. Tile: 64 rows for M <= 64 (64x64, or 64x128 when 64x64 gives > 256 tiles),
+// else 128x128. K is split until the grid holds ~3 (64-row tiles) or ~1.5 (128x128) workgroups
+// per CU, keeping >= 512 k per slice. Measured on the Llama-2-7B shapes at M = 64..512
+// (bench/gemm_bench.py --sweep): within ~5% of the best (tile, split) of the sweep everywhere.
+static int tiles_of(int M, int N, int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); }
+static int tile_dims(int tsel, int* bm, int* bn) {
+  *bm = tsel == 1 ? 128 : 64;
+  *bn = tsel == 3 ? 64 : 128;
+  return 0;
+}
+void gemm_tiled_plan(int M, int N, int K, int* tsel_io, int* split_io) {
+  int tsel = *tsel_io;
+  if (tsel == 0) tsel = M <= 64 ? (tiles_of(M, N, 64, 64) > 256 ? 2 : 3) : 1;
+  const int hint_bits = tsel & ~15;
+  tsel &= 15;
+  int bm, bn;
+  tile_dims(tsel, &bm, &bn);
+  const int nt = tiles_of(M, N, bm, bn);
+  int s = *split_io;
+  if (s <= 0) {
+    const int bound = bm == 64 ? 800 : 537;
+    s = 1;
+    while (nt * s * 2 <= bound && s < 8 && K / (2 * s) >= 512) s *= 2;
+  }
+  s = std::max(1, std::min(s, (K + TBK - 1) / TBK));
+  // 3-stage LDS ring when the grid is too small for block-level latency hiding (measured: o/down
+  // projections and the LM head at M <= 128 gain 10-20%; wide grids lose occupancy to its LDS)
+  if (*tsel_io == 0 && nt * s <= (bm == 64 ? 600 : 256)) tsel |= 16;
+  *tsel_io = tsel | hint_bits;
+  *split_io = s;
+}
+
+int launch_tiled(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, const bf16_t* B, bf16_t* Y, int64_t ldy,
+                 int M, int N, int K, int act, int g, int tsel, int split_hint, void* workspace, int64_t ws_bytes,
+                 bool partial_out, hipStream_t st) {
+  int s = split_hint;
+  gemm_tiled_plan(M, N, K, &tsel, &s);
+  const int ns = (tsel >> 4) & 1 ? 3 : 2;  // 3-stage LDS ring
+  tsel &= 15;
+  int bm, bn;
+  tile_dims(tsel, &bm, &bn);
+  const int nt = tiles_of(M, N, bm, bn);
+  if ((int64_t)s * M * N * 4 > ws_bytes) s = 1;
+  float* part = s > 1 ? (float*)workspace : nullptr;
+  const int act_k = s > 1 ? 0 : act, glu_k = s > 1 ? 0 : g;
+  dim3 grid(nt, s);
+#define LT(BM_, BN_, NS_) \
+  gemm_tiled_kernel<BM_, BN_, NS_><<<grid, 256, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N, K, act_k, glu_k)
+  if (ns == 3) {
+    if (tsel == 1) LT(128, 128, 3); else if (tsel == 2) LT(64, 128, 3); else LT(64, 64, 3);
+  } else {
+    if (tsel == 1) LT(128, 128, 2); else if (tsel == 2) LT(64, 128, 2); else LT(64, 64, 2);
+  }
+#undef LT
   HIP_CHECK_LAUNCH();
+  if (s > 1 && partial_out && !g && act == 0) return s;
+  if (s > 1) {
+    const int nout = g ? N / 2 : N;
+    dim3 rgrid(std::min((nout + 255) / 256, 64), M);
+    splitk_reduce_kernel<<<rgrid, 256, 0, st>>>(part, s, M, N, B, Y, ldy, act, g);
+    HIP_CHECK_LAUNCH();
+  }
   return 0;
 }
 
 void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk) {
-  if (M <= 128 || w_fp8) {
+  if (w_fp8 || M <= 16) {
     gemm_stream_plan(std::min(M, 128), N, K, nt, splitk);
   } else {
-    *nt = 0;
-    *splitk = 1;
+    int tsel = 0, s = 0;
+    gemm_tiled_plan(M, N, K, &tsel, &s);
+    *nt = tsel << 8;
+    *splitk = s;
   }
 }

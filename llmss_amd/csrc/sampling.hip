@@ -150,185 +150,6 @@ __global__ __launch_bounds__(1024) void sample_kernel(const T* __restrict__ logi
   }
 }
 
-// ----------------------------------------------------------------------------------------------
-// v2 (bf16 logits, V <= 1024 * 8 * CPT): the row lives in registers (one read of the logits);
-// thresholds come from a 16-way bisection over the 32-bit order-preserving key space (8 passes,
-// exact), each pass = 15 per-thread counts (or exp-masses) + one block reduction - no contended
-// LDS atomics (the v1 radix histograms serialise on the few exponent bins real logits occupy).
-// ----------------------------------------------------------------------------------------------
-template <int CPT>
-__device__ __forceinline__ void block_reduce15(float (&v)[15], float* red /* [16][16] */) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-#pragma unroll
-  for (int j = 0; j < 15; ++j) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v[j] += __shfl_xor(v[j], o, 64);
-  }
-  __syncthreads();
-  if (lane < 15) {
-    float mine = 0.f;
-#pragma unroll
-    for (int j = 0; j < 15; ++j) mine = (lane == j) ? v[j] : mine;
-    red[wid * 16 + lane] = mine;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 15; ++j) {
-    float t = 0.f;
-    for (int w = 0; w < nw; ++w) t += red[w * 16 + j];
-    v[j] = t;
-  }
-}
-
-// Largest key threshold t with weight{key >= t} >= target (weights: 1 or e[i]); keys <= floor masked.
-template <int CPT, bool MASS>
-__device__ unsigned bisect_keys(const float (&x)[CPT * 8], float mx, float target, unsigned floor_key, float* red) {
-  unsigned long long lo = floor_key, hi = 0x100000000ull;
-  while (hi - lo > 1) {
-    const unsigned long long step = (hi - lo + 15) / 16;
-    unsigned t[15];  // 32-bit thresholds (saturated): no 64-bit compares in the hot loop
-#pragma unroll
-    for (int j = 0; j < 15; ++j) {
-      const unsigned long long tj = lo + (j + 1) * step;
-      t[j] = tj > 0xFFFFFFFFull ? 0xFFFFFFFFu : (unsigned)tj;
-    }
-    float cnt[15];
-#pragma unroll
-    for (int j = 0; j < 15; ++j) cnt[j] = 0.f;
-    for (int i = 0; i < CPT * 8; ++i) {
-      const unsigned k = fkey(x[i]);  // recomputed: keeps VGPRs low at 1024 threads
-      const float wgt = MASS ? __expf(x[i] - mx) : 1.f;
-#pragma unroll
-      for (int j = 0; j < 15; ++j) cnt[j] += (k >= t[j]) ? wgt : 0.f;
-    }
-    // a saturated threshold (> 0xFFFFFFFF) must count nothing
-#pragma unroll
-    for (int j = 0; j < 15; ++j)
-      if (lo + (j + 1) * step > 0xFFFFFFFFull) cnt[j] = 0.f;
-    block_reduce15<CPT>(cnt, red);
-    int jb = 0;  // number of thresholds that still meet the target (monotone in j)
-#pragma unroll
-    for (int j = 0; j < 15; ++j) jb += (cnt[j] >= target) ? 1 : 0;
-    const unsigned long long nlo = lo + jb * step;
-    hi = (jb == 15) ? hi : lo + (jb + 1) * step;
-    lo = nlo;
-    if (hi > 0x100000000ull) hi = 0x100000000ull;
-  }
-  return (unsigned)lo;
-}
-
-template <int CPT>
-__global__ __launch_bounds__(1024) void sample_v2_kernel(const bf16_t* __restrict__ logits, int64_t ld, int V,
-                                                         const float* __restrict__ temperature,
-                                                         const int* __restrict__ top_k, const float* __restrict__ top_p,
-                                                         const int64_t* __restrict__ seeds, int64_t* __restrict__ out,
-                                                         int64_t* __restrict__ out2) {
-  __shared__ float red[16 * 16];
-  __shared__ int redi[16];
-  const int b = blockIdx.x;
-  const bf16_t* row = logits + b * ld;
-  const float temp = temperature ? temperature[b] : 0.f;
-  const int k = top_k ? top_k[b] : 0;
-  const float p = top_p ? top_p[b] : 1.f;
-  const bool greedy = !(temp > 0.f) || k == 1;
-  const float scale = greedy ? 1.f : 1.f / temp;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-
-  float x[CPT * 8];
-#pragma unroll
-  for (int c = 0; c < CPT; ++c) {
-    const int ch = threadIdx.x + c * 1024;
-    if (ch * 8 < V) {
-      const u16x8 v = *reinterpret_cast<const u16x8*>(row + ch * 8);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[c * 8 + j] = (ch * 8 + j < V) ? bf2f(v[j]) * scale : -INFINITY;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[c * 8 + j] = -INFINITY;
-    }
-  }
-  unsigned thr = 0;
-  if (!greedy) {
-    float mx = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < CPT * 8; ++i) mx = fmaxf(mx, x[i]);
-    mx = block_max(mx, red);
-    if (k > 0 && k < V) thr = bisect_keys<CPT, false>(x, mx, (float)k, 0u, red);
-    if (p < 1.f) {
-      float z = 0.f;
-#pragma unroll
-      for (int i = 0; i < CPT * 8; ++i) z += fkey(x[i]) >= thr ? __expf(x[i] - mx) : 0.f;
-      __syncthreads();
-      z = block_sum(z, red);
-      const unsigned tp = bisect_keys<CPT, true>(x, mx, p * z, thr, red);
-      thr = tp > thr ? tp : thr;
-    }
-  }
-  const unsigned long long seed = seeds ? (unsigned long long)seeds[b] : 0ull;
-  const unsigned s0 = (unsigned)seed, s1 = (unsigned)(seed >> 32);
-  float best = -INFINITY;
-  int besti = 0x7fffffff;
-#pragma unroll
-  for (int c = 0; c < CPT; ++c) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int i = (threadIdx.x + c * 1024) * 8 + j;
-      const float xv = x[c * 8 + j];
-      float v = xv;
-      bool keep = i < V;
-      if (!greedy) {
-        keep = keep && fkey(xv) >= thr;
-        const unsigned r = philox((unsigned)i, 0u, s0, s1);
-        const float u = ((float)(r >> 8) + 0.5f) * (1.0f / 16777216.0f);
-        v = xv - __logf(-__logf(u));
-      }
-      if (keep && (v > best || (v == best && i < besti))) { best = v; besti = i; }
-    }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ob = __shfl_xor(best, o, 64);
-    const int oi = __shfl_xor(besti, o, 64);
-    if (ob > best || (ob == best && oi < besti)) { best = ob; besti = oi; }
-  }
-  __syncthreads();
-  if (lane == 0) { red[wid] = best; redi[wid] = besti; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float bb = red[0];
-    int bi = redi[0];
-    for (int i = 1; i < (int)(blockDim.x >> 6); ++i)
-      if (red[i] > bb || (red[i] == bb && redi[i] < bi)) { bb = red[i]; bi = redi[i]; }
-    if (bi >= V) bi = 0;
-    out[b] = bi;
-    if (out2) out2[b] = bi;
-  }
-}
-
-void launch_sample(const void* logits, int64_t ld, bool fp32_logits, int B, int V, const void* temperature,
-                   const void* top_k, const void* top_p, const void* seeds, void* out, void* out2, hipStream_t st);
-
-void launch_sample_fast(const void* logits, int64_t ld, bool fp32_logits, int B, int V, const void* temperature,
-                        const void* top_k, const void* top_p, const void* seeds, void* out, void* out2,
-                        hipStream_t st) {
-  if (B == 0) return;
-  const bool aligned = (ld % 8 == 0) && ((uintptr_t)logits % 16 == 0);
-  const int chunks = (V + 7) / 8;
-  if (fp32_logits || !aligned || chunks > 8 * 1024) {
-    launch_sample(logits, ld, fp32_logits, B, V, temperature, top_k, top_p, seeds, out, out2, st);
-    return;
-  }
-  auto L = (const bf16_t*)logits;
-  auto T = (const float*)temperature;
-  auto TK = (const int*)top_k;
-  auto TP = (const float*)top_p;
-  auto S = (const int64_t*)seeds;
-  if (chunks <= 2048) sample_v2_kernel<2><<<B, 1024, 0, st>>>(L, ld, V, T, TK, TP, S, (int64_t*)out, (int64_t*)out2);
-  else if (chunks <= 4096) sample_v2_kernel<4><<<B, 1024, 0, st>>>(L, ld, V, T, TK, TP, S, (int64_t*)out, (int64_t*)out2);
-  else sample_v2_kernel<8><<<B, 1024, 0, st>>>(L, ld, V, T, TK, TP, S, (int64_t*)out, (int64_t*)out2);
-  HIP_CHECK_LAUNCH();
-}
-
 void launch_sample(const void* logits, int64_t ld, bool fp32_logits, int B, int V, const void* temperature,
                    const void* top_k, const void* top_p, const void* seeds, void* out, void* out2, hipStream_t st) {
   if (B == 0) return;

@@ -29,6 +29,8 @@ from .. import _native, ops
 from ..models.decoder import DecoderLM, StepInput
 from ..ops import hip as _hip_ops
 from ..utils.logging import get_logger
+from ..utils.tracing import PhaseTimer
+from ..utils.tracing import range as trace_range
 from .sampling import SamplingParams, step_seed
 
 log = get_logger(__name__)
@@ -137,6 +139,7 @@ class LLMEngine:
         self.check_tokens = check_tokens if check_tokens is not None else os.environ.get("LLMSS_CHECK_TOKENS") == "1"
         self.stats = {"steps": 0, "prefill_steps": 0, "decode_steps": 0, "tokens": 0, "prefill_tokens": 0,
                       "preemptions": 0, "decode_time_s": 0.0, "prefill_time_s": 0.0}
+        self.timer = PhaseTimer()  # LLMSS_TIMING=1: HIP-event device time per phase; LLMSS_ROCTX=1: roctx ranges
         self.use_graphs = self.is_gpu if use_graphs is None else (use_graphs and self.is_gpu)
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.buckets = sorted(set(graph_buckets or self._default_buckets()))
@@ -218,7 +221,8 @@ class LLMEngine:
         return temp, topk, topp, seeds
 
     def step(self) -> List[StepEvent]:
-        batch = self.sched.schedule()
+        with trace_range("schedule"):
+            batch = self.sched.schedule()
         if batch.kind == 0:
             return []
         for rid in batch.preempted.tolist():
@@ -227,11 +231,13 @@ class LLMEngine:
         reqs = [self.requests[i] for i in ids]
         t0 = time.perf_counter()
         if batch.kind == 1:
-            tokens = self._prefill(batch, reqs)
+            with self.timer.phase("prefill"):
+                tokens = self._prefill(batch, reqs)
             self.stats["prefill_steps"] += 1
             self.stats["prefill_tokens"] += int(batch.query_lens.sum())
         else:
-            tokens = self._decode(batch, reqs)
+            with self.timer.phase("decode"):
+                tokens = self._decode(batch, reqs)
             self.stats["decode_steps"] += 1
         if self.check_tokens and self.tp.is_real:
             allt = self.tp.all_gather_object(tokens)
@@ -312,6 +318,10 @@ class LLMEngine:
         self.buf.h_out[:n].copy_(self.buf.out[:n], non_blocking=True)
         torch.cuda.current_stream().synchronize()
         return self.buf.h_out[:n].tolist()
+
+    def phase_summary(self) -> Dict[str, Dict[str, float]]:
+        """Per-phase device time (LLMSS_TIMING=1) - {"prefill": {...}, "decode": {...}}."""
+        return self.timer.summary()
 
     # -------------------------------------------------------------------------- graphs
     def capture_graphs(self):

@@ -121,6 +121,21 @@ def test_gemm(M, N, K):
         close(H.linear(x, w, None, glu=True), R.linear(x.float(), w.float(), None, glu=True), 2e-2)
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3])  # 128x128, 64x128, 64x64
+@pytest.mark.parametrize("stages", [2, 3])
+@pytest.mark.parametrize("split", [1, 3, 8])
+@pytest.mark.parametrize("M,N,K", [(64, 1536, 4096), (200, 4800, 1600), (37, 256, 64 * 5 + 16)])
+def test_gemm_tiled_variants(tile, stages, split, M, N, K):
+    torch.manual_seed(0)
+    x, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
+    b = rnd(N, scale=0.1)
+    hint = (tile | (16 if stages == 3 else 0)) << 8
+    ref = R.linear(x.float(), w.float(), b.float(), act="gelu_tanh")
+    close(H.linear(x, w, b, act="gelu_tanh", nt_hint=hint, split_hint=split), ref, 2e-2)
+    close(H.linear(x, w, None, glu=True, nt_hint=hint, split_hint=split),
+          R.linear(x.float(), w.float(), None, glu=True), 2e-2)
+
+
 @pytest.mark.parametrize("M", [1, 8, 64, 100])
 def test_gemm_fp8(M):
     torch.manual_seed(0)
