@@ -48,9 +48,13 @@ def make_tokenizer(path: str, vocab: int):
     tok = Tokenizer(models.BPE())
     tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
     tok.decoder = decoders.ByteLevel()
-    trainer = trainers.BpeTrainer(vocab_size=vocab, special_tokens=["<|endoftext|>"],
-                                  initial_alphabet=pre_tokenizers.ByteLevel.alphabet()[: vocab - 1])
     corpus = ["hello world, this is a tiny corpus for an offline tokenizer."] * 50
+    # deterministic alphabet that covers the corpus: ByteLevel.alphabet() is an unordered set, and a
+    # corpus symbol left out of the first vocab-1 entries would get an id >= vocab
+    used = sorted({c for w, _ in tok.pre_tokenizer.pre_tokenize_str(corpus[0]) for c in w})
+    rest = [c for c in sorted(pre_tokenizers.ByteLevel.alphabet()) if c not in used]
+    trainer = trainers.BpeTrainer(vocab_size=vocab, special_tokens=["<|endoftext|>"],
+                                  initial_alphabet=(used + rest)[: vocab - 1])
     tok.train_from_iterator(corpus, trainer)
     fast = PreTrainedTokenizerFast(tokenizer_object=tok, eos_token="<|endoftext|>", pad_token="<|endoftext|>")
     fast.save_pretrained(path)
