@@ -68,8 +68,10 @@ def main():
                 cfgs = [(0, 0)]
                 if a.sweep and M <= 128:  # nt_hint = nt + 16 * variant (1: LDS-DMA X, 2: register X + W ring)
                     cfgs += [(nt + 16 * v, sp) for v, nt, sp in itertools.product([1, 2], [1, 2], [1, 2, 4, 8])]
-                if a.sweep and 32 <= M <= 1024 and not a.fp8:  # tiled kernel: nt_hint = tile << 8 (1: 128x128, 2: 64x128, 3: 64x64)
+                if a.sweep and 32 <= M <= 512 and not a.fp8:  # tiled kernel: nt_hint = tile << 8 (1: 128x128, 2: 64x128, 3: 64x64)
                     cfgs += [((t | st) << 8, sp) for t, st, sp in itertools.product([1, 2, 3], [0, 16], [1, 2, 4, 8])]
+                if a.sweep and M >= 256 and not a.fp8:
+                    cfgs += [(4 << 8, 1), (1 << 8, 1)]
                 best = None
                 for nt, sp in cfgs:
                     try:

@@ -598,6 +598,149 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
 }
 
 // -------------------------------------------------------------------------------------------
+// big-tile GEMM (prefill, M >= ~1024): 256x256x64 tile, 8 waves (2 x 4), each wave 128x64 =
+// 8x4 mfma_f32_16x16x32 accumulators (AGPRs). LDS = 2 buffers x {A rows 0-127, A rows 128-255,
+// B rows 0-127, B rows 128-255} of 16 KiB = 128 KiB -> one workgroup per CU.
+// Per K-tile t: (1) counted vmcnt(8) retires stage t while stage t+1 stays in flight, raw
+// barrier; (2) every wave reads ALL its fragments of tile t into VGPRs (24 ds_read_b128) and
+// runs the first k-half of its MFMAs; (3) barrier (lgkmcnt(0): all reads of buffer t&1 done) and
+// stage t+2 is issued into that same buffer, then the second k-half of MFMAs. Prefetch distance
+// is therefore ~1.5 K-tiles of MFMA time and no barrier ever drains the DMA queue (guide:
+// "Pipelining across barriers", 3-buffer-equivalent depth in 2 buffers).
+// Requires K % 64 == 0; rows beyond M / N are clamped on load and masked on store.
+// -------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                          const bf16_t* __restrict__ B, int64_t ldb,
+                                                          const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
+                                                          int64_t ldy, int M, int N, int K, int act, int glu) {
+  constexpr int HALF = 16384, BUF = 4 * HALF;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  const int wr = w >> 2, wc = w & 3;
+  const int ntn = (N + 255) / 256, ntm = (M + 255) / 256;
+  const int tile = xcd_remap(blockIdx.x, ntn * ntm);
+  const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
+  const int nk = K / 64;
+
+  // staging: half h (0,1: A rows 128h.., 2,3: B rows 128(h-2)..), 2 x 1-KiB glds per wave; lane ->
+  // row inst*8 + lane/8, LDS chunk lane&7 holding global chunk (lane&7) ^ (row&7) (swizzle on source)
+  const bf16_t* src[4] = {A, A, B, B};
+  const int64_t ld[4] = {lda, lda, ldb, ldb};
+  int64_t soff[4][2];
+  int lofs[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int inst = i * 8 + w;
+    const int row = inst * 8 + (lane >> 3);
+    const int gc = (lane & 7) ^ (row & 7);
+    lofs[i] = inst * 1024;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const bool isA = h < 2;
+      const int lim = isA ? M : N;
+      const int r = min((isA ? m0 : n0) + (h & 1) * 128 + row, lim - 1);
+      soff[h][i] = (int64_t)r * ld[h] + gc * 8;
+    }
+  }
+  auto stage = [&](int t, char* buf) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(src[h] + soff[h][i] + t * 64),
+                                         (LDS_AS void*)(buf + h * HALF + lofs[i]), 16, 0, 0);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets (bytes within a buffer): A half wr, B half wc>>1 (+64 rows for odd wc)
+  int aoff[8][2], boff[4][2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int c = 4 * s + g;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int r = m * 16 + li;
+      aoff[m][s] = wr * HALF + r * 128 + ((c ^ (r & 7)) << 4);
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int r = (wc & 1) * 64 + n * 16 + li;
+      boff[n][s] = (2 + (wc >> 1)) * HALF + r * 128 + ((c ^ (r & 7)) << 4);
+    }
+  }
+
+  stage(0, smem);
+  if (nk > 1) stage(1, smem + BUF);
+  for (int t = 0; t < nk; ++t) {
+    char* cur = smem + (t & 1) * BUF;
+    if (t + 1 < nk) wait_vmcnt<8>();
+    else wait_vmcnt<0>();
+    lds_barrier();  // stage t landed for every wave
+    s16x8 a[8][2], b[4][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int n = 0; n < 4; ++n) b[n][s] = *reinterpret_cast<const s16x8*>(cur + boff[n][s]);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) a[m][s] = *reinterpret_cast<const s16x8*>(cur + aoff[m][s]);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][0], b[n][0], acc[m][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    lds_barrier();  // every wave's reads of this buffer are complete -> restage it
+    if (t + 2 < nk) stage(t + 2, cur);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][1], b[n][1], acc[m][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  }
+
+  // epilogue (C layout: col = lane&15 -> n, row = 4*(lane>>4)+i -> m)
+  const int wn0 = n0 + wc * 64;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = m0 + wr * 128 + m * 16 + 4 * g + i;
+      if (row >= M) continue;
+      if (glu) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int ng = wn0 + 2 * p * 16 + li, nu = ng + 16;
+          if (nu < N) {
+            float gv = acc[m][2 * p][i], uv = acc[m][2 * p + 1][i];
+            if (bias) { gv += bf2f(bias[ng]); uv += bf2f(bias[nu]); }
+            Y[(int64_t)row * ldy + wn0 / 2 + p * 16 + li] = f2bf(silu(gv) * uv);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          const int col = wn0 + n * 16 + li;
+          if (col < N) {
+            float v = acc[m][n][i];
+            if (bias) v += bf2f(bias[col]);
+            Y[(int64_t)row * ldy + col] = f2bf(apply_act(v, act));
+          }
+        }
+      }
+    }
+  }
+}
+
+// -------------------------------------------------------------------------------------------
 // host dispatch
 // -------------------------------------------------------------------------------------------
 template <int MT, int NT, int KC, bool FP8W, int VARIANT>
@@ -737,9 +880,18 @@ static int tile_dims(int tsel, int* bm, int* bn) {
 }
 void gemm_tiled_plan(int M, int N, int K, int* tsel_io, int* split_io) {
   int tsel = *tsel_io;
-  if (tsel == 0) tsel = M <= 64 ? (tiles_of(M, N, 64, 64) > 256 ? 2 : 3) : 1;
+  if (tsel == 0) {
+    if (K % 64 == 0 && tiles_of(M, N, 256, 256) >= 192) tsel = 4;
+    else tsel = M <= 64 ? (tiles_of(M, N, 64, 64) > 256 ? 2 : 3) : 1;
+  }
+  if (tsel == 4 && K % 64) tsel = 1;
   const int hint_bits = tsel & ~15;
   tsel &= 15;
+  if (tsel == 4) {  // big-tile kernel: no split-K, no stage option
+    *tsel_io = 4;
+    *split_io = 1;
+    return;
+  }
   int bm, bn;
   tile_dims(tsel, &bm, &bn);
   const int nt = tiles_of(M, N, bm, bn);
@@ -770,6 +922,11 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, con
   if ((int64_t)s * M * N * 4 > ws_bytes) s = 1;
   float* part = s > 1 ? (float*)workspace : nullptr;
   const int act_k = s > 1 ? 0 : act, glu_k = s > 1 ? 0 : g;
+  if (tsel == 4) {
+    gemm_big_kernel<<<tiles_of(M, N, 256, 256), 512, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, M, N, K, act, g);
+    HIP_CHECK_LAUNCH();
+    return 0;
+  }
   dim3 grid(nt, s);
 #define LT(BM_, BN_, NS_) \
   gemm_tiled_kernel<BM_, BN_, NS_><<<grid, 256, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N, K, act_k, glu_k)
