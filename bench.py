@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--fp8", action="store_true")
     ap.add_argument("--greedy", action="store_true")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--simulate-tp", type=int, default=0,
+                    help="dev tool: one process computes rank 0 of a TP=N shard plan with no communication "
+                         "(per-rank compute time at TP=N shapes; not a headline number)")
     args = ap.parse_args()
 
     from llmss_amd.engine import LLMEngine, SamplingParams, build_model
@@ -47,8 +50,14 @@ def main():
     tp, rank, world = initialize_distributed()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.simulate_tp > 1:
+        from llmss_amd.parallel.dist import TPGroup
+
+        if world != 1:
+            raise SystemExit("--simulate-tp runs in a single process")
+        tp = TPGroup(0, args.simulate_tp, fake=True)
     dev = torch.device("cuda", torch.cuda.current_device())
-    batch = args.batch_per_gpu * world
+    batch = args.batch_per_gpu * max(world, args.simulate_tp)
     model = build_model(args.model, tp, "bf16", dev, fp8=args.fp8, random_init=True)
     max_len = min(model.cfg.max_position_embeddings, max(256, args.prompt_len + args.gen_len))
     eng = LLMEngine(model, max_num_seqs=batch, max_batched_tokens=max(8192, batch * args.prompt_len),
@@ -77,6 +86,11 @@ def main():
 
     progress(f"engine ready: {model.cfg.model_type} tp={world} batch={batch} kv_blocks={eng.num_blocks} "
              f"graphs={sorted(eng.graphs)}")
+    if eng.tuned:
+        mx = max(m for _, m in eng.tuned)
+        progress("autotuned GEMMs at M=%d: " % mx + ", ".join(
+            f"{n} {nt:#x}/s{sp} {t:.1f}us (static {t0:.1f})" for (n, m), (nt, sp, t, t0) in sorted(eng.tuned.items())
+            if m == mx))
     for i in range(args.warmup):
         t = time.perf_counter()
         one_step()
@@ -119,9 +133,10 @@ def main():
             "p50_ttft_ms": round(float(ttft), 3),
             "p50_request_latency_ms": round(float(e2e), 3),
             "config": {"model": args.model, "global_batch": batch, "seq_len": args.prompt_len + args.gen_len,
-                       "prompt_len": args.prompt_len, "gen_len": args.gen_len, "parallelism": f"tp{world}",
+                       "prompt_len": args.prompt_len, "gen_len": args.gen_len, "parallelism": (f"tp{args.simulate_tp}-simulated-no-comm" if args.simulate_tp > 1 else f"tp{world}"),
                        "sampling": "greedy" if args.greedy else "temperature=1.0,top_p=0.95,top_k=50",
-                       "engine_stats": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()}},
+                       "engine_stats": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()},
+                       **({"phase_ms": eng.phase_summary()} if eng.timer.enabled else {})},
         }))
     if tp.is_real:
         torch.distributed.destroy_process_group()

@@ -69,7 +69,14 @@ def main():
                 if a.sweep and M <= 128:  # nt_hint = nt + 16 * variant (1: LDS-DMA X, 2: register X + W ring)
                     cfgs += [(nt + 16 * v, sp) for v, nt, sp in itertools.product([1, 2], [1, 2], [1, 2, 4, 8])]
                 if a.sweep and 32 <= M <= 512 and not a.fp8:  # tiled kernel: nt_hint = tile << 8 (1: 128x128, 2: 64x128, 3: 64x64)
+                    # tile << 8 | depth code << 12 (depth 2, 3, 4, 6)
                     cfgs += [((t | st) << 8, sp) for t, st, sp in itertools.product([1, 2, 3], [0, 16], [1, 2, 4, 8])]
+                    cfgs += [((t | st) << 8, sp) for t, st, sp in itertools.product([2, 3], [32], [1, 2, 4, 8])]
+                    cfgs += [((3 | 48) << 8, sp) for sp in [1, 2, 4, 8]]
+                if a.sweep and M <= 128 and not a.fp8:  # planner's choice with default-policy weight loads
+                    pnt, psp = H.lib().gemm_plan(M, N, K, False)
+                    if pnt >= 256:
+                        cfgs += [(pnt | (64 << 8), psp)]
                 if a.sweep and M >= 256 and not a.fp8:
                     cfgs += [(4 << 8, 1), (1 << 8, 1)]
                 best = None

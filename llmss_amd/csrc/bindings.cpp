@@ -16,7 +16,8 @@ void launch_embed(const void* ids, const void* pos, const void* wte, const void*
                   int vocab, hipStream_t st);
 void launch_rope_cache(void* qkv, int64_t row_stride, const void* pos, const void* cos_t, const void* sin_t, void* kc,
                        void* vc, const void* slot, int T, int nh, int nkv, int D, int rot, int block_size, int k_off,
-                       int v_off, int style, bool do_rope, hipStream_t st);
+                       int v_off, int style, bool do_rope, const void* part, int S, int64_t slab, const void* bias,
+                       hipStream_t st);
 void launch_attn_decode(const void* q, int64_t q_stride, const void* kc, const void* vc, const void* block_tables,
                         int bt_stride, const void* ctx_lens, void* out, int64_t out_stride, void* part_o,
                         void* part_ml, int B, int nh, int nkv, int D, int block_size, int nsplit, int part_size,
@@ -28,6 +29,9 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_f
                 const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace,
                 int64_t ws_bytes, int nt_hint, int split_hint, bool partial_out, hipStream_t st);
 void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk);
+void gemm_tuned_set(int M, int N, int K, bool glu, bool fp8, int nt_hint, int split);
+void gemm_tuned_clear();
+bool gemm_tuned_get(int M, int N, int K, bool glu, bool fp8, int* nt_hint, int* split);
 void launch_add_norm_partial(const void* part, int S, int64_t slab, const void* xbias, const void* res_in,
                              void* res_out, const void* w, const void* b, void* y, int64_t y_stride, int T, int H,
                              float eps, bool rms, hipStream_t st);
@@ -51,9 +55,10 @@ PYBIND11_MODULE(_C, m) {
                     uintptr_t st) { launch_embed(CP(ids), CP(pos), CP(wte), CP(wpe), P(out), T, H, V, S(st)); });
   m.def("rope_cache", [](uintptr_t qkv, int64_t rs, uintptr_t pos, uintptr_t cos_t, uintptr_t sin_t, uintptr_t kc,
                          uintptr_t vc, uintptr_t slot, int T, int nh, int nkv, int D, int rot, int bs, int k_off,
-                         int v_off, int style, bool do_rope, uintptr_t st) {
+                         int v_off, int style, bool do_rope, uintptr_t part, int nslab, int64_t slab, uintptr_t bias,
+                         uintptr_t st) {
     launch_rope_cache(P(qkv), rs, CP(pos), CP(cos_t), CP(sin_t), P(kc), P(vc), CP(slot), T, nh, nkv, D, rot, bs, k_off,
-                      v_off, style, do_rope, S(st));
+                      v_off, style, do_rope, CP(part), nslab, slab, CP(bias), S(st));
   });
   m.def("attn_decode", [](uintptr_t q, int64_t qs, uintptr_t kc, uintptr_t vc, uintptr_t bt, int bts, uintptr_t cl,
                           uintptr_t out, int64_t os, uintptr_t po, uintptr_t pml, int B, int nh, int nkv, int D, int bs,
@@ -74,6 +79,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_plan", [](int M, int N, int K, bool fp8) {
     int nt, s;
     gemm_plan(M, N, K, fp8, &nt, &s);
+    return py::make_tuple(nt, s);
+  });
+  m.def("gemm_tuned_set", &gemm_tuned_set);
+  m.def("gemm_tuned_clear", &gemm_tuned_clear);
+  m.def("gemm_tuned_get", [](int M, int N, int K, bool glu, bool fp8) -> py::object {
+    int nt, s;
+    if (!gemm_tuned_get(M, N, K, glu, fp8, &nt, &s)) return py::none();
     return py::make_tuple(nt, s);
   });
   m.def("add_norm_partial", [](uintptr_t part, int S, int64_t slab, uintptr_t xbias, uintptr_t ri, uintptr_t ro,

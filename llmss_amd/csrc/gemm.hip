@@ -20,6 +20,9 @@
 //    simulator), double-buffered, XCD-aware tile order (guide T1).
 #include "common.h"
 
+#include <mutex>
+#include <unordered_map>
+
 // -------------------------------------------------------------------------------------------
 // helpers
 // -------------------------------------------------------------------------------------------
@@ -422,7 +425,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // -------------------------------------------------------------------------------------------
 constexpr int TBK = 64;
 
-template <int BM, int BN>
+template <int BM, int BN, bool WNT = false>
 __device__ __forceinline__ void tiled_stage(const bf16_t* __restrict__ A, int64_t lda, int M, const bf16_t* __restrict__ B,
                                             int64_t ldb, int N, int K, int m0, int n0, int k0, char* sA, char* sB,
                                             int w, int lane) {
@@ -443,7 +446,8 @@ __device__ __forceinline__ void tiled_stage(const bf16_t* __restrict__ A, int64_
     const int c = (lane & 7) ^ (row & 7);
     const int kc = min(k0 + c * 8, K - 8);
     const bf16_t* gb = B + (int64_t)min(n0 + row, N - 1) * ldb + kc;
-    __builtin_amdgcn_global_load_lds((const void*)gb, (LDS_AS void*)(sB + inst * 1024), 16, 0, 0);
+    // weights read once per step (single M tile): non-temporal (aux = 2), guide 'nt-weights'
+    __builtin_amdgcn_global_load_lds((const void*)gb, (LDS_AS void*)(sB + inst * 1024), 16, 0, WNT ? 2 : 0);
   }
 }
 
@@ -483,6 +487,17 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// wait until at most min(younger, MAXY) stages of LOADS instructions each are outstanding
+template <int LOADS, int MAXY>
+__device__ __forceinline__ void wait_vmcnt_upto(int younger) {
+  if constexpr (MAXY <= 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (younger >= MAXY) wait_vmcnt<LOADS * MAXY>();
+    else wait_vmcnt_upto<LOADS, MAXY - 1>(younger);
+  }
+}
+
 // Barrier that lets global_load_lds stay in flight across it: __syncthreads()' release fence
 // would emit vmcnt(0) and drain the prefetch (guide: "Pipelining across barriers").
 __device__ __forceinline__ void lds_barrier() {
@@ -491,7 +506,7 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int BM, int BN, int NS>
+template <int BM, int BN, int NS, bool WNT>
 __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                          const bf16_t* __restrict__ B, int64_t ldb,
                                                          const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
@@ -520,7 +535,7 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
   const int t0 = blockIdx.y * per, t1 = min(nk_all, t0 + per);
   if constexpr (NS == 2) {
     if (t0 < t1) {
-      tiled_stage<BM, BN>(A, lda, M, B, ldb, N, K, m0, n0, t0 * TBK, smem, smem + A_BYTES, w, lane);
+      tiled_stage<BM, BN, WNT>(A, lda, M, B, ldb, N, K, m0, n0, t0 * TBK, smem, smem + A_BYTES, w, lane);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
@@ -528,33 +543,34 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
       const int cur = (t - t0) & 1;
       char* nA = smem + (cur ^ 1) * STAGE;
       char* cA = smem + cur * STAGE;
-      if (t + 1 < t1) tiled_stage<BM, BN>(A, lda, M, B, ldb, N, K, m0, n0, (t + 1) * TBK, nA, nA + A_BYTES, w, lane);
+      if (t + 1 < t1) tiled_stage<BM, BN, WNT>(A, lda, M, B, ldb, N, K, m0, n0, (t + 1) * TBK, nA, nA + A_BYTES, w, lane);
       if (t + 1 == nk_all && (K % TBK)) tiled_compute<MTW, NTW, true>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
       else tiled_compute<MTW, NTW, false>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
   } else {
-    // 3-stage ring: stage t+2 is issued while stage t is computed; the wait before compute only
-    // covers stage t (the younger stage's LOADS instructions stay in flight): no per-step drain.
+    // NS-stage ring: stage t+NS-1 is issued while stage t is computed; the wait before compute
+    // only covers stage t (the younger stages' LOADS instructions each stay in flight): no drain.
     constexpr int LOADS = BM / 32 + BN / 32;  // global_load_lds per wave per stage
-    if (t0 < t1) tiled_stage<BM, BN>(A, lda, M, B, ldb, N, K, m0, n0, t0 * TBK, smem, smem + A_BYTES, w, lane);
-    if (t0 + 1 < t1)
-      tiled_stage<BM, BN>(A, lda, M, B, ldb, N, K, m0, n0, (t0 + 1) * TBK, smem + STAGE, smem + STAGE + A_BYTES, w, lane);
+#pragma unroll
+    for (int j = 0; j < NS - 1; ++j)
+      if (t0 + j < t1)
+        tiled_stage<BM, BN, WNT>(A, lda, M, B, ldb, N, K, m0, n0, (t0 + j) * TBK, smem + j * STAGE,
+                            smem + j * STAGE + A_BYTES, w, lane);
     int cur = 0;
     for (int t = t0; t < t1; ++t) {
-      if (t + 1 < t1) wait_vmcnt<LOADS>();
-      else wait_vmcnt<0>();
+      wait_vmcnt_upto<LOADS, NS - 2>(t1 - 1 - t);  // stages younger than t still in flight
       lds_barrier();  // stage t visible; every wave is past compute(t-1), so its buffer is free
       char* cA = smem + cur * STAGE;
-      const int nxt = cur == 0 ? 2 : cur - 1;  // (cur + 2) % 3
-      if (t + 2 < t1) {
+      const int nxt = cur == 0 ? NS - 1 : cur - 1;  // (cur + NS - 1) % NS
+      if (t + NS - 1 < t1) {
         char* nA = smem + nxt * STAGE;
-        tiled_stage<BM, BN>(A, lda, M, B, ldb, N, K, m0, n0, (t + 2) * TBK, nA, nA + A_BYTES, w, lane);
+        tiled_stage<BM, BN, WNT>(A, lda, M, B, ldb, N, K, m0, n0, (t + NS - 1) * TBK, nA, nA + A_BYTES, w, lane);
       }
       if (t + 1 == nk_all && (K % TBK)) tiled_compute<MTW, NTW, true>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
       else tiled_compute<MTW, NTW, false>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
-      cur = cur == 2 ? 0 : cur + 1;
+      cur = cur == NS - 1 ? 0 : cur + 1;
     }
   }
   // epilogue (C layout: col = lane&15 -> n, row = 4*(lane>>4)+i -> m)
@@ -820,10 +836,39 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, con
 // Returns the number of fp32 partial slabs [S, M, N] left in `workspace` (partial_out and the
 // planner chose split-K: the consumer - add_norm - reduces them and adds `bias`), or 0 when Y
 // holds the finished bf16 output.
+// Autotuned plans: (M, N, K, glu, fp8) -> (nt_hint, split) measured by llmss_amd/ops/autotune.py
+// for the shapes an engine will actually run (decode batch buckets x layer GEMMs). Consulted by
+// every call without explicit hints and by gemm_plan, so split-K partial fusion stays consistent.
+namespace {
+std::mutex g_tuned_mu;
+std::unordered_map<uint64_t, std::pair<int, int>> g_tuned;
+uint64_t tune_key(int M, int N, int K, bool glu, bool fp8) {
+  return ((uint64_t)M << 43) | ((uint64_t)N << 22) | ((uint64_t)K << 2) | (glu ? 2u : 0u) | (fp8 ? 1u : 0u);
+}
+}  // namespace
+
+void gemm_tuned_set(int M, int N, int K, bool glu, bool fp8, int nt_hint, int split) {
+  std::lock_guard<std::mutex> lk(g_tuned_mu);
+  g_tuned[tune_key(M, N, K, glu, fp8)] = {nt_hint, split};
+}
+void gemm_tuned_clear() {
+  std::lock_guard<std::mutex> lk(g_tuned_mu);
+  g_tuned.clear();
+}
+bool gemm_tuned_get(int M, int N, int K, bool glu, bool fp8, int* nt_hint, int* split) {
+  std::lock_guard<std::mutex> lk(g_tuned_mu);
+  auto it = g_tuned.find(tune_key(M, N, K, glu, fp8));
+  if (it == g_tuned.end()) return false;
+  *nt_hint = it->second.first;
+  *split = it->second.second;
+  return true;
+}
+
 int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_fp8, const void* w_scale,
                 const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace,
                 int64_t ws_bytes, int nt_hint, int split_hint, bool partial_out, hipStream_t st) {
   if (M == 0 || N == 0) return 0;
+  if (nt_hint == 0 && split_hint == 0) gemm_tuned_get(M, N, K, glu, w_fp8, &nt_hint, &split_hint);
   if (K % 16) throw std::runtime_error("gemm: K must be a multiple of 16");
   if (glu && (N % 32)) throw std::runtime_error("gemm: glu needs N % 32 == 0");
   auto X = (const bf16_t*)x;
@@ -878,8 +923,15 @@ static int tile_dims(int tsel, int* bm, int* bn) {
   *bn = tsel == 3 ? 64 : 128;
   return 0;
 }
-void gemm_tiled_plan(int M, int N, int K, int* tsel_io, int* split_io) {
+void gemm_tiled_plan(int M, int N, int K, int* tsel_io, int* split_io, bool glu) {
   int tsel = *tsel_io;
+  // SwiGLU output cannot be folded into the next kernel, so a split would cost its own reduce
+  // launch: with >= 256 64x64 tiles, no split (measured equal or better at M <= 128)
+  if (tsel == 0 && glu && M <= 128 && tiles_of(M, N, 64, 64) >= 256 && *split_io <= 0) {
+    *tsel_io = 3 | 16;
+    *split_io = 1;
+    return;
+  }
   if (tsel == 0) {
     if (K % 64 == 0 && tiles_of(M, N, 256, 256) >= 192) tsel = 4;
     else tsel = M <= 64 ? (tiles_of(M, N, 64, 64) > 256 ? 2 : 3) : 1;
@@ -912,10 +964,14 @@ void gemm_tiled_plan(int M, int N, int K, int* tsel_io, int* split_io) {
 int launch_tiled(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, const bf16_t* B, bf16_t* Y, int64_t ldy,
                  int M, int N, int K, int act, int g, int tsel, int split_hint, void* workspace, int64_t ws_bytes,
                  bool partial_out, hipStream_t st) {
+  const int tsel_raw = tsel;
   int s = split_hint;
-  gemm_tiled_plan(M, N, K, &tsel, &s);
-  const int ns = (tsel >> 4) & 1 ? 3 : 2;  // 3-stage LDS ring
+  gemm_tiled_plan(M, N, K, &tsel, &s, g != 0);
+  static constexpr int kDepth[4] = {2, 3, 4, 6};
+  int ns = kDepth[(tsel >> 4) & 3];  // LDS ring depth (hint bits 4-5); bit 6: default-policy weights
   tsel &= 15;
+  if (tsel == 1 && ns > 3) ns = 3;  // 128x128 x 4 stages would exceed the 160 KiB LDS
+  if (tsel == 2 && ns > 4) ns = 4;
   int bm, bn;
   tile_dims(tsel, &bm, &bn);
   const int nt = tiles_of(M, N, bm, bn);
@@ -928,10 +984,23 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, con
     return 0;
   }
   dim3 grid(nt, s);
-#define LT(BM_, BN_, NS_) \
-  gemm_tiled_kernel<BM_, BN_, NS_><<<grid, 256, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N, K, act_k, glu_k)
+  // non-temporal weight staging when every weight tile is read by exactly one workgroup row
+  const bool wnt = !(tsel_raw & 64) && M <= bm;
+#define LT(BM_, BN_, NS_)                                                                                          \
+  do {                                                                                                             \
+    if (wnt)                                                                                                       \
+      gemm_tiled_kernel<BM_, BN_, NS_, true><<<grid, 256, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N, K, act_k, \
+                                                                    glu_k);                                         \
+    else                                                                                                           \
+      gemm_tiled_kernel<BM_, BN_, NS_, false><<<grid, 256, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N, K, act_k, \
+                                                                     glu_k);                                        \
+  } while (0)
   if (ns == 3) {
     if (tsel == 1) LT(128, 128, 3); else if (tsel == 2) LT(64, 128, 3); else LT(64, 64, 3);
+  } else if (ns == 4) {
+    if (tsel == 2) LT(64, 128, 4); else LT(64, 64, 4);
+  } else if (ns == 6) {
+    LT(64, 64, 6);
   } else {
     if (tsel == 1) LT(128, 128, 2); else if (tsel == 2) LT(64, 128, 2); else LT(64, 64, 2);
   }
@@ -948,11 +1017,18 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, con
 }
 
 void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk) {
+  if (gemm_tuned_get(M, N, K, false, w_fp8, nt, splitk)) {
+    if (*nt >> 8) {  // tiled hint: the split the kernel will really use
+      int tsel = *nt >> 8;
+      gemm_tiled_plan(M, N, K, &tsel, splitk, false);
+    }
+    return;
+  }
   if (w_fp8 || M <= 16) {
     gemm_stream_plan(std::min(M, 128), N, K, nt, splitk);
   } else {
     int tsel = 0, s = 0;
-    gemm_tiled_plan(M, N, K, &tsel, &s);
+    gemm_tiled_plan(M, N, K, &tsel, &s, false);
     *nt = tsel << 8;
     *splitk = s;
   }

@@ -118,7 +118,8 @@ class LLMEngine:
     def __init__(self, model: DecoderLM, *, max_num_seqs: int = 256, max_batched_tokens: int = 8192,
                  block_size: int = 16, num_blocks: Optional[int] = None, max_model_len: Optional[int] = None,
                  kv_fraction: float = 0.9, use_graphs: Optional[bool] = None, eos_token_id: Optional[int] = None,
-                 graph_buckets: Optional[Sequence[int]] = None, check_tokens: Optional[bool] = None):
+                 graph_buckets: Optional[Sequence[int]] = None, check_tokens: Optional[bool] = None,
+                 autotune: Optional[bool] = None):
         self.model = model
         self.cfg = model.cfg
         self.tp = model.tp
@@ -153,8 +154,23 @@ class LLMEngine:
                 nsplit, _ = self._splits(b)
                 if nsplit > 1:
                     _hip_ops._DECODE_WS.get(b, model.plan.nh_l, nsplit, self.cfg.head_dim, self.device)
+        if autotune is None:
+            autotune = os.environ.get("LLMSS_AUTOTUNE", "1") != "0"
+        self.tuned = {}
+        if self.is_gpu and autotune:  # per-shape GEMM plans for every decode bucket (ops/autotune.py)
+            from ..ops.autotune import tune_model
+
+            self.tuned = tune_model(model, self.buckets)
+        if self.use_graphs and os.environ.get("LLMSS_GRAPHS", "1") == "0":
+            self.use_graphs = False
         if self.use_graphs:
-            self.capture_graphs()
+            try:
+                self.capture_graphs()
+            except RuntimeError as e:  # e.g. a collective backend that refuses stream capture
+                log.warning("decode graph capture failed (%s): running decode eagerly", e)
+                torch.cuda.synchronize()
+                self.graphs.clear()
+                self.use_graphs = False
 
     # -------------------------------------------------------------------------- sizing
     def _default_buckets(self):
@@ -286,7 +302,8 @@ class LLMEngine:
         logits = self.model(inp, self.kv)
         temp, topk, topp, seeds = self._sampling_arrays(reqs)
         tok = ops.sample(logits, torch.from_numpy(temp).to(dev), torch.from_numpy(topk).to(dev),
-                         torch.from_numpy(topp).to(dev), torch.from_numpy(seeds).to(dev), vocab=self.cfg.vocab_size)
+                         torch.from_numpy(topp).to(dev), torch.from_numpy(seeds).to(dev),
+                         vocab=min(self.cfg.vocab_size, logits.shape[-1]))
         return tok.cpu().tolist()
 
     def _decode_forward(self, b: int, buf: _DecodeBuffers):
@@ -294,8 +311,8 @@ class LLMEngine:
                         block_tables=buf.bt[:b], ctx_lens=buf.ctx[:b], max_ctx=self.max_model_len,
                         decode_splits=self._splits(b))
         logits = self.model(inp, self.kv)
-        _hip_ops.sample(logits, buf.temp[:b], buf.topk[:b], buf.topp[:b], buf.seeds[:b], vocab=self.cfg.vocab_size,
-                        out=buf.out[:b])
+        _hip_ops.sample(logits, buf.temp[:b], buf.topk[:b], buf.topp[:b], buf.seeds[:b],
+                        vocab=min(self.cfg.vocab_size, logits.shape[-1]), out=buf.out[:b])
 
     def _decode(self, batch, reqs: List[Request]) -> List[int]:
         n = len(reqs)
@@ -308,7 +325,7 @@ class LLMEngine:
                             block_tables=torch.from_numpy(batch.block_table.astype(np.int32)),
                             ctx_lens=torch.from_numpy(batch.ctx_lens.astype(np.int32)), max_ctx=self.max_model_len)
             logits = self.model(inp, self.kv)
-            return ops.sample(logits, temp, topk, topp, seeds, vocab=self.cfg.vocab_size).tolist()
+            return ops.sample(logits, temp, topk, topp, seeds, vocab=min(self.cfg.vocab_size, logits.shape[-1])).tolist()
         b = next(x for x in self.buckets if x >= n)
         self.buf.fill(b, ids, batch.positions, batch.slots, seeds, batch.ctx_lens, topk, batch.block_table, temp, topp)
         if self.use_graphs and b in self.graphs:

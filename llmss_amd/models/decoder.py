@@ -81,8 +81,8 @@ class DecoderLM:
     def _attention(self, qkv, inp: StepInput, kc, vc):
         cfg, p = self.cfg, self.plan
         D = cfg.head_dim
-        ops.rope_cache(qkv, inp.positions, self.w.cos, self.w.sin, kc, vc, inp.slots, p.nh_l, p.nkv_l, D,
-                       cfg.rotary_dim, cfg.rope_style, do_rope=cfg.position == "rope")
+        qkv = ops.rope_cache(qkv, inp.positions, self.w.cos, self.w.sin, kc, vc, inp.slots, p.nh_l, p.nkv_l, D,
+                             cfg.rotary_dim, cfg.rope_style, do_rope=cfg.position == "rope")
         if inp.kind == "prefill":
             return ops.attn_prefill(qkv, inp.cu_seqlens, inp.max_seqlen, p.nh_l, p.nkv_l, D, self.scale)
         return ops.attn_decode(qkv, kc, vc, inp.block_tables, inp.ctx_lens, p.nh_l, p.nkv_l, D, self.scale,
@@ -94,11 +94,12 @@ class DecoderLM:
         x = ops.embed(inp.input_ids, w.wte, inp.positions if w.wpe is not None else None, w.wpe)
         residual = None
         delta = x
-        fuse = not self.tp.is_real  # split-K partials can skip their own reduce only without a TP all-reduce
+        fuse = self.tp.size == 1  # split-K partials can skip their own reduce only without a TP all-reduce
         for i, L in enumerate(w.layers):
             kc, vc = kv_caches[i]
             y, residual = ops.add_norm(delta, L.ln1_w, L.ln1_b, eps, rms, residual)
-            a = self._attention(L.qkv(y), inp, kc, vc)
+            # column-parallel QKV: its split-K partials are summed inside the rope/cache kernel
+            a = self._attention(L.qkv(y, partial_ok=True), inp, kc, vc)
             o = L.o(a, partial_ok=fuse and not cfg.parallel_block)
             if cfg.parallel_block:
                 m = L.down(L.up(y, self.act))

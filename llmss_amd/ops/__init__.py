@@ -38,9 +38,11 @@ def embed(ids, wte, positions=None, wpe=None):
 
 
 def rope_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, rot, style, do_rope=True):
+    """Returns the (rotated) bf16 qkv tensor; ``qkv`` may be a GPU split-K PartialSum."""
     if qkv.is_cuda:
         return _hip().rope_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, rot, style, do_rope)
-    return ref.rope_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, rot, style, do_rope)
+    ref.rope_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, rot, style, do_rope)
+    return qkv
 
 
 def attn_prefill(qkv, cu_seqlens, max_seqlen, nh, nkv, D, scale):

@@ -1,0 +1,161 @@
+"""GEMM autotuner for the shapes an engine runs (decode batch buckets x layer projections).
+
+The static planner in ``csrc/gemm.hip`` is a good default, but the best (kernel, tile, LDS ring
+depth, split-K) choice for a memory-bound decode GEMM moves with M, N and K by 10-40% in ways a
+rule does not capture (``bench/gemm_bench.py --sweep``). At engine start every decode shape is
+timed over a candidate list and the winner goes into the native plan table, which every later
+call (and HIP-graph capture) uses without hints.
+
+Timing streams the weights from HBM the way a decode step does: candidates rotate over enough
+weight copies (> 2x the 256 MiB Infinity Cache) that no call hits a cached tile. When the layer's
+consumer reduces split-K partials itself (QKV -> rope, o/down -> add_norm at TP=1), the GEMM is
+timed without its reduce and charged the consumer's extra slab reads instead.
+"""
+from __future__ import annotations
+
+import itertools
+import math
+import time
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ..utils.logging import get_logger
+
+log = get_logger(__name__)
+
+_SLAB_READ_BPS = 4.0e12  # consumer-side fp32 partial reads (add_norm / rope), bytes/s
+
+
+@dataclass(frozen=True)
+class GemmShape:
+    N: int
+    K: int
+    glu: bool = False
+    fp8: bool = False
+    partial: bool = False  # consumer sums split-K slabs itself
+    act: str = "none"
+
+
+def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, int]]:
+    """(nt_hint, split) pairs; nt_hint encodings are documented in csrc/gemm.hip launch_gemm."""
+    out: List[Tuple[int, int]] = []
+    splits = (1, 2, 4, 8)
+    if fp8 or M <= 32:  # weight-streaming kernels: nt + 16 * variant
+        out += [(nt + 16 * v, s) for v, nt, s in itertools.product((1, 2), (1, 2), splits)]
+    if fp8:
+        return out
+    # tiled: tile << 8 | depth code << 12   (tile 1: 128x128, 2: 64x128, 3: 64x64; depth 2/3/4/6)
+    tiles = [(3, (0, 16, 32, 48)), (2, (0, 16, 32))]
+    if M > 32:
+        tiles.append((1, (0, 16)))
+    for t, depths in tiles:
+        for d in depths:
+            out += [((t | d) << 8, s) for s in splits]
+    if M >= 256 and K % 64 == 0:
+        out.append((4 << 8, 1))
+    return out
+
+
+def _time(fn, iters: int) -> float:
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for i in range(iters):
+        fn(i)
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) * 1e3 / iters  # us
+
+
+def tune_shape(M: int, shape: GemmShape, device, weight_budget: int = 600 << 20, iters: int = 6,
+               cands: Optional[Sequence[Tuple[int, int]]] = None) -> Tuple[int, int, float, float]:
+    """Best (nt_hint, split, us, default_us) for one shape."""
+    from . import hip as H
+
+    N, K = shape.N, shape.K
+    wbytes = N * K * (1 if shape.fp8 else 2)
+    ncopy = max(2, min(64, math.ceil(weight_budget / wbytes)))
+    g = torch.Generator(device=device)
+    g.manual_seed(1234)
+    x = (torch.randn(M, K, device=device, generator=g) * 0.5).to(torch.bfloat16)
+    if shape.fp8:
+        base = torch.randint(0, 120, (N, K), device=device, dtype=torch.uint8, generator=g)
+        ws = [base.clone() for _ in range(ncopy)]
+        sc = torch.full((N,), 1e-2, device=device)
+    else:
+        base = (torch.randn(N, K, device=device, generator=g) * K ** -0.5).to(torch.bfloat16)
+        ws = [base.clone() for _ in range(ncopy)]
+        sc = None
+    nout = N // 2 if shape.glu else N
+    y = torch.empty(M, nout, dtype=torch.bfloat16, device=device)
+    partial = shape.partial and not shape.glu and shape.act in ("none", None)
+
+    def run(nt, s):
+        def f(i):
+            r = H.linear(x, ws[i % ncopy], None, shape.act, shape.glu, sc, out=None if partial else y,
+                         nt_hint=nt, split_hint=s, partial_ok=partial)
+            return r
+        return f
+
+    def cost(nt, s):
+        f = run(nt, s)
+        r = f(0)
+        slabs = r.S if isinstance(r, H.PartialSum) else 0
+        for i in range(2):
+            f(i)
+        t = min(_time(f, iters), _time(f, iters))
+        return t + (slabs * M * N * 4 / _SLAB_READ_BPS * 1e6 if slabs else 0.0)
+
+    default = cost(0, 0)
+    best = (0, 0, default)
+    for nt, s in (cands if cands is not None else candidates(M, N, K, shape.glu, shape.fp8)):
+        try:
+            t = cost(nt, s)
+        except (ValueError, RuntimeError):  # config rejected by host-side validation
+            continue
+        if t < best[2] * 0.98:  # prefer the static plan unless a candidate is clearly faster
+            best = (nt, s, t)
+    del ws
+    return best[0], best[1], best[2], default
+
+
+def model_shapes(model) -> Dict[str, GemmShape]:
+    """The per-layer projections of a DecoderLM (layer 0 is representative) + the LM head."""
+    L = model.w.layers[0]
+    fuse = model.tp.size == 1 and not model.cfg.parallel_block
+    act = model.act if not L.up.glu else "none"
+    out = {
+        "qkv": GemmShape(L.qkv.w.shape[0], L.qkv.w.shape[1], False, L.qkv.w_scale is not None, True),
+        "o": GemmShape(L.o.w.shape[0], L.o.w.shape[1], False, L.o.w_scale is not None, fuse),
+        "up": GemmShape(L.up.w.shape[0], L.up.w.shape[1], L.up.glu, L.up.w_scale is not None, False, act),
+        "down": GemmShape(L.down.w.shape[0], L.down.w.shape[1], False, L.down.w_scale is not None, fuse),
+    }
+    head = model.w.head
+    out["head"] = GemmShape(head.w.shape[0], head.w.shape[1], False, head.w_scale is not None, False)
+    return out
+
+
+def tune_model(model, ms: Sequence[int], native=None) -> Dict[Tuple[str, int], Tuple[int, int, float, float]]:
+    """Tune every (shape, M) pair and install the winners in the native plan table."""
+    from .. import _native
+
+    lib = native or _native()
+    dev = model.device
+    t0 = time.perf_counter()
+    res = {}
+    done = {}
+    for name, shp in model_shapes(model).items():
+        for M in sorted(set(int(m) for m in ms)):
+            key = (M, shp)
+            if key not in done:
+                done[key] = tune_shape(M, shp, dev)
+            nt, s, t, t0_us = done[key]
+            if nt:
+                lib.gemm_tuned_set(M, shp.N, shp.K, shp.glu, shp.fp8, nt, s)
+            res[(name, M)] = done[key]
+    torch.cuda.synchronize(dev)
+    gain = sum(v[3] - v[2] for v in res.values())
+    log.info("autotuned %d GEMM shapes in %.1fs (sum of per-call gains %.1f us)", len(res),
+             time.perf_counter() - t0, gain)
+    return res

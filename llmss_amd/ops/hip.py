@@ -94,6 +94,15 @@ def embed(ids, wte, positions=None, wpe=None, out=None):
 
 # ------------------------------------------------------------------------------ rope + cache
 def rope_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, rot, style, do_rope=True):
+    """Rotate q/k in place and write k/v to the paged cache; returns the bf16 qkv tensor.
+
+    ``qkv`` may be a :class:`PartialSum` (split-K slabs of the QKV GEMM): the kernel then sums the
+    slabs (+ bias) itself and writes the finished rows into a fresh bf16 qkv tensor.
+    """
+    part = qkv if isinstance(qkv, PartialSum) else None
+    if part is not None:
+        _check(part.N == (nh + 2 * nkv) * D, "partial qkv width")
+        qkv = torch.empty(part.M, part.N, dtype=torch.bfloat16, device=part.device)
     T = qkv.shape[0]
     _bf16_rows(qkv, "qkv")
     _check(qkv.shape[1] >= (nh + 2 * nkv) * D, "qkv too narrow")
@@ -113,7 +122,10 @@ def rope_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, ro
     lib().rope_cache(qkv.data_ptr(), qkv.stride(0), positions.data_ptr(), _ptr(cos) if do_rope else 0,
                      _ptr(sin) if do_rope else 0, _ptr(k_cache), _ptr(v_cache),
                      _ptr(slots) if k_cache is not None else 0, T, nh, nkv, D, rot,
-                     bs, nh * D, (nh + nkv) * D, 1 if style == "gptj" else 0, bool(do_rope and rot > 0), _stream())
+                     bs, nh * D, (nh + nkv) * D, 1 if style == "gptj" else 0, bool(do_rope and rot > 0),
+                     part.buf.data_ptr() if part else 0, part.S if part else 0, part.M * part.N if part else 0,
+                     _ptr(part.bias) if part else 0, _stream())
+    return qkv
 
 
 # -------------------------------------------------------------------------------- attention

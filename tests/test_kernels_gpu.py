@@ -75,6 +75,29 @@ def test_rope_cache(style, D, rot, nh, nkv):
     close(vc1, vc2, 0)
 
 
+@pytest.mark.parametrize("style,T", [("neox", 40), ("gptj", 7), ("neox", 300)])
+def test_rope_cache_from_split_k_partials(style, T):
+    """QKV GEMM leaves split-K slabs; the rope kernel sums them (+bias) - same result as the unfused path."""
+    torch.manual_seed(0)
+    D, nh, nkv, K, bs, nb = 128, 8, 2, 4096, 16, 32
+    N = (nh + 2 * nkv) * D
+    x, w, b = rnd(T, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
+    pos = torch.randint(0, 100, (T,), device=dev)
+    cos, sin = R.rope_tables(128, D, 10000.0, dev)
+    slots = torch.randperm(nb * bs, device=dev)[:T]
+    p = H.linear(x, w, b, partial_ok=True)
+    if T == 40:
+        assert isinstance(p, H.PartialSum) and p.S > 1
+    kc1, vc1 = [torch.zeros(nb, nkv, bs, D, dtype=torch.bfloat16, device=dev) for _ in range(2)]
+    q1 = H.rope_cache(p, pos, cos, sin, kc1, vc1, slots, nh, nkv, D, D, style)
+    q2 = H.linear(x, w, b)
+    kc2, vc2 = torch.zeros_like(kc1), torch.zeros_like(vc1)
+    R.rope_cache(q2, pos, cos, sin, kc2, vc2, slots, nh, nkv, D, D, style)
+    close(q1, q2, 2e-2)
+    close(kc1, kc2, 2e-2)
+    close(vc1, vc2, 2e-2)
+
+
 @pytest.mark.parametrize("D,nh,nkv", [(64, 4, 4), (128, 8, 2), (128, 16, 1), (256, 4, 4)])
 def test_attn_prefill(D, nh, nkv):
     torch.manual_seed(0)
@@ -122,16 +145,16 @@ def test_gemm(M, N, K):
 
 
 @pytest.mark.parametrize("tile", [1, 2, 3, 4])  # 128x128, 64x128, 64x64, 256x256 (8 waves)
-@pytest.mark.parametrize("stages", [2, 3])
+@pytest.mark.parametrize("stages", [2, 3, 4, 6])
 @pytest.mark.parametrize("split", [1, 3, 8])
 @pytest.mark.parametrize("M,N,K", [(64, 1536, 4096), (200, 4800, 1600), (37, 256, 64 * 5 + 16), (700, 1312, 192)])
 def test_gemm_tiled_variants(tile, stages, split, M, N, K):
-    if tile == 4 and (stages == 3 or split > 1):
+    if tile == 4 and (stages != 2 or split > 1):
         pytest.skip("the 256x256 kernel has one pipeline and no split-K")
     torch.manual_seed(0)
     x, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
     b = rnd(N, scale=0.1)
-    hint = (tile | (16 if stages == 3 else 0)) << 8
+    hint = (tile | ({2: 0, 3: 16, 4: 32, 6: 48}[stages])) << 8
     ref = R.linear(x.float(), w.float(), b.float(), act="gelu_tanh")
     close(H.linear(x, w, b, act="gelu_tanh", nt_hint=hint, split_hint=split), ref, 2e-2)
     close(H.linear(x, w, None, glu=True, nt_hint=hint, split_hint=split),
@@ -238,3 +261,25 @@ def test_sample_topk_topp_sets(V):
         o = H.sample(logits, temp, topk, topp, seeds)
         for b in range(B):
             assert allowed[b][o[b]], (b, int(o[b]), int(topk[b]), float(topp[b]))
+
+
+def test_autotune_installs_plan():
+    from llmss_amd import _native
+    from llmss_amd.ops.autotune import GemmShape, tune_shape
+
+    lib = _native()
+    torch.manual_seed(0)
+    M, N, K = 48, 1536, 1024
+    nt, s, t, t_default = tune_shape(M, GemmShape(N, K), dev, weight_budget=64 << 20, iters=2,
+                                     cands=[(0x300, 2), (0x1200, 1), (3 + 32, 4)])
+    assert t <= t_default and (nt == 0 or nt in (0x300, 0x1200, 35))
+    try:
+        lib.gemm_tuned_set(M, N, K, False, False, 0x1300, 4)
+        assert lib.gemm_tuned_get(M, N, K, False, False) == (0x1300, 4)
+        assert lib.gemm_plan(M, N, K, False)[1] == 4
+        x, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
+        close(H.linear(x, w), R.linear(x.float(), w.float()), 2e-2)
+        p = H.linear(x, w, partial_ok=True)
+        assert isinstance(p, H.PartialSum) and p.S == 4
+    finally:
+        lib.gemm_tuned_clear()
