@@ -150,9 +150,259 @@ __global__ __launch_bounds__(1024) void sample_kernel(const T* __restrict__ logi
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// v3 (bf16 logits, 16-B aligned rows, V <= 1024 * 8 * CPT). The row is read once into registers.
+// Thresholds: ONE histogram pass over the distance to the row max (2048 bins of 1/32 logit; the
+// last bin collects everything >= 64 below the max), then an exact rank selection among the few
+// elements of the boundary bin only (gathered into LDS). Probability mass is accumulated as
+// 2^-32 fixed-point integers, so every sum is order-independent: all TP ranks (same all-gathered
+// logits) derive bit-identical thresholds and draw the same token without any broadcast - v1's
+// float LDS atomics did not guarantee that. More than SV3_MAXC elements tied within 1/32 logit at
+// the boundary (pathological) keeps the whole bin.
+// ---------------------------------------------------------------------------------------------
+constexpr int SV3_BINS = 2048;
+constexpr int SV3_MAXC = 2048;
+
+struct Sv3Smem {
+  unsigned cnt[SV3_BINS];
+  unsigned long long mass[SV3_BINS];
+  float cv[SV3_MAXC];
+  int ci[SV3_MAXC];
+  unsigned long long wtot[16];
+  float red[32];
+  int redi[32];
+  int ncand;
+  int bin;
+  unsigned long long excl;
+  unsigned long long acc;
+  float thr;
+};
+
+__device__ __forceinline__ int sv3_bin(float e, float mx) {
+  const float d = (mx - e) * 32.f;
+  return d < 2047.f ? (int)d : 2047;
+}
+__device__ __forceinline__ unsigned long long sv3_mass(float e, float mx) {
+  return (unsigned long long)(__expf(e - mx) * 4294967296.f);
+}
+
+// First bin b < limit whose inclusive prefix of arr reaches target; sm.bin / sm.excl (prefix
+// before b). 1024 threads x 2 bins. If the total never reaches target: bin = limit - 1.
+template <typename T>
+__device__ void sv3_find(const T* arr, unsigned long long target, int limit, Sv3Smem& sm) {
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const unsigned long long a0 = 2 * t < limit ? (unsigned long long)arr[2 * t] : 0ull;
+  const unsigned long long a1 = 2 * t + 1 < limit ? (unsigned long long)arr[2 * t + 1] : 0ull;
+  const unsigned long long loc = a0 + a1;
+  unsigned long long inc = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  if (t == 0) { sm.bin = limit - 1; sm.excl = 0; }
+  if (lane == 63) sm.wtot[wid] = inc;
+  __syncthreads();
+  unsigned long long off = 0;
+  for (int w = 0; w < wid; ++w) off += sm.wtot[w];
+  const unsigned long long e0 = off + inc - loc, e1 = e0 + a0;
+  if (e0 < target && e0 + a0 >= target) { sm.bin = 2 * t; sm.excl = e0; }
+  else if (e1 < target && e1 + a1 >= target) { sm.bin = 2 * t + 1; sm.excl = e1; }
+  __syncthreads();
+}
+
+template <int CPT>
+__global__ __launch_bounds__(1024) void sample_v3_kernel(const bf16_t* __restrict__ logits, int64_t ld, int V,
+                                                         const float* __restrict__ temperature,
+                                                         const int* __restrict__ top_k, const float* __restrict__ top_p,
+                                                         const int64_t* __restrict__ seeds, int64_t* __restrict__ out,
+                                                         int64_t* __restrict__ out2) {
+  __shared__ Sv3Smem sm;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const bf16_t* row = logits + b * ld;
+  const float temp = temperature ? temperature[b] : 0.f;
+  const int k = top_k ? top_k[b] : 0;
+  const float p = top_p ? top_p[b] : 1.f;
+  const bool greedy = !(temp > 0.f) || k == 1;
+  const float scale = greedy ? 1.f : 1.f / temp;
+
+  // the row stays packed (bf16) in registers; X(i) = scaled logit of element slot i, -inf past V
+  u16x8 raw[CPT];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int ch = tid + c * 1024;
+    raw[c] = ch * 8 < V ? *reinterpret_cast<const u16x8*>(row + ch * 8) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+#define X(i) (((tid + ((i) >> 3) * 1024) * 8 + ((i) & 7) < V) ? bf2f(raw[(i) >> 3][(i) & 7]) * scale : -INFINITY)
+  float thr = -INFINITY;
+  if (!greedy) {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < CPT * 8; ++i) mx = fmaxf(mx, X(i));
+    mx = block_max(mx, sm.red);
+    const bool do_k = k > 0 && k < V, do_p = p < 1.f;
+    if (do_k || do_p) {
+      for (int i = tid; i < SV3_BINS; i += 1024) { sm.cnt[i] = 0u; sm.mass[i] = 0ull; }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < CPT * 8; ++i) {
+        const float xi = X(i);
+        if (xi > -INFINITY) {
+          const int bn = sv3_bin(xi, mx);
+          atomicAdd(&sm.cnt[bn], 1u);
+          if (do_p) atomicAdd(&sm.mass[bn], sv3_mass(xi, mx));
+        }
+      }
+      __syncthreads();
+    }
+    int bk = SV3_BINS;  // top-k boundary bin (bins > bk are cut)
+    unsigned long long kept_bk = 0;
+    if (do_k) {
+      sv3_find(sm.cnt, (unsigned long long)k, SV3_BINS, sm);
+      bk = sm.bin;
+      const int r = k - (int)sm.excl;  // 1-based rank of the k-th largest inside bin bk
+      if (tid == 0) { sm.ncand = 0; sm.acc = 0; }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < CPT * 8; ++i) {
+        const float xi = X(i);
+        if (xi > -INFINITY && sv3_bin(xi, mx) == bk) {
+          const int slot = atomicAdd(&sm.ncand, 1);
+          if (slot < SV3_MAXC) { sm.cv[slot] = xi; sm.ci[slot] = (tid + (i >> 3) * 1024) * 8 + (i & 7); }
+        }
+      }
+      __syncthreads();
+      const int n = sm.ncand;
+      if (n > SV3_MAXC) {  // pathological tie mass: keep the whole bin
+        thr = mx - (float)(bk + 1) / 32.f;
+        thr = nextafterf(thr, INFINITY);
+      } else {
+        for (int c = tid; c < n; c += 1024) {
+          const float v = sm.cv[c];
+          const int vi = sm.ci[c];
+          int rank = 0;
+          for (int c2 = 0; c2 < n; ++c2) {
+            const float v2 = sm.cv[c2];
+            rank += (v2 > v || (v2 == v && sm.ci[c2] < vi)) ? 1 : 0;
+          }
+          if (rank == r - 1) sm.thr = v;
+        }
+        __syncthreads();
+        thr = sm.thr;
+      }
+      if (do_p) {  // kept mass inside the boundary bin
+        for (int c = tid; c < min(n, SV3_MAXC); c += 1024)
+          if (sm.cv[c] >= thr) atomicAdd(&sm.acc, sv3_mass(sm.cv[c], mx));
+        __syncthreads();
+        kept_bk = sm.acc;
+      }
+    }
+    if (do_p) {
+      // kept-set mass Z: full bins above bk + the kept part of bin bk
+      const int limit = do_k ? bk : SV3_BINS;
+      sv3_find(sm.mass, ~0ull, limit, sm);  // only for the total below `limit`
+      unsigned long long z = 0;
+      for (int w = 0; w < 16; ++w) z += sm.wtot[w];
+      __syncthreads();
+      if (do_k && tid == 0) sm.mass[bk] = kept_bk;
+      __syncthreads();
+      z += do_k ? kept_bk : 0ull;
+      const unsigned long long target = (unsigned long long)((double)p * (double)z);
+      const int lim2 = do_k ? bk + 1 : SV3_BINS;
+      sv3_find(sm.mass, target < 1ull ? 1ull : target, lim2, sm);
+      const int bp = sm.bin;
+      const unsigned long long above = sm.excl;
+      if (tid == 0) sm.ncand = 0;
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < CPT * 8; ++i) {
+        const float xi = X(i);
+        if (xi > -INFINITY && xi >= thr && sv3_bin(xi, mx) == bp) {
+          const int slot = atomicAdd(&sm.ncand, 1);
+          if (slot < SV3_MAXC) { sm.cv[slot] = xi; sm.ci[slot] = (tid + (i >> 3) * 1024) * 8 + (i & 7); }
+        }
+      }
+      __syncthreads();
+      const int n = sm.ncand;
+      float tp = -INFINITY;
+      if (n > SV3_MAXC) {
+        tp = nextafterf(mx - (float)(bp + 1) / 32.f, INFINITY);
+      } else {
+        if (tid == 0) sm.thr = -INFINITY;
+        __syncthreads();
+        for (int c = tid; c < n; c += 1024) {
+          const float v = sm.cv[c];
+          const int vi = sm.ci[c];
+          unsigned long long before = 0;
+          for (int c2 = 0; c2 < n; ++c2) {
+            const float v2 = sm.cv[c2];
+            if (v2 > v || (v2 == v && sm.ci[c2] < vi)) before += sv3_mass(v2, mx);
+          }
+          const unsigned long long lo = above + before, hi = lo + sv3_mass(v, mx);
+          if (lo < target && hi >= target) sm.thr = v;
+        }
+        __syncthreads();
+        tp = sm.thr;
+      }
+      thr = fmaxf(thr, tp);
+    }
+  }
+  // Gumbel-max over the kept set (greedy: plain argmax, lowest index on ties)
+  const unsigned long long seed = seeds ? (unsigned long long)seeds[b] : 0ull;
+  const unsigned s0 = (unsigned)seed, s1 = (unsigned)(seed >> 32);
+  float best = -INFINITY;
+  int besti = 0x7fffffff;
+#pragma unroll
+  for (int i = 0; i < CPT * 8; ++i) {
+    const int idx = (tid + (i >> 3) * 1024) * 8 + (i & 7);
+    float v = X(i);
+    if (!(v > -INFINITY)) continue;
+    if (!greedy) {
+      if (v < thr) continue;
+      const unsigned r = philox((unsigned)idx, 0u, s0, s1);
+      const float u = ((float)(r >> 8) + 0.5f) * (1.0f / 16777216.0f);
+      v = v - __logf(-__logf(u));
+    }
+    if (v > best || (v == best && idx < besti)) { best = v; besti = idx; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(besti, o, 64);
+    if (ob > best || (ob == best && oi < besti)) { best = ob; besti = oi; }
+  }
+  __syncthreads();
+  if (lane == 0) { sm.red[wid] = best; sm.redi[wid] = besti; }
+  __syncthreads();
+  if (tid == 0) {
+    float bb = sm.red[0];
+    int bi = sm.redi[0];
+    for (int i = 1; i < 16; ++i)
+      if (sm.red[i] > bb || (sm.red[i] == bb && sm.redi[i] < bi)) { bb = sm.red[i]; bi = sm.redi[i]; }
+    if (bi >= V) bi = 0;
+    out[b] = bi;
+    if (out2) out2[b] = bi;
+  }
+#undef X
+}
+
 void launch_sample(const void* logits, int64_t ld, bool fp32_logits, int B, int V, const void* temperature,
                    const void* top_k, const void* top_p, const void* seeds, void* out, void* out2, hipStream_t st) {
   if (B == 0) return;
+  const int chunks = (V + 7) / 8;
+  if (!fp32_logits && ld % 8 == 0 && (uintptr_t)logits % 16 == 0 && chunks <= 8 * 1024) {
+#define SV3(CPT_)                                                                                                  \
+  sample_v3_kernel<CPT_><<<B, 1024, 0, st>>>((const bf16_t*)logits, ld, V, (const float*)temperature,             \
+                                             (const int*)top_k, (const float*)top_p, (const int64_t*)seeds,       \
+                                             (int64_t*)out, (int64_t*)out2)
+    if (chunks <= 2048) SV3(2);
+    else if (chunks <= 4096) SV3(4);
+    else SV3(8);
+#undef SV3
+    HIP_CHECK_LAUNCH();
+    return;
+  }
   if (fp32_logits)
     sample_kernel<float><<<B, 1024, 0, st>>>((const float*)logits, ld, V, (const float*)temperature, (const int*)top_k,
                                              (const float*)top_p, (const int64_t*)seeds, (int64_t*)out, (int64_t*)out2);

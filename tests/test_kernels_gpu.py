@@ -283,3 +283,44 @@ def test_autotune_installs_plan():
         assert isinstance(p, H.PartialSum) and p.S == 4
     finally:
         lib.gemm_tuned_clear()
+
+
+def _kept_sets(logits, temp, k, p):
+    """Exact kept token sets (reference semantics: temperature -> top-k (ties kept) -> top-p)."""
+    out = []
+    for row in logits.float().cpu():
+        x = row.double() / temp
+        if 0 < k < x.numel():
+            x = x.masked_fill(x < torch.topk(x, k).values[-1], float("-inf"))
+        if p < 1.0:
+            pr = torch.softmax(x, -1)
+            sp, _ = pr.sort(descending=True)
+            keep = (sp.cumsum(0) - sp) < p * sp.sum()
+            thr = sp[keep].min()
+            x = x.masked_fill(pr < thr, float("-inf"))
+        out.append(set(torch.nonzero(x > float("-inf")).flatten().tolist()))
+    return out
+
+
+@pytest.mark.parametrize("V", [32000, 50257, 1000])
+@pytest.mark.parametrize("k,p,temp", [(50, 1.0, 1.0), (0, 0.6, 0.8), (40, 0.9, 1.0), (7, 0.3, 1.3)])
+def test_sample_kept_set_exact(V, k, p, temp):
+    torch.manual_seed(V + k)
+    B = 6
+    logits = rnd(B, V, scale=2.5)
+    sets = _kept_sets(logits, temp, k, p)
+    tt = torch.full((B,), temp, device=dev)
+    tk = torch.full((B,), k, dtype=torch.int32, device=dev)
+    tp = torch.full((B,), p, device=dev)
+    seen = [set() for _ in range(B)]
+    for s in range(64):
+        seeds = torch.arange(B, dtype=torch.int64, device=dev) * 7919 + s * 104729
+        o = H.sample(logits, tt, tk, tp, seeds).tolist()
+        o2 = H.sample(logits, tt, tk, tp, seeds).tolist()
+        assert o == o2  # deterministic for identical inputs (TP ranks rely on it)
+        for b in range(B):
+            assert o[b] in sets[b], (b, o[b], len(sets[b]))
+            seen[b].add(o[b])
+    for b in range(B):
+        if len(sets[b]) <= 3:
+            assert seen[b] == sets[b]
