@@ -136,6 +136,11 @@ def model_shapes(model) -> Dict[str, GemmShape]:
     return out
 
 
+# process-wide results: a second engine in the same process reuses the first one's plans, so both
+# run bit-identical kernels (and skip the tuning time)
+_DONE: Dict[Tuple[int, GemmShape, str], Tuple[int, int, float, float]] = {}
+
+
 def tune_model(model, ms: Sequence[int], native=None) -> Dict[Tuple[str, int], Tuple[int, int, float, float]]:
     """Tune every (shape, M) pair and install the winners in the native plan table."""
     from .. import _native
@@ -144,10 +149,10 @@ def tune_model(model, ms: Sequence[int], native=None) -> Dict[Tuple[str, int], T
     dev = model.device
     t0 = time.perf_counter()
     res = {}
-    done = {}
+    done = _DONE
     for name, shp in model_shapes(model).items():
         for M in sorted(set(int(m) for m in ms)):
-            key = (M, shp)
+            key = (M, shp, str(dev))
             if key not in done:
                 done[key] = tune_shape(M, shp, dev)
             nt, s, t, t0_us = done[key]

@@ -23,7 +23,11 @@ for s in $STAGES; do
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()"; rc=$? ;;
     bench) step bench 380 python bench.py ${BENCH_ARGS:-}; rc=$? ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null;
-          step prof 380 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py ${BENCH_ARGS:-}; rc=$? ;;
+          step prof 380 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py ${BENCH_ARGS:-}; rc=$?
+          rm -f gpurun_out/prof/*kernel_trace.csv ;;
+    prof8) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null;
+          step prof8 380 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8 -o run --output-format csv -- python3 bench.py --simulate-tp 8; rc=$?
+          rm -f gpurun_out/prof8/*kernel_trace.csv ;;
     *) echo "unknown stage $s"; rc=2 ;;
   esac
   ok $rc || { echo "stopping after $s (rc=$rc)"; exit $rc; }
