@@ -118,6 +118,8 @@ def initialize_distributed(timeout_s: int = 120, backend: Optional[str] = None):
         return TPGroup(rank, world_size, fake=True), rank, world_size
 
     if not dist.is_initialized():
+        if backend == "nccl":  # a hung or dead peer aborts the communicator after `timeout_s` (clean error, no hang)
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         kwargs = dict(backend=backend, world_size=world_size, rank=rank, timeout=timedelta(seconds=timeout_s))
         if backend == "nccl":
             kwargs["device_id"] = torch.device("cuda", torch.cuda.current_device())

@@ -9,9 +9,20 @@ requests / aborts over a dedicated gloo (CPU/TCP) group, and all ranks then run 
 ``engine.step()`` (same scheduler decisions, same all-gathered logits, same Philox keys => same
 tokens, no token broadcast). When there is no work the leader blocks on its inbox and followers
 block in a CPU receive - nothing spins on the GPU.
+
+Failure handling (the reference has none beyond the 60 s NCCL timeout):
+* leader heartbeat: an idle leader still broadcasts a heartbeat every ``heartbeat_s``; followers
+  wait on the control group with ``leader_timeout_s``, so a lost leader ends them cleanly instead
+  of hanging in a collective forever.
+* any exception in a step or a collective (a dead peer, a RCCL/gloo timeout) fails every
+  in-flight request with ``finish_reason="error"`` and stops the driver on that rank.
+* per-request deadlines (``submit(..., deadline_s=)``, gRPC deadlines) abort on every rank.
+* fault injection for tests: ``LLMSS_FAULT_INJECT="rank:step:kind"`` (kind = exit | raise | hang)
+  makes one rank misbehave at a given engine step.
 """
 from __future__ import annotations
 
+import os
 import queue
 import threading
 import time
@@ -41,6 +52,8 @@ class Handle:
     metrics: Dict[str, float] = field(default_factory=dict)
     on_done: Optional[Callable[["Handle"], None]] = None
     t_submit: float = field(default_factory=time.perf_counter)
+    deadline: Optional[float] = None  # perf_counter time after which the request is aborted
+    error: str = ""
 
     def wait(self, timeout: Optional[float] = None) -> bool:
         return self.done.wait(timeout)
@@ -53,15 +66,32 @@ class Handle:
             yield t
 
 
+@dataclass
+class FaultSpec:
+    rank: int
+    step: int
+    kind: str  # exit | raise | hang
+
+    @staticmethod
+    def from_env() -> Optional["FaultSpec"]:
+        v = os.environ.get("LLMSS_FAULT_INJECT")
+        if not v:
+            return None
+        r, st, kind = v.split(":")
+        return FaultSpec(int(r), int(st), kind)
+
+
 class EngineDriver:
-    def __init__(self, engine: LLMEngine, control_group=None):
+    def __init__(self, engine: LLMEngine, control_group=None, heartbeat_s: float = 1.0,
+                 leader_timeout_s: float = 300.0, fault: Optional[FaultSpec] = None):
         self.engine = engine
         self.tp = engine.tp
         self.rank = self.tp.rank
         self.leader = self.rank == 0
+        self.heartbeat_s = heartbeat_s
         self.cg = control_group
         if self.tp.is_real and self.cg is None:
-            self.cg = dist.new_group(backend="gloo", timeout=timedelta(days=30))
+            self.cg = dist.new_group(backend="gloo", timeout=timedelta(seconds=leader_timeout_s))
         self.inbox: "queue.Queue" = queue.Queue()
         self.handles: Dict[int, Handle] = {}
         self._next = 0
@@ -69,10 +99,13 @@ class EngineDriver:
         self._thread: Optional[threading.Thread] = None
         self._lock = threading.Lock()
         self.idle_wait_s = 0.05
+        self.fault = fault if fault is not None else FaultSpec.from_env()
+        self.error: Optional[BaseException] = None
+        self._last_bcast = time.perf_counter()
 
     # --------------------------------------------------------------------- leader API
     def submit(self, prompt_ids: List[int], params: SamplingParams,
-               on_done: Optional[Callable[[Handle], None]] = None) -> Handle:
+               on_done: Optional[Callable[[Handle], None]] = None, deadline_s: Optional[float] = None) -> Handle:
         if not self.leader:
             raise RuntimeError("submit() is only valid on rank 0")
         params.resolved_seed()  # fix the seed on the leader so every rank uses the same one
@@ -80,6 +113,12 @@ class EngineDriver:
             rid = self._next
             self._next += 1
         h = Handle(rid, list(prompt_ids), params, on_done=on_done)
+        if deadline_s is not None:
+            h.deadline = h.t_submit + deadline_s
+        if self.error is not None:  # the driver already failed: refuse instead of queueing forever
+            h.error = f"driver stopped: {self.error}"
+            self._complete(h, "error")
+            return h
         self.handles[rid] = h
         self.inbox.put(("new", h))
         return h
@@ -122,22 +161,54 @@ class EngineDriver:
                 item = self.inbox.get_nowait()
         except queue.Empty:
             pass
+        now = time.perf_counter()
+        for h in list(self.handles.values()):  # server-side deadlines
+            if h.deadline is not None and now > h.deadline and h.rid not in aborts:
+                h.error = "deadline exceeded"
+                aborts.append(h.rid)
         return {"new": new, "abort": aborts, "stop": stop}
 
+    def _inject(self, step: int):
+        f = self.fault
+        if f is None or f.rank != self.rank or step != f.step:
+            return
+        log.warning("rank %d: injecting fault %r at step %d", self.rank, f.kind, step)
+        if f.kind == "exit":
+            os._exit(17)
+        if f.kind == "hang":
+            while True:
+                time.sleep(3600)
+        raise RuntimeError(f"injected fault at step {step}")
+
     def run(self):
+        try:
+            self._run()
+        except Exception as e:  # noqa: BLE001 - a dead peer, a collective timeout, a kernel error
+            self.error = e
+            log.error("rank %d: engine driver stopped: %s", self.rank, e)
+            for h in list(self.handles.values()):
+                h.error = h.error or f"engine failure: {e}"
+                self._complete(h, "error")
+
+    def _run(self):
         eng = self.engine
         dev_ok = eng.is_gpu
         if dev_ok:
             torch.cuda.set_device(eng.device)
+        steps = 0
         while True:
             if self.leader:
                 idle = not eng.has_unfinished()
                 msg = self._collect(block=idle)
-                if idle and not msg["new"] and not msg["abort"] and not msg["stop"] and not self._stop:
-                    continue  # nothing to do, nothing to tell the followers
+                quiet = not msg["new"] and not msg["abort"] and not msg["stop"] and not self._stop
+                if idle and quiet:
+                    if not self.tp.is_real or time.perf_counter() - self._last_bcast < self.heartbeat_s:
+                        continue  # nothing to do, nothing to tell the followers
+                    msg["hb"] = True  # heartbeat: followers time out if the leader disappears
             else:
                 msg = None
             msg = self._bcast(msg)
+            self._last_bcast = time.perf_counter()
             for rid, prompt, pd in msg["new"]:
                 eng.add_request(prompt, SamplingParams(**pd), req_id=rid)
             for rid in msg["abort"]:
@@ -147,7 +218,9 @@ class EngineDriver:
                 break
             if not eng.has_unfinished():
                 continue
+            self._inject(steps)
             events = eng.step()
+            steps += 1
             if self.leader:
                 for ev in events:
                     h = self.handles.get(ev.req_id)
@@ -177,7 +250,7 @@ class EngineDriver:
     def _finish_abort(self, rid):
         h = self.handles.get(rid)
         if h is not None:
-            self._complete(h, "abort")
+            self._complete(h, "deadline" if h.error == "deadline exceeded" else "abort")
 
     # --------------------------------------------------------------------- convenience
     def generate(self, prompt_ids: List[int], params: SamplingParams, timeout: Optional[float] = None) -> Handle:

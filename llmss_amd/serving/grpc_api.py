@@ -131,11 +131,13 @@ class EngineServicer:
             params = _params(req)
         except ValueError as e:
             ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
-        h = self.driver.submit(self._prompt_ids(req), params)
-        remaining = ctx.time_remaining()
+        remaining = ctx.time_remaining()  # gRPC deadline -> server-side deadline on every rank
+        h = self.driver.submit(self._prompt_ids(req), params, deadline_s=remaining)
         if not h.wait(remaining if remaining is not None else None):
             self.driver.abort(h.rid)
             ctx.abort(grpc.StatusCode.DEADLINE_EXCEEDED, "generation deadline exceeded")
+        if h.finish_reason == "error":
+            ctx.abort(grpc.StatusCode.UNAVAILABLE, h.error or "engine failure")
         m = h.metrics or {}
         return GenerateResponse(prompt=req.prompt, continuation=self.tok.decode(h.output_ids), request_id=req.request_id,
                                 token_ids=h.output_ids, finish_reason=h.finish_reason,
@@ -146,7 +148,7 @@ class EngineServicer:
             params = _params(req)
         except ValueError as e:
             ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
-        h = self.driver.submit(self._prompt_ids(req), params)
+        h = self.driver.submit(self._prompt_ids(req), params, deadline_s=ctx.time_remaining())
         ctx.add_callback(lambda: (not h.done.is_set()) and self.driver.abort(h.rid))
         ids, prev = [], ""
         for t in h.stream():
@@ -157,7 +159,11 @@ class EngineServicer:
         yield Token(token_id=-1, text="", finished=True, finish_reason=h.finish_reason)
 
     def Stats(self, req, ctx):
-        return StatsResponse(json=json.dumps(self.driver.engine.stats))
+        st = dict(self.driver.engine.stats)
+        st["healthy"] = self.driver.error is None
+        if self.driver.error is not None:
+            st["error"] = str(self.driver.error)
+        return StatsResponse(json=json.dumps(st))
 
 
 class BrokerServicer:

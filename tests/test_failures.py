@@ -1,0 +1,132 @@
+"""Failure detection in the serving driver: server-side deadlines, a follower that
+dies mid-generation (every in-flight request must fail, not hang), a leader that disappears
+(followers must notice through the heartbeat timeout), and the fault-injection hook."""
+import os
+import queue
+import socket
+import time
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from helpers import save_hf_model
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module")
+def ckpt(tmp_path_factory):
+    d = str(tmp_path_factory.mktemp("fail_llama"))
+    save_hf_model("llama", d, vocab=101)
+    return d
+
+
+def test_deadline_aborts_request(ckpt):
+    from llmss_amd.engine import LLMEngine, SamplingParams, build_model
+    from llmss_amd.serving.driver import EngineDriver
+
+    m = build_model(ckpt, None, "fp32", "cpu")
+    drv = EngineDriver(LLMEngine(m, max_num_seqs=4, block_size=4, num_blocks=128, eos_token_id=None)).start()
+    try:
+        h = drv.submit([1, 2, 3], SamplingParams(max_new_tokens=10_000, is_greedy=True, ignore_eos=True),
+                       deadline_s=0.0)
+        assert h.wait(30)
+        assert h.finish_reason == "deadline" and len(h.output_ids) < 10_000
+        ok = drv.submit([4, 5], SamplingParams(max_new_tokens=3, is_greedy=True, ignore_eos=True))
+        assert ok.wait(30) and ok.finish_reason == "length" and len(ok.output_ids) == 3
+    finally:
+        drv.stop()
+
+
+def _worker(rank, world, port, ckpt, role, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from llmss_amd.engine import LLMEngine, SamplingParams, build_model
+    from llmss_amd.parallel.dist import initialize_distributed
+    from llmss_amd.serving.driver import EngineDriver, FaultSpec
+
+    tp, r, w = initialize_distributed(backend="gloo", timeout_s=20)
+    m = build_model(ckpt, tp, "fp32", "cpu")
+    eng = LLMEngine(m, max_num_seqs=4, block_size=4, num_blocks=64, eos_token_id=None)
+    fault = FaultSpec(1, 3, "exit") if role == "follower_crash" else None
+    drv = EngineDriver(eng, heartbeat_s=0.2, leader_timeout_s=5.0, fault=fault).start()
+    if role == "follower_crash":
+        if r == 0:
+            h = drv.submit([1, 2, 3, 4], SamplingParams(max_new_tokens=50, is_greedy=True, ignore_eos=True))
+            done = h.wait(90)
+            q.put(("leader", done, h.finish_reason, len(h.output_ids), h.error))
+            later = drv.submit([5, 6], SamplingParams(max_new_tokens=2, is_greedy=True))
+            q.put(("later", later.wait(5), later.finish_reason))
+            q.close()
+            q.join_thread()  # flush the queue's feeder thread before the hard exit
+            os._exit(0)
+        drv._thread.join(120)  # rank 1 exits inside the driver (os._exit(17)) at step 3
+        os._exit(0)
+    else:  # leader_loss
+        if r == 0:
+            time.sleep(1.5)  # a few idle heartbeats
+            os._exit(0)  # leader vanishes without a word
+        t0 = time.time()
+        drv._thread.join(60)
+        q.put(("follower", drv.error is not None, time.time() - t0, str(drv.error)[:200]))
+        q.close()
+        q.join_thread()
+        os._exit(0)
+
+
+def _spawn(world, ckpt, role):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, ckpt, role, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    return procs, q
+
+
+def _drain(q, n, timeout):
+    out, t0 = [], time.time()
+    while len(out) < n and time.time() - t0 < timeout:
+        try:
+            out.append(q.get(timeout=1))
+        except queue.Empty:
+            pass
+    return out
+
+
+def test_follower_crash_fails_inflight_requests(ckpt):
+    procs, q = _spawn(2, ckpt, "follower_crash")
+    try:
+        res = {r[0]: r for r in _drain(q, 2, 150)}
+        assert "leader" in res, res
+        _, done, reason, ntok, err = res["leader"]
+        assert done and reason == "error" and ntok < 50 and err
+        assert res["later"][1] and res["later"][2] == "error"  # a failed driver refuses new work
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    assert procs[1].exitcode == 17  # the injected exit
+
+
+def test_leader_loss_detected_by_follower(ckpt):
+    procs, q = _spawn(2, ckpt, "leader_loss")
+    try:
+        res = _drain(q, 1, 120)
+        assert res and res[0][0] == "follower", res
+        _, errored, waited, msg = res[0]
+        assert errored and waited < 60, res
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
