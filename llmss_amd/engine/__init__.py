@@ -8,7 +8,7 @@ import torch
 
 from ..models.config import ModelConfig, get_preset
 from ..models.decoder import DecoderLM
-from ..models.weights import load_hf_weights, random_weights
+from ..models.weights import load_hf_weights, load_shard, random_weights, save_shard, shard_cache_path
 from ..parallel.dist import TPGroup
 from ..utils.checkpoint import CheckpointReader, weight_files
 from .engine import LLMEngine, Request, StepEvent
@@ -26,8 +26,12 @@ def default_device(tp: TPGroup) -> torch.device:
 
 
 def build_model(model: str, tp: Optional[TPGroup] = None, dtype: str = "bf16", device=None, fp8: bool = False,
-                random_init: Optional[bool] = None, seed: int = 0) -> DecoderLM:
-    """``model`` is a HF checkpoint directory or a preset name (random-init weights)."""
+                random_init: Optional[bool] = None, seed: int = 0, shard_cache: Optional[str] = None) -> DecoderLM:
+    """``model`` is a HF checkpoint directory or a preset name (random-init weights).
+
+    ``shard_cache`` (or ``LLMSS_SHARD_CACHE``): directory of finished per-rank weight shards; the
+    first load writes this rank's file, later loads mmap it instead of re-sharding the checkpoint.
+    """
     tp = tp or TPGroup()
     device = torch.device(device) if device is not None else default_device(tp)
     if device.type == "cuda":
@@ -44,8 +48,15 @@ def build_model(model: str, tp: Optional[TPGroup] = None, dtype: str = "bf16", d
     if random_init:
         w = random_weights(cfg, tp.size, tp.rank, device=device, dtype=tdtype, seed=seed, fp8=fp8)
     else:
-        reader = CheckpointReader(weight_files(model))
-        w = load_hf_weights(cfg, reader, tp.size, tp.rank, device=device, dtype=tdtype, fp8=fp8)
+        files = weight_files(model)
+        shard_cache = shard_cache or os.environ.get("LLMSS_SHARD_CACHE")
+        cpath = shard_cache_path(shard_cache, model, files, tp.size, tp.rank, tdtype, fp8) if shard_cache else None
+        if cpath and os.path.exists(cpath):
+            w = load_shard(cfg, cpath, device, tdtype)
+        else:
+            w = load_hf_weights(cfg, CheckpointReader(files), tp.size, tp.rank, device=device, dtype=tdtype, fp8=fp8)
+            if cpath:
+                save_shard(w, cpath)
     return DecoderLM(cfg, w, tp)
 
 

@@ -22,8 +22,9 @@ replication (``gpt_bigcode_modeling.py:150-155``) to GQA.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 import torch
 
@@ -375,3 +376,88 @@ def load_hf_weights(cfg: ModelConfig, reader, tp: int = 1, rank: int = 0, device
     else:
         raise ValueError(mt)
     return _finish(cfg, plan, wte, wpe, layers, lnf_w, lnf_b, head_w, head_b, device, dtype, fp8)
+
+
+# ------------------------------------------------------------------------------ per-rank shard cache
+# a restart of a large TP deployment should not re-read, re-shard, re-interleave and
+# re-quantize the HF checkpoint on every rank. The finished per-rank weights (this rank's shards,
+# padded head, SwiGLU interleave, fp8 + scales) are written once as one safetensors file per rank
+# and mmap-loaded by the native reader afterwards.
+def _flat(mw: ModelWeights) -> Dict[str, torch.Tensor]:
+    out: Dict[str, torch.Tensor] = {"wte": mw.wte, "lnf_w": mw.lnf_w}
+    if mw.wpe is not None:
+        out["wpe"] = mw.wpe
+    if mw.lnf_b is not None:
+        out["lnf_b"] = mw.lnf_b
+
+    def put_lin(pfx, lin: Linear):
+        out[pfx + ".w"] = lin.w
+        if lin.b is not None:
+            out[pfx + ".b"] = lin.b
+        if lin.w_scale is not None:
+            out[pfx + ".s"] = lin.w_scale
+
+    for i, L in enumerate(mw.layers):
+        for nm in ("ln1_w", "ln1_b", "ln2_w", "ln2_b"):
+            t = getattr(L, nm)
+            if t is not None:
+                out[f"l{i}.{nm}"] = t
+        for nm in ("qkv", "o", "up", "down"):
+            put_lin(f"l{i}.{nm}", getattr(L, nm))
+    put_lin("head", mw.head)
+    return out
+
+
+def save_shard(mw: ModelWeights, path: str) -> None:
+    from safetensors.torch import save_file
+
+    tensors = {k: v.detach().contiguous().cpu() for k, v in _flat(mw).items()}
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+    tmp = path + f".tmp{os.getpid()}"
+    save_file(tensors, tmp, metadata={"format": "llmss_amd-shard-v1", "layers": str(len(mw.layers)),
+                                      "glu": str(int(mw.layers[0].up.glu)) if mw.layers else "0"})
+    os.replace(tmp, path)  # atomic: a concurrent reader never sees a partial file
+
+
+def load_shard(cfg: ModelConfig, path: str, device, dtype) -> ModelWeights:
+    from ..utils.checkpoint import CheckpointReader
+
+    rd = CheckpointReader([path])
+    names = set(rd.routing)
+
+    def get(name):
+        if name not in names:
+            return None
+        t = rd.get(name)
+        return t.to(device=device, dtype=dtype if t.is_floating_point() and t.dtype != torch.float32 else t.dtype)
+
+    def lin(pfx, glu=False):
+        s = rd.get(pfx + ".s").to(device) if pfx + ".s" in names else None
+        w = rd.get(pfx + ".w").to(device)
+        if s is None and w.is_floating_point():
+            w = w.to(dtype)
+        return Linear(w, get(pfx + ".b"), s, glu)
+
+    layers = []
+    for i in range(cfg.num_layers):
+        layers.append(LayerWeights(get(f"l{i}.ln1_w"), get(f"l{i}.ln1_b"), get(f"l{i}.ln2_w"), get(f"l{i}.ln2_b"),
+                                   lin(f"l{i}.qkv"), lin(f"l{i}.o"), lin(f"l{i}.up", glu=cfg.gated_mlp),
+                                   lin(f"l{i}.down")))
+    mw = ModelWeights(wte=get("wte"), wpe=get("wpe"), layers=layers, lnf_w=get("lnf_w"), lnf_b=get("lnf_b"),
+                      head=lin("head"))
+    if cfg.position == "rope":
+        mw.cos, mw.sin = ref.rope_tables(cfg.max_position_embeddings, cfg.rotary_dim, cfg.rope_theta, device)
+    return mw
+
+
+def shard_cache_path(root: str, model_dir: str, files: List[str], tp: int, rank: int, dtype: torch.dtype,
+                     fp8: bool) -> str:
+    """Cache file for (checkpoint identity, TP layout, dtype); identity = paths + sizes + mtimes."""
+    import hashlib
+
+    h = hashlib.sha1(os.path.abspath(model_dir).encode())
+    for f in sorted(files):
+        st = os.stat(f)
+        h.update(f"{os.path.basename(f)}:{st.st_size}:{int(st.st_mtime)}".encode())
+    tag = str(dtype).replace("torch.", "") + ("-fp8" if fp8 else "")
+    return os.path.join(root, h.hexdigest()[:16], f"tp{tp}-r{rank}-{tag}.safetensors")

@@ -1,5 +1,7 @@
 """CPU parity of the family-agnostic decoder vs HF transformers at fp32 (tiny random checkpoints
 loaded through the native safetensors reader), incl. paged-KV greedy decoding through the engine."""
+import os
+
 import pytest
 import torch
 
@@ -99,3 +101,24 @@ def test_random_weights_shapes():
     assert L.qkv.w.shape == ((plan.nh_l + 2 * plan.nkv_l) * cfg.head_dim, cfg.hidden_size)
     assert L.up.w.shape == (2 * plan.F_l, cfg.hidden_size) and L.up.glu
     assert L.o.b is None and w.head.w.shape[0] == plan.v_l
+
+
+@pytest.mark.parametrize("name", ["llama", "gpt2", "gptj"])
+def test_shard_cache_roundtrip(tmp_path, name):
+    """Per-rank shard cache: the second build mmaps the cached shard, same logits."""
+    from llmss_amd.engine import build_model
+    from llmss_amd.models.decoder import StepInput
+
+    d = str(tmp_path / name)
+    save_hf_model(name, d, vocab=101)
+    cache = str(tmp_path / "cache")
+    m1 = build_model(d, None, "fp32", "cpu", shard_cache=cache)
+    files = [os.path.join(r, f) for r, _, fs in os.walk(cache) for f in fs]
+    assert len(files) == 1 and files[0].endswith("tp1-r0-float32.safetensors")
+    m2 = build_model(d, None, "fp32", "cpu", shard_cache=cache)
+    ids = torch.tensor([5, 17, 3, 99, 42])
+    inp = StepInput(kind="prefill", input_ids=ids, positions=torch.arange(5), slots=None,
+                    cu_seqlens=torch.tensor([0, 5], dtype=torch.int32), max_seqlen=5,
+                    last_idx=torch.tensor([4]))
+    kv1, kv2 = m1.allocate_kv_cache(4, 4), m2.allocate_kv_cache(4, 4)
+    assert torch.equal(m1(inp, kv1), m2(inp, kv2))
