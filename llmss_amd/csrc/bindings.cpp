@@ -38,6 +38,7 @@ void launch_add_norm_partial(const void* part, int S, int64_t slab, const void* 
 void launch_sample(const void* logits, int64_t ld, bool fp32_logits, int B, int V, const void* temperature,
                    const void* top_k, const void* top_p, const void* seeds, void* out, void* out2, hipStream_t st);
 void launch_quant_fp8_rows(const void* w, void* q, void* scale, int64_t N, int64_t K, hipStream_t st);
+void launch_dequant_fp8_rows(const void* q, const void* scale, void* w, int64_t N, int64_t K, hipStream_t st);
 
 void register_runtime(py::module_& m);  // host-side C++ runtime (runtime.cpp)
 
@@ -99,6 +100,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("quant_fp8_rows", [](uintptr_t w, uintptr_t q, uintptr_t scale, int64_t N, int64_t K, uintptr_t st) {
     launch_quant_fp8_rows(CP(w), P(q), P(scale), N, K, S(st));
+  });
+  m.def("dequant_fp8_rows", [](uintptr_t q, uintptr_t scale, uintptr_t w, int64_t N, int64_t K, uintptr_t st) {
+    launch_dequant_fp8_rows(CP(q), CP(scale), P(w), N, K, S(st));
   });
   register_runtime(m);
 }

@@ -68,14 +68,26 @@ struct QkvIn {
     if (part) {
 #pragma unroll
       for (int i = 0; i < W; ++i) v[i] = 0.f;
-      for (int z = 0; z < S; ++z) {
+      // up to 8 slabs issued together (a runtime-bounded loop would serialise one round trip per slab)
+      f32x4 x[8][W / 4];
+#pragma unroll
+      for (int z = 0; z < 8; ++z)
+#pragma unroll
+        for (int q = 0; q < W / 4; ++q)
+          x[z][q] = *reinterpret_cast<const f32x4*>(part + min(z, S - 1) * slab + e + 4 * q);
+#pragma unroll
+      for (int z = 0; z < 8; ++z)
+#pragma unroll
+        for (int q = 0; q < W / 4; ++q)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[4 * q + i] += z < S ? x[z][q][i] : 0.f;
+      for (int z = 8; z < S; ++z)
 #pragma unroll
         for (int q = 0; q < W / 4; ++q) {
-          const f32x4 x = *reinterpret_cast<const f32x4*>(part + z * slab + e + 4 * q);
+          const f32x4 y = *reinterpret_cast<const f32x4*>(part + z * slab + e + 4 * q);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[4 * q + i] += x[i];
+          for (int i = 0; i < 4; ++i) v[4 * q + i] += y[i];
         }
-      }
 #pragma unroll
       for (int i = 0; i < W; ++i) v[i] = bf2f(f2bf(v[i] + (bias ? bf2f(bias[e + i]) : 0.f)));
     } else if constexpr (W == 8) {

@@ -15,7 +15,9 @@
 
 // PART: x is not a bf16 tensor but S fp32 split-K partial slabs of the preceding GEMM
 // (part[s*slab + row*H + col]) plus an optional bf16 bias - the split-K reduction is fused here.
-template <int MAXC, bool RMS, bool HAS_RES, bool HAS_BIAS, bool PART>
+// PS: 0 = bf16 input; > 0 = that many partial slabs (compile-time: every load is issued before
+// the first add - a runtime trip count would serialise one memory round trip per slab); -1 = S.
+template <int MAXC, bool RMS, bool HAS_RES, bool HAS_BIAS, int PS>
 __global__ __launch_bounds__(256) void add_norm_kernel(const bf16_t* __restrict__ x, int64_t x_stride,
                                                        const bf16_t* res_in, bf16_t* res_out,
                                                        const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
@@ -31,15 +33,28 @@ __global__ __launch_bounds__(256) void add_norm_kernel(const bf16_t* __restrict_
   for (int c = 0; c < MAXC; ++c) {
     const int ch = threadIdx.x + c * blockDim.x;
     if (ch < nchunk) {
-      if constexpr (PART) {
+      if constexpr (PS != 0) {
         const float* pr = part + (int64_t)row * H + ch * 8;
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
-        for (int sp = 0; sp < S; ++sp) {
-          const f32x4 p0 = *reinterpret_cast<const f32x4*>(pr + sp * slab);
-          const f32x4 p1 = *reinterpret_cast<const f32x4*>(pr + sp * slab + 4);
+        if constexpr (PS > 0) {
+          f32x4 p[PS][2];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) { v[c][j] += p0[j]; v[c][4 + j] += p1[j]; }
+          for (int sp = 0; sp < PS; ++sp) {
+            p[sp][0] = *reinterpret_cast<const f32x4*>(pr + sp * slab);
+            p[sp][1] = *reinterpret_cast<const f32x4*>(pr + sp * slab + 4);
+          }
+#pragma unroll
+          for (int sp = 0; sp < PS; ++sp)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { v[c][j] += p[sp][0][j]; v[c][4 + j] += p[sp][1][j]; }
+        } else {
+          for (int sp = 0; sp < S; ++sp) {
+            const f32x4 p0 = *reinterpret_cast<const f32x4*>(pr + sp * slab);
+            const f32x4 p1 = *reinterpret_cast<const f32x4*>(pr + sp * slab + 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { v[c][j] += p0[j]; v[c][4 + j] += p1[j]; }
+          }
         }
         if (xbias) {
           u16x8 bb = *reinterpret_cast<const u16x8*>(xbias + ch * 8);
@@ -110,7 +125,7 @@ __global__ __launch_bounds__(256) void add_norm_kernel(const bf16_t* __restrict_
   }
 }
 
-template <bool RMS, bool HAS_RES, bool HAS_BIAS, bool PART = false>
+template <bool RMS, bool HAS_RES, bool HAS_BIAS, int PART = 0>
 static void launch_norm_t(const bf16_t* x, int64_t xs, const bf16_t* ri, bf16_t* ro, const bf16_t* w,
                           const bf16_t* b, bf16_t* y, int64_t ys, int T, int H, float eps, hipStream_t st,
                           const float* part = nullptr, int S = 0, int64_t slab = 0, const bf16_t* xbias = nullptr) {
@@ -171,7 +186,17 @@ void launch_add_norm_partial(const void* part, int S, int64_t slab, const void* 
   auto W = (const bf16_t*)w;
   auto B = (const bf16_t*)b;
   auto Y = (bf16_t*)y;
-  if (rms) launch_norm_t<true, true, false, true>(nullptr, 0, RI, RO, W, B, Y, y_stride, T, H, eps, st, P, S, slab, XB);
-  else if (b) launch_norm_t<false, true, true, true>(nullptr, 0, RI, RO, W, B, Y, y_stride, T, H, eps, st, P, S, slab, XB);
-  else launch_norm_t<false, true, false, true>(nullptr, 0, RI, RO, W, B, Y, y_stride, T, H, eps, st, P, S, slab, XB);
+#define LNP(PS_)                                                                                                   \
+  do {                                                                                                             \
+    if (rms) launch_norm_t<true, true, false, PS_>(nullptr, 0, RI, RO, W, B, Y, y_stride, T, H, eps, st, P, S, slab, XB); \
+    else if (b) launch_norm_t<false, true, true, PS_>(nullptr, 0, RI, RO, W, B, Y, y_stride, T, H, eps, st, P, S, slab, XB); \
+    else launch_norm_t<false, true, false, PS_>(nullptr, 0, RI, RO, W, B, Y, y_stride, T, H, eps, st, P, S, slab, XB); \
+  } while (0)
+  switch (S) {
+    case 2: LNP(2); break;
+    case 4: LNP(4); break;
+    case 8: LNP(8); break;
+    default: LNP(-1); break;
+  }
+#undef LNP
 }

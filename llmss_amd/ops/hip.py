@@ -245,6 +245,31 @@ class PartialSum:
         return True
 
 
+_FP8_PREFILL_M = 128  # above this, fp8 weights are expanded to bf16 and the compute-bound tile kernels run
+
+
+class _DequantScratch:
+    def __init__(self):
+        self.buf = None
+
+    def get(self, numel, device):
+        if self.buf is None or self.buf.numel() < numel or self.buf.device != device:
+            self.buf = torch.empty(numel, dtype=torch.bfloat16, device=device)
+        return self.buf
+
+
+_DEQ = _DequantScratch()
+
+
+def dequant_fp8_rows(q, scale, out=None):
+    N, K = q.shape
+    _check(q.dtype == torch.uint8 and q.is_contiguous() and K % 8 == 0, "fp8 weight [N, K] uint8, K % 8 == 0")
+    _check(scale.dtype == torch.float32 and scale.numel() == N and scale.is_contiguous(), "scale [N] fp32")
+    w = out if out is not None else torch.empty(N, K, dtype=torch.bfloat16, device=q.device)
+    lib().dequant_fp8_rows(q.data_ptr(), scale.data_ptr(), w.data_ptr(), N, K, _stream())
+    return w
+
+
 def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hint=0, split_hint=0,
            partial_ok=False):
     M, K = x.shape
@@ -253,6 +278,10 @@ def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hi
     if fp8:
         _check(w.dtype == torch.uint8 and w.is_contiguous() and w.is_cuda, "fp8 weight stored as uint8 [N, K]")
         _check(w_scale.dtype == torch.float32 and w_scale.numel() == w.shape[0], "w_scale [N] fp32")
+        if M > _FP8_PREFILL_M and not nt_hint and not torch.cuda.is_current_stream_capturing():
+            wd = _DEQ.get(w.numel(), x.device)[: w.numel()].view(w.shape)
+            dequant_fp8_rows(w, w_scale, out=wd)
+            return linear(x, wd, bias, act, glu, None, out, 0, split_hint, partial_ok)
     else:
         _bf16_rows(w, "w")
         _check(w.is_contiguous(), "w contiguous")

@@ -173,6 +173,10 @@ def test_gemm_fp8(M):
     assert ((a - b).abs() <= 0.125 * b.abs() + 2 ** -9).all()  # at most one e4m3 ulp of rounding difference
     ref = R.linear(x.float(), q, None, w_scale=s)
     close(H.linear(x, q, None, w_scale=s), ref, 2e-2)
+    xb = rnd(300, K)  # prefill size: fp8 weights expanded to bf16, big-tile path
+    close(H.linear(xb, q, None, w_scale=s), R.linear(xb.float(), q, None, w_scale=s), 3e-2)
+    wd = H.dequant_fp8_rows(q, s)
+    close(wd, R.dequant_fp8(q, s), 1e-6, rtol=1e-2)
 
 
 def test_sample_greedy_and_filters():
