@@ -21,6 +21,7 @@ followed by an all-gather of [B, V/tp] logits.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
 
@@ -56,6 +57,9 @@ class DecoderLM:
         self.scale = cfg.head_dim ** -0.5
         self.rms = cfg.norm == "rmsnorm"
         self.act = "none" if cfg.gated_mlp else cfg.activation
+        # TP all-reduce / GEMM overlap for large steps (prefill): row chunks of this many tokens
+        self.overlap_rows = int(os.environ.get("LLMSS_TP_OVERLAP_ROWS", "4096"))
+        self._comm_stream = None
 
     @property
     def device(self):
@@ -88,6 +92,37 @@ class DecoderLM:
         return ops.attn_decode(qkv, kc, vc, inp.block_tables, inp.ctx_lens, p.nh_l, p.nkv_l, D, self.scale,
                                inp.max_ctx, splits=inp.decode_splits)
 
+    def _reduce_rows(self, fn, *inputs) -> torch.Tensor:
+        """``all_reduce(fn(*inputs))`` for a row-parallel projection (or a whole MLP).
+
+        Large steps run in row chunks: chunk c's RCCL all-reduce is issued on a high-priority comm
+        stream while the compute stream already runs chunk c+1's GEMMs, so the per-layer
+        all-reduce hides behind the next GEMM (prefill at TP=8 moves ~0.5 GB per all-reduce). Decode
+        steps (a few MB, latency-bound) keep one all-reduce.
+        """
+        if not self.tp.is_real:
+            return fn(*inputs)
+        M = inputs[0].shape[0]
+        step = self.overlap_rows
+        if M <= step or step <= 0:
+            return self.tp.all_reduce(fn(*inputs))
+        if not inputs[0].is_cuda:  # gloo / CPU: same chunking (numerics), no streams
+            return torch.cat([self.tp.all_reduce(fn(*(t[r:r + step] for t in inputs))) for r in range(0, M, step)])
+        cur = torch.cuda.current_stream()
+        if self._comm_stream is None:
+            self._comm_stream = torch.cuda.Stream(device=inputs[0].device, priority=-1)
+        comm = self._comm_stream
+        outs = []
+        for r in range(0, M, step):
+            y = fn(*(t[r:r + step] for t in inputs))
+            comm.wait_stream(cur)  # chunk r's GEMM done
+            with torch.cuda.stream(comm):
+                self.tp.all_reduce(y)
+            y.record_stream(comm)
+            outs.append(y)
+        cur.wait_stream(comm)
+        return torch.cat(outs)
+
     def hidden_states(self, inp: StepInput, kv_caches) -> torch.Tensor:
         cfg, w = self.cfg, self.w
         eps, rms = cfg.norm_eps, self.rms
@@ -100,16 +135,17 @@ class DecoderLM:
             y, residual = ops.add_norm(delta, L.ln1_w, L.ln1_b, eps, rms, residual)
             # column-parallel QKV: its split-K partials are summed inside the rope/cache kernel
             a = self._attention(L.qkv(y, partial_ok=True), inp, kc, vc)
-            o = L.o(a, partial_ok=fuse and not cfg.parallel_block)
-            if cfg.parallel_block:
-                m = L.down(L.up(y, self.act))
-                o.add_(m)
-                delta = self.tp.all_reduce(o)
-            else:
-                o = self.tp.all_reduce(o)
+            if cfg.parallel_block:  # GPT-J: one all-reduce for attention + MLP
+                delta = self._reduce_rows(lambda a_, y_: L.o(a_).add_(L.down(L.up(y_, self.act))), a, y)
+            elif fuse:
+                # TP=1: the split-K partials of o / down are reduced inside the next add_norm
+                o = L.o(a, partial_ok=True)
                 y2, residual = ops.add_norm(o, L.ln2_w, L.ln2_b, eps, rms, residual)
-                # TP=1: the down-projection's split-K partials are reduced inside the next add_norm
-                delta = self.tp.all_reduce(L.down(L.up(y2, self.act), partial_ok=fuse))
+                delta = L.down(L.up(y2, self.act), partial_ok=True)
+            else:
+                o = self._reduce_rows(L.o, a)
+                y2, residual = ops.add_norm(o, L.ln2_w, L.ln2_b, eps, rms, residual)
+                delta = self._reduce_rows(lambda y_: L.down(L.up(y_, self.act)), y2)
         h, _ = ops.add_norm(delta, w.lnf_w, w.lnf_b, eps, rms, residual)
         return h
 

@@ -19,9 +19,11 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, ckpt, prompts, q):
+def _worker(rank, world, port, ckpt, prompts, q, overlap_rows=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
+    if overlap_rows is not None:  # row-chunked all-reduce / GEMM overlap path
+        os.environ["LLMSS_TP_OVERLAP_ROWS"] = str(overlap_rows)
     torch.set_num_threads(1)
     from llmss_amd.engine import LLMEngine, SamplingParams, build_model
     from llmss_amd.parallel.dist import initialize_distributed
@@ -38,11 +40,11 @@ def _worker(rank, world, port, ckpt, prompts, q):
     torch.distributed.destroy_process_group()
 
 
-def _run(world, ckpt, prompts):
+def _run(world, ckpt, prompts, overlap_rows=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, ckpt, prompts, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, ckpt, prompts, q, overlap_rows)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=240)
@@ -52,8 +54,10 @@ def _run(world, ckpt, prompts):
     return res
 
 
-@pytest.mark.parametrize("name,world", [("llama", 2), ("gptj", 2), ("bigcode", 4), ("gpt2", 2), ("bigcode_mha", 2)])
-def test_tp_matches_single(tmp_path, name, world):
+@pytest.mark.parametrize("name,world,overlap", [("llama", 2, None), ("gptj", 2, None), ("bigcode", 4, None),
+                                                ("gpt2", 2, None), ("bigcode_mha", 2, None), ("llama", 2, 4),
+                                                ("gptj", 2, 5)])
+def test_tp_matches_single(tmp_path, name, world, overlap):
     d = str(tmp_path / name)
     save_hf_model(name, d, vocab=101)  # 101 % world != 0 -> exercises the padded vocab-parallel head
     prompts = [[(3 * i + 7 * j) % 100 for j in range(5 + 2 * i)] for i in range(3)]
@@ -64,6 +68,6 @@ def test_tp_matches_single(tmp_path, name, world):
     ref_g = eng.generate(prompts, SamplingParams(max_new_tokens=8, is_greedy=True, ignore_eos=True))
     ref_s = eng.generate(prompts, [SamplingParams(max_new_tokens=8, temperature=0.9, top_k=20, top_p=0.9, seed=5 + i,
                                                   ignore_eos=True) for i in range(len(prompts))])
-    g, s = _run(world, d, prompts)
+    g, s = _run(world, d, prompts, overlap)
     assert g == ref_g
     assert s == ref_s
