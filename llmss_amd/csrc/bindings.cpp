@@ -25,6 +25,12 @@ void launch_attn_decode(const void* q, int64_t q_stride, const void* kc, const v
 void launch_attn_prefill(const void* qkv, int64_t row_stride, const void* cu_seqlens, void* out, int64_t out_stride,
                          int B, int max_seqlen, int nh, int nkv, int D, int k_off, int v_off, float scale,
                          hipStream_t st);
+void launch_attn_decode_fused(const void* qkv, int64_t q_stride, const void* part, int S, int64_t slab,
+                              const void* bias, int N, const void* pos, const void* cos_t, const void* sin_t,
+                              const void* slots, int rot, int style, int k_off, int v_off, void* kc, void* vc,
+                              const void* block_tables, int bt_stride, const void* ctx_lens, void* out,
+                              int64_t out_stride, void* part_o, void* part_ml, int B, int nh, int nkv, int D,
+                              int block_size, int nsplit, int part_size, float scale, hipStream_t st);
 int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_fp8, const void* w_scale,
                 const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace,
                 int64_t ws_bytes, int nt_hint, int split_hint, bool partial_out, hipStream_t st);
@@ -66,6 +72,15 @@ PYBIND11_MODULE(_C, m) {
                           int nsplit, int psize, float scale, uintptr_t st) {
     launch_attn_decode(CP(q), qs, CP(kc), CP(vc), CP(bt), bts, CP(cl), P(out), os, P(po), P(pml), B, nh, nkv, D, bs,
                        nsplit, psize, scale, S(st));
+  });
+  m.def("attn_decode_fused", [](uintptr_t qkv, int64_t qs, uintptr_t part, int S, int64_t slab, uintptr_t bias, int N,
+                                uintptr_t pos, uintptr_t cos_t, uintptr_t sin_t, uintptr_t slots, int rot, int style,
+                                int k_off, int v_off, uintptr_t kc, uintptr_t vc, uintptr_t bt, int bts, uintptr_t cl,
+                                uintptr_t out, int64_t os, uintptr_t po, uintptr_t pml, int B, int nh, int nkv, int D,
+                                int bs, int nsplit, int psize, float scale, uintptr_t st) {
+    launch_attn_decode_fused(CP(qkv), qs, CP(part), S, slab, CP(bias), N, CP(pos), CP(cos_t), CP(sin_t), CP(slots), rot,
+                             style, k_off, v_off, P(kc), P(vc), CP(bt), bts, CP(cl), P(out), os, P(po), P(pml), B, nh,
+                             nkv, D, bs, nsplit, psize, scale, S(st));
   });
   m.def("attn_prefill", [](uintptr_t qkv, int64_t rs, uintptr_t cu, uintptr_t out, int64_t os, int B, int maxlen,
                            int nh, int nkv, int D, int k_off, int v_off, float scale, uintptr_t st) {

@@ -33,6 +33,12 @@ from .config import ModelConfig
 from .weights import ModelWeights, ShardPlan, shard_plan
 
 
+def _hip_ops():
+    from ..ops import hip
+
+    return hip
+
+
 @dataclass
 class StepInput:
     kind: str  # "prefill" | "decode"
@@ -59,6 +65,9 @@ class DecoderLM:
         self.act = "none" if cfg.gated_mlp else cfg.activation
         # TP all-reduce / GEMM overlap for large steps (prefill): row chunks of this many tokens
         self.overlap_rows = int(os.environ.get("LLMSS_TP_OVERLAP_ROWS", "4096"))
+        # fused RoPE+KV-write+attention decode: correct, but measured slower (its prologue halves the
+        # attention kernel's occupancy), so opt-in
+        self.fused_decode = os.environ.get("LLMSS_FUSED_DECODE", "0") == "1"
         self._comm_stream = None
 
     @property
@@ -85,6 +94,14 @@ class DecoderLM:
     def _attention(self, qkv, inp: StepInput, kc, vc):
         cfg, p = self.cfg, self.plan
         D = cfg.head_dim
+        do_rope = cfg.position == "rope"
+        if inp.kind == "decode" and qkv.is_cuda and self.fused_decode and \
+                _hip_ops().fused_decode_ok(D, cfg.rotary_dim, cfg.rope_style, do_rope):
+            # one launch: RoPE + paged KV write of the new token + attention (no rope_cache kernel)
+            return _hip_ops().attn_decode_fused(
+                qkv, inp.positions, self.w.cos, self.w.sin, kc, vc, inp.slots, inp.block_tables, inp.ctx_lens,
+                p.nh_l, p.nkv_l, D, cfg.rotary_dim, cfg.rope_style, self.scale, inp.max_ctx, do_rope=do_rope,
+                splits=inp.decode_splits)
         qkv = ops.rope_cache(qkv, inp.positions, self.w.cos, self.w.sin, kc, vc, inp.slots, p.nh_l, p.nkv_l, D,
                              cfg.rotary_dim, cfg.rope_style, do_rope=cfg.position == "rope")
         if inp.kind == "prefill":

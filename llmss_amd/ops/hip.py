@@ -200,6 +200,61 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale, 
     return y
 
 
+def fused_decode_ok(D: int, rot: int, style: str, do_rope: bool) -> bool:
+    """Whether attn_decode_fused supports this rotary setup (neox partners need a power-of-two lane stride)."""
+    if D not in (64, 128, 256):
+        return False
+    if not do_rope or rot == 0:
+        return True
+    if style == "gptj":
+        return rot % 8 == 0 and rot <= D
+    return rot >= 16 and rot <= D and (rot & (rot - 1)) == 0
+
+
+def attn_decode_fused(qkv, positions, cos, sin, k_cache, v_cache, slots, block_tables, ctx_lens, nh, nkv, D, rot,
+                      style, scale, max_ctx, do_rope=True, out=None, splits=None):
+    """Decode attention with the new token's RoPE + paged KV-cache write fused in (replaces rope_cache +
+    attn_decode). ``qkv`` = the QKV GEMM output [B, (nh+2nkv)*D] or its split-K :class:`PartialSum`."""
+    part = qkv if isinstance(qkv, PartialSum) else None
+    N = (nh + 2 * nkv) * D
+    if part is not None:
+        _check(part.N == N, "partial qkv width")
+        B = part.M
+        qptr, qstride = 0, N
+    else:
+        _bf16_rows(qkv, "qkv")
+        _check(qkv.shape[1] >= N, "qkv too narrow")
+        B = qkv.shape[0]
+        qptr, qstride = qkv.data_ptr(), qkv.stride(0)
+    _check(fused_decode_ok(D, rot, style, do_rope), "unsupported head_dim / rotary setup for the fused path")
+    rot = rot if do_rope else 0
+    if rot:
+        _check(cos.dtype == torch.float32 and cos.is_contiguous() and cos.shape[1] == rot // 2, "cos table")
+        _check(sin.shape == cos.shape and sin.is_contiguous(), "sin table")
+    _check(positions.dtype == torch.int64 and positions.numel() >= B and positions.is_contiguous(), "positions")
+    _check(slots.dtype == torch.int64 and slots.numel() >= B and slots.is_contiguous(), "slots")
+    _check(k_cache.dtype == torch.bfloat16 and k_cache.is_contiguous() and k_cache.shape[1] == nkv
+           and k_cache.shape[3] == D, "k_cache [nb, nkv, bs, D]")
+    _check(v_cache.shape == k_cache.shape and v_cache.is_contiguous(), "v_cache")
+    _check(block_tables.dtype == torch.int32 and block_tables.dim() == 2 and block_tables.shape[0] >= B
+           and block_tables.stride(1) == 1, "block_tables int32 [B, maxb]")
+    _check(ctx_lens.dtype == torch.int32 and ctx_lens.numel() >= B and ctx_lens.is_contiguous(), "ctx_lens int32")
+    bs = k_cache.shape[2]
+    _check(block_tables.shape[1] * bs >= max_ctx, "block table too short for max_ctx")
+    nsplit, psize = splits if splits is not None else decode_splits(B, nkv, max_ctx, bs)
+    _check(nsplit * psize >= max_ctx, "splits do not cover max_ctx")
+    y = out if out is not None else torch.empty(B, nh * D, dtype=torch.bfloat16, device=k_cache.device)
+    po, pml = _DECODE_WS.get(B, nh, nsplit, D, k_cache.device) if nsplit > 1 else (None, None)
+    lib().attn_decode_fused(qptr, qstride, part.buf.data_ptr() if part else 0, part.S if part else 0,
+                            part.M * part.N if part else 0, _ptr(part.bias) if part else 0, N, positions.data_ptr(),
+                            _ptr(cos) if rot else 0, _ptr(sin) if rot else 0, slots.data_ptr(), int(rot),
+                            1 if style == "gptj" else 0, nh * D, (nh + nkv) * D, k_cache.data_ptr(),
+                            v_cache.data_ptr(), block_tables.data_ptr(), block_tables.stride(0), ctx_lens.data_ptr(),
+                            y.data_ptr(), y.stride(0), _ptr(po), _ptr(pml), B, nh, nkv, D, bs, nsplit, psize,
+                            float(scale), _stream())
+    return y
+
+
 # ------------------------------------------------------------------------------------- GEMM
 class GemmWorkspace:
     def __init__(self):

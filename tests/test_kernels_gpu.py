@@ -328,3 +328,43 @@ def test_sample_kept_set_exact(V, k, p, temp):
     for b in range(B):
         if len(sets[b]) <= 3:
             assert seen[b] == sets[b]
+
+
+@pytest.mark.parametrize("style,D,rot,nh,nkv", [("neox", 128, 128, 8, 2), ("gptj", 256, 64, 4, 4), ("neox", 64, 32, 4, 1),
+                                               ("none", 64, 0, 8, 8)])
+@pytest.mark.parametrize("partial", [False, True])
+def test_attn_decode_fused_rope(style, D, rot, nh, nkv, partial):
+    """Fused decode (RoPE + KV write of the new token + attention) == rope_cache followed by attn_decode."""
+    torch.manual_seed(0)
+    B, bs, maxctx = 5, 16, 300
+    maxb = (maxctx + bs - 1) // bs
+    nb = B * maxb + 2
+    kc, vc = rnd(nb, nkv, bs, D), rnd(nb, nkv, bs, D)
+    bt = torch.randperm(nb, device=dev)[: B * maxb].view(B, maxb).to(torch.int32)
+    ctx = torch.tensor([1, 17, 300, 64, 0], dtype=torch.int32, device=dev)  # row 4 = padding (ctx 0, slot -1)
+    pos = (ctx.long() - 1).clamp(min=0)
+    slots = torch.tensor([int(bt[b, int(pos[b]) // bs]) * bs + int(pos[b]) % bs for b in range(B)], device=dev)
+    slots[4] = -1
+    N = (nh + 2 * nkv) * D
+    if partial:
+        K = 512
+        x, w, bias = rnd(B, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
+        src = H.linear(x, w, bias, partial_ok=True, split_hint=4)
+        qkv = H.linear(x, w, bias)
+    else:
+        qkv = rnd(B, N)
+        src = qkv
+    do_rope = style != "none"
+    sty = "neox" if style == "none" else style
+    cos, sin = R.rope_tables(512, max(rot, 8), 10000.0, dev)
+    sc = 1 / math.sqrt(D)
+    k1, v1 = kc.clone(), vc.clone()
+    out = H.attn_decode_fused(src, pos, cos, sin, k1, v1, slots, bt, ctx, nh, nkv, D, rot, sty, sc, maxctx,
+                              do_rope=do_rope)
+    k2, v2, q2 = kc.clone(), vc.clone(), qkv.clone()
+    H.rope_cache(q2, pos, cos, sin, k2, v2, slots, nh, nkv, D, rot, sty, do_rope=do_rope)
+    ref = H.attn_decode(q2, k2, v2, bt, ctx, nh, nkv, D, sc, maxctx)
+    close(out[:4], ref[:4], 2e-2)
+    assert bool((out[4] == 0).all())
+    close(k1, k2, 2e-2)
+    close(v1, v2, 1e-2)
