@@ -77,6 +77,9 @@ def main():
                     pnt, psp = H.lib().gemm_plan(M, N, K, False)
                     if pnt >= 256:
                         cfgs += [(pnt | (64 << 8), psp)]
+                if a.sweep and M > 32 and not a.fp8:  # stream-K: (tile | depth | 128) << 8, split = WGs per CU
+                    cfgs += [((t | d | 128) << 8, g) for t, d in ((1, 0), (1, 16), (2, 16), (2, 32), (3, 16), (3, 32))
+                             for g in (1, 2, 3)]
                 if a.sweep and M >= 256 and not a.fp8:
                     cfgs += [(4 << 8, 1), (1 << 8, 1)]
                 best = None

@@ -757,6 +757,176 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16_t* __restri
 }
 
 // -------------------------------------------------------------------------------------------
+// stream-K tiled GEMM (mid-size M: TP-sharded decode at M = 128-512, mid prefill). Split-K grids
+// leave CUs unevenly loaded (e.g. 352 blocks on 256 CUs: some CUs run two, the rest one) and pay
+// a reduce launch. Here a persistent grid of G workgroups splits the flattened (tile, k-step)
+// iteration space into G equal contiguous ranges; the LDS ring of the tiled kernel runs straight
+// across tile boundaries. A tile whose k-range spans several workgroups is combined in-kernel:
+// every segment stores its fp32 accumulators (register layout, 16 B per lane, coalesced), then
+// draws a ticket (agent-scope release fence + relaxed atomic, guide 'splitk-seam' recipe); the
+// last arriver acquires, adds the other segments and runs the epilogue. Counters reset themselves.
+// -------------------------------------------------------------------------------------------
+__device__ __forceinline__ int sk_block_of(int64_t x, int64_t U, int G) {  // block whose range holds unit x
+  int g = (int)((x * G) / U);
+  while (g + 1 < G && (int64_t)(g + 1) * U / G <= x) ++g;
+  while (g > 0 && (int64_t)g * U / G > x) --g;
+  return g;
+}
+
+template <int MTW, int NTW>
+__device__ __forceinline__ void tile_epilogue(const f32x4 (&acc)[MTW][NTW], bf16_t* __restrict__ Y, int64_t ldy,
+                                              const bf16_t* __restrict__ bias, int M, int N, int m0, int n0, int wr,
+                                              int wc, int li, int g, int act, int glu) {
+  const int wn0 = n0 + wc * (NTW * 16);
+#pragma unroll
+  for (int mt = 0; mt < MTW; ++mt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wr * (MTW * 16) + mt * 16 + 4 * g + i;
+      if (m >= M) continue;
+      if (glu) {
+#pragma unroll
+        for (int p = 0; p < NTW / 2; ++p) {
+          const int ng = wn0 + 2 * p * 16 + li, nu = ng + 16;
+          if (nu < N) {
+            float gv = acc[mt][2 * p][i], uv = acc[mt][2 * p + 1][i];
+            if (bias) { gv += bf2f(bias[ng]); uv += bf2f(bias[nu]); }
+            Y[(int64_t)m * ldy + wn0 / 2 + p * 16 + li] = f2bf(silu(gv) * uv);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) {
+          const int n = wn0 + nt * 16 + li;
+          if (n < N) {
+            float v = acc[mt][nt][i];
+            if (bias) v += bf2f(bias[n]);
+            Y[(int64_t)m * ldy + n] = f2bf(apply_act(v, act));
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int NS, bool WNT>
+__global__ __launch_bounds__(256) void gemm_streamk_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                           const bf16_t* __restrict__ B, int64_t ldb,
+                                                           const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
+                                                           int64_t ldy, float* __restrict__ part,
+                                                           int* __restrict__ counters, int maxseg, int M, int N, int K,
+                                                           int act, int glu) {
+  constexpr int MTW = BM / 32, NTW = BN / 32;
+  constexpr int A_BYTES = BM * TBK * 2, B_BYTES = BN * TBK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int LOADS = BM / 32 + BN / 32;
+  constexpr int TILE_F = BM * BN;  // fp32 per partial tile
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE + 16];  // + ticket broadcast (one LDS object)
+  int* s_ticket = reinterpret_cast<int*>(smem + NS * STAGE);
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  const int wr = w >> 1, wc = w & 1;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
+  const int tiles = ntn * ntm, nk = (K + TBK - 1) / TBK;
+  const int U = tiles * nk;  // host guarantees < 2^31
+  const int G = gridDim.x;
+  const int u0 = (int)((int64_t)blockIdx.x * U / G), u1 = (int)((int64_t)(blockIdx.x + 1) * U / G);
+  if (u0 >= u1) return;
+
+  // (tile, k-step) of the next unit to stage, advanced incrementally: no divisions in the k-loop
+  int pf_t = u0 / nk, pf_k = u0 - (u0 / nk) * nk;
+  int pf_m0 = (pf_t / ntn) * BM, pf_n0 = (pf_t % ntn) * BN;
+  auto stage_next = [&](char* buf) {
+    tiled_stage<BM, BN, WNT>(A, lda, M, B, ldb, N, K, pf_m0, pf_n0, pf_k * TBK, buf, buf + A_BYTES, w, lane);
+    if (++pf_k == nk) {
+      pf_k = 0;
+      ++pf_t;
+      pf_m0 = (pf_t / ntn) * BM;
+      pf_n0 = (pf_t % ntn) * BN;
+    }
+  };
+
+  f32x4 acc[MTW][NTW];
+#pragma unroll
+  for (int a = 0; a < MTW; ++a)
+#pragma unroll
+    for (int b = 0; b < NTW; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int j = 0; j < NS - 1; ++j)
+    if (u0 + j < u1) stage_next(smem + j * STAGE);
+  int cur = 0;
+  int t = u0 / nk, kk = u0 - (u0 / nk) * nk;  // unit being computed
+  for (int u = u0; u < u1; ++u) {
+    wait_vmcnt_upto<LOADS, NS - 2>(min(u1 - 1 - u, NS));
+    lds_barrier();
+    char* cA = smem + cur * STAGE;
+    if (u + NS - 1 < u1) stage_next(smem + (cur == 0 ? NS - 1 : cur - 1) * STAGE);
+    if (kk == nk - 1 && (K % TBK)) tiled_compute<MTW, NTW, true>(cA, cA + A_BYTES, acc, wr, wc, li, g, kk * TBK, K);
+    else tiled_compute<MTW, NTW, false>(cA, cA + A_BYTES, acc, wr, wc, li, g, kk * TBK, K);
+    cur = cur == NS - 1 ? 0 : cur + 1;
+
+    if (u + 1 != u1 && kk != nk - 1) {  // segment continues
+      ++kk;
+      continue;
+    }
+    // ---- segment end: tile t, this workgroup's k-steps up to kk
+    const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
+    const int tu0 = t * nk;
+    const bool whole = u0 <= tu0 && kk == nk - 1;
+    if (whole) {
+      tile_epilogue<MTW, NTW>(acc, Y, ldy, bias, M, N, m0, n0, wr, wc, li, g, act, glu);
+    } else {
+      const int gfirst = sk_block_of(tu0, U, G), glast = sk_block_of((int64_t)tu0 + nk - 1, U, G);
+      const int nseg = glast - gfirst + 1, seg = (int)blockIdx.x - gfirst;
+      float* pt = part + (int64_t)t * maxseg * TILE_F;
+#pragma unroll
+      for (int mt = 0; mt < MTW; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt)
+          *reinterpret_cast<f32x4*>(pt + (int64_t)seg * TILE_F + (((w * MTW + mt) * NTW + nt) * 64 + lane) * 4) =
+              acc[mt][nt];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        *s_ticket = __hip_atomic_fetch_add(&counters[t], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (*s_ticket == nseg - 1) {  // last arriver: combine and finish the tile
+        if (threadIdx.x == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          counters[t] = 0;  // ready for the next launch
+        }
+        __syncthreads();
+        for (int s2 = 0; s2 < nseg; ++s2) {
+          if (s2 == seg) continue;
+#pragma unroll
+          for (int mt = 0; mt < MTW; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NTW; ++nt) {
+              const f32x4 o = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(
+                  pt + (int64_t)s2 * TILE_F + (((w * MTW + mt) * NTW + nt) * 64 + lane) * 4));
+#pragma unroll
+              for (int i = 0; i < 4; ++i) acc[mt][nt][i] += o[i];
+            }
+        }
+        tile_epilogue<MTW, NTW>(acc, Y, ldy, bias, M, N, m0, n0, wr, wc, li, g, act, glu);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stores / reads above must not count as ring stages
+#pragma unroll
+    for (int a = 0; a < MTW; ++a)
+#pragma unroll
+      for (int b = 0; b < NTW; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    ++t;
+    kk = 0;
+  }
+}
+
+// -------------------------------------------------------------------------------------------
 // host dispatch
 // -------------------------------------------------------------------------------------------
 template <int MT, int NT, int KC, bool FP8W, int VARIANT>
@@ -939,6 +1109,11 @@ void gemm_tiled_plan(int M, int N, int K, int* tsel_io, int* split_io, bool glu)
   if (tsel == 4 && K % 64) tsel = 1;
   const int hint_bits = tsel & ~15;
   tsel &= 15;
+  if (hint_bits & 128) {  // stream-K: output is final (no slabs); split_io carries workgroups per CU
+    *tsel_io = tsel | hint_bits;
+    if (*split_io <= 0) *split_io = 2;
+    return;
+  }
   if (tsel == 4) {  // big-tile kernel: no split-K, no stage option
     *tsel_io = 4;
     *split_io = 1;
@@ -961,6 +1136,71 @@ void gemm_tiled_plan(int M, int N, int K, int* tsel_io, int* split_io, bool glu)
   *split_io = s;
 }
 
+static bool wnt_ok(int tsel_raw, int M, int tsel) {
+  int bm, bn;
+  tile_dims(tsel & 15, &bm, &bn);
+  return !(tsel_raw & 64) && M <= bm;
+}
+
+// per-tile arrival counters of the stream-K combine: zeroed once, reset by every last arriver
+static int* g_sk_counters = nullptr;
+static int g_sk_capacity = 0;
+
+static int* sk_counters(int n) {
+  if (n <= g_sk_capacity) return g_sk_counters;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(nullptr, &cs);
+  if (cs != hipStreamCaptureStatusNone) throw std::runtime_error("stream-K counters must be allocated before capture");
+  int cap = std::max(n, 1 << 16);
+  int* p = nullptr;
+  if (hipMalloc(&p, (size_t)cap * sizeof(int)) != hipSuccess) throw std::runtime_error("stream-K counters: hipMalloc");
+  if (hipMemset(p, 0, (size_t)cap * sizeof(int)) != hipSuccess) throw std::runtime_error("stream-K counters: memset");
+  (void)hipDeviceSynchronize();
+  g_sk_counters = p;  // the old (smaller) buffer is left to the process: launches may still reference it
+  g_sk_capacity = cap;
+  return p;
+}
+
+void gemm_reserve_streamk(int n) { sk_counters(n); }
+
+static bool launch_streamk(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, const bf16_t* B, bf16_t* Y,
+                           int64_t ldy, int M, int N, int K, int act, int g, int tsel, int ns, int per_cu,
+                           void* workspace, int64_t ws_bytes, bool wnt, hipStream_t st) {
+  int bm, bn;
+  tile_dims(tsel, &bm, &bn);
+  if (tsel == 1 && ns > 3) ns = 3;
+  if (tsel == 2 && ns > 4) ns = 4;
+  if (ns == 6) ns = 4;
+  const int tiles = tiles_of(M, N, bm, bn), nk = (K + TBK - 1) / TBK;
+  const int64_t U = (int64_t)tiles * nk;
+  if (U >= (1LL << 31)) return false;
+  const int G = (int)std::min<int64_t>(U, 256LL * std::max(1, std::min(per_cu, 8)));
+  const int64_t per = U / G;  // >= 1
+  const int maxseg = (int)std::min<int64_t>(G, (nk + per - 1) / per + 1);
+  if ((int64_t)tiles * maxseg * bm * bn * 4 > ws_bytes) return false;
+  int* cnt = sk_counters(tiles);
+  float* part = (float*)workspace;
+#define SK(BM_, BN_, NS_)                                                                                          \
+  do {                                                                                                             \
+    if (wnt)                                                                                                       \
+      gemm_streamk_kernel<BM_, BN_, NS_, true><<<G, 256, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, cnt, maxseg, M, N, \
+                                                                   K, act, g);                                     \
+    else                                                                                                           \
+      gemm_streamk_kernel<BM_, BN_, NS_, false><<<G, 256, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, cnt, maxseg, M, \
+                                                                    N, K, act, g);                                 \
+  } while (0)
+  if (tsel == 1) {
+    if (ns == 3) SK(128, 128, 3); else SK(128, 128, 2);
+  } else if (tsel == 2) {
+    if (ns == 4) SK(64, 128, 4); else if (ns == 3) SK(64, 128, 3); else SK(64, 128, 2);
+  } else {
+    if (ns == 4) SK(64, 64, 4); else if (ns == 3) SK(64, 64, 3); else SK(64, 64, 2);
+  }
+#undef SK
+  HIP_CHECK_LAUNCH();
+  return true;
+}
+
 int launch_tiled(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, const bf16_t* B, bf16_t* Y, int64_t ldy,
                  int M, int N, int K, int act, int g, int tsel, int split_hint, void* workspace, int64_t ws_bytes,
                  bool partial_out, hipStream_t st) {
@@ -972,20 +1212,26 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, con
   tsel &= 15;
   if (tsel == 1 && ns > 3) ns = 3;  // 128x128 x 4 stages would exceed the 160 KiB LDS
   if (tsel == 2 && ns > 4) ns = 4;
+  if (tsel == 4) {
+    gemm_big_kernel<<<tiles_of(M, N, 256, 256), 512, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, M, N, K, act, g);
+    HIP_CHECK_LAUNCH();
+    return 0;
+  }
+  if (tsel_raw & 128) {
+    if (launch_streamk(X, ldx, W, ldw, B, Y, ldy, M, N, K, act, g, tsel, ns, s, workspace, ws_bytes,
+                       wnt_ok(tsel_raw, M, tsel), st))
+      return 0;
+    s = 1;  // workspace too small for the partial tiles: plain tiled launch
+  }
   int bm, bn;
   tile_dims(tsel, &bm, &bn);
   const int nt = tiles_of(M, N, bm, bn);
   if ((int64_t)s * M * N * 4 > ws_bytes) s = 1;
   float* part = s > 1 ? (float*)workspace : nullptr;
   const int act_k = s > 1 ? 0 : act, glu_k = s > 1 ? 0 : g;
-  if (tsel == 4) {
-    gemm_big_kernel<<<tiles_of(M, N, 256, 256), 512, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, M, N, K, act, g);
-    HIP_CHECK_LAUNCH();
-    return 0;
-  }
   dim3 grid(nt, s);
   // non-temporal weight staging when every weight tile is read by exactly one workgroup row
-  const bool wnt = !(tsel_raw & 64) && M <= bm;
+  const bool wnt = wnt_ok(tsel_raw, M, tsel);
 #define LT(BM_, BN_, NS_)                                                                                          \
   do {                                                                                                             \
     if (wnt)                                                                                                       \
@@ -1018,7 +1264,9 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, con
 
 void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk) {
   if (gemm_tuned_get(M, N, K, false, w_fp8, nt, splitk)) {
-    if (*nt >> 8) {  // tiled hint: the split the kernel will really use
+    if ((*nt >> 8) & 128) {
+      *splitk = 1;  // stream-K finishes its tiles in-kernel: no partial slabs for the consumer
+    } else if (*nt >> 8) {  // tiled hint: the split the kernel will really use
       int tsel = *nt >> 8;
       gemm_tiled_plan(M, N, K, &tsel, splitk, false);
     }

@@ -53,6 +53,9 @@ def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, 
     for t, depths in tiles:
         for d in depths:
             out += [((t | d) << 8, s) for s in splits]
+    if M > 32:  # stream-K (tile | depth | 128) << 8, split = workgroups per CU
+        for t, d in ((1, 0), (1, 16), (2, 16), (2, 32), (3, 16), (3, 32)):
+            out += [((t | d | 128) << 8, g) for g in (1, 2, 3)]
     if M >= 256 and K % 64 == 0:
         out.append((4 << 8, 1))
     return out

@@ -368,3 +368,18 @@ def test_attn_decode_fused_rope(style, D, rot, nh, nkv, partial):
     assert bool((out[4] == 0).all())
     close(k1, k2, 2e-2)
     close(v1, v2, 1e-2)
+
+
+@pytest.mark.parametrize("tile,stages", [(1, 2), (1, 3), (2, 2), (2, 4), (3, 3), (3, 4)])
+@pytest.mark.parametrize("per_cu", [1, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(512, 1536, 4096), (300, 2752, 1376), (64, 4096, 11008), (130, 544, 208)])
+def test_gemm_streamk(tile, stages, per_cu, M, N, K):
+    """Stream-K tiled GEMM: tiles split across workgroups, combined in-kernel by the last arriver."""
+    torch.manual_seed(0)
+    x, w, b = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
+    hint = (tile | {2: 0, 3: 16, 4: 32}[stages] | 128) << 8
+    for _ in range(2):  # second launch reuses the self-reset arrival counters
+        close(H.linear(x, w, b, act="gelu_tanh", nt_hint=hint, split_hint=per_cu),
+              R.linear(x.float(), w.float(), b.float(), act="gelu_tanh"), 2e-2)
+    close(H.linear(x, w, None, glu=True, nt_hint=hint, split_hint=per_cu),
+          R.linear(x.float(), w.float(), None, glu=True), 2e-2)
