@@ -25,6 +25,7 @@ typedef float __attribute__((ext_vector_type(4))) f32x4;
 typedef float __attribute__((ext_vector_type(16))) f32x16;
 typedef float __attribute__((ext_vector_type(2))) f32x2;
 typedef unsigned int __attribute__((ext_vector_type(4))) u32x4;
+typedef unsigned int __attribute__((ext_vector_type(2))) u32x2;
 
 #define LDS_AS __attribute__((address_space(3)))
 

@@ -425,8 +425,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 // -------------------------------------------------------------------------------------------
 constexpr int TBK = 64;
 
-template <int BM, int BN, bool WNT = false>
-__device__ __forceinline__ void tiled_stage(const bf16_t* __restrict__ A, int64_t lda, int M, const bf16_t* __restrict__ B,
+// F8: B (weights) is fp8-e4m3, one byte per element: its LDS image is [BN][64 B] with the 16-B chunk
+// q of row r stored at q ^ ((r >> 2) & 3) (ds_read_b64 fragment reads conflict-free, bank-simulated).
+template <int BN, bool F8>
+struct TiledB {
+  static constexpr int ROWB = F8 ? 64 : 128;  // LDS bytes per B row per 64-k stage
+  static constexpr int BYTES = BN * ROWB;
+  static constexpr int LOADS = F8 ? BN / 64 : BN / 32;  // glds per wave per stage
+};
+
+template <int BM, int BN, bool WNT = false, bool F8 = false>
+__device__ __forceinline__ void tiled_stage(const bf16_t* __restrict__ A, int64_t lda, int M, const void* __restrict__ Bv,
                                             int64_t ldb, int N, int K, int m0, int n0, int k0, char* sA, char* sB,
                                             int w, int lane) {
   // one wave-instruction = 1 KiB = 8 rows x 128 B; A needs BM/8 of them, B BN/8 (4 waves share)
@@ -439,19 +448,33 @@ __device__ __forceinline__ void tiled_stage(const bf16_t* __restrict__ A, int64_
     const bf16_t* ga = A + (int64_t)min(m0 + row, M - 1) * lda + kc;
     __builtin_amdgcn_global_load_lds((const void*)ga, (LDS_AS void*)(sA + inst * 1024), 16, 0, 0);
   }
+  if constexpr (F8) {
+    const unsigned char* B = reinterpret_cast<const unsigned char*>(Bv);
 #pragma unroll
-  for (int it = 0; it < BN / 32; ++it) {
-    const int inst = it * 4 + w;
-    const int row = inst * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ (row & 7);
-    const int kc = min(k0 + c * 8, K - 8);
-    const bf16_t* gb = B + (int64_t)min(n0 + row, N - 1) * ldb + kc;
-    // weights read once per step (single M tile): non-temporal (aux = 2), guide 'nt-weights'
-    __builtin_amdgcn_global_load_lds((const void*)gb, (LDS_AS void*)(sB + inst * 1024), 16, 0, WNT ? 2 : 0);
+    for (int it = 0; it < BN / 64; ++it) {  // one wave-instruction = 16 rows x 64 B
+      const int inst = it * 4 + w;
+      const int row = inst * 16 + (lane >> 2);
+      const int gq = (lane & 3) ^ ((row >> 2) & 3);
+      const int kc = min(k0 + gq * 16, K - 16);
+      const unsigned char* gb = B + (int64_t)min(n0 + row, N - 1) * ldb + kc;
+      __builtin_amdgcn_global_load_lds((const void*)gb, (LDS_AS void*)(sB + inst * 1024), 16, 0, WNT ? 2 : 0);
+    }
+  } else {
+    const bf16_t* B = reinterpret_cast<const bf16_t*>(Bv);
+#pragma unroll
+    for (int it = 0; it < BN / 32; ++it) {
+      const int inst = it * 4 + w;
+      const int row = inst * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (row & 7);
+      const int kc = min(k0 + c * 8, K - 8);
+      const bf16_t* gb = B + (int64_t)min(n0 + row, N - 1) * ldb + kc;
+      // weights read once per step (single M tile): non-temporal (aux = 2), guide 'nt-weights'
+      __builtin_amdgcn_global_load_lds((const void*)gb, (LDS_AS void*)(sB + inst * 1024), 16, 0, WNT ? 2 : 0);
+    }
   }
 }
 
-template <int MTW, int NTW, bool MASK>
+template <int MTW, int NTW, bool MASK, bool F8 = false>
 __device__ __forceinline__ void tiled_compute(const char* sA, const char* sB, f32x4 (&acc)[MTW][NTW], int wr, int wc,
                                               int li, int g, int k0, int K) {
 #pragma unroll
@@ -469,7 +492,13 @@ __device__ __forceinline__ void tiled_compute(const char* sA, const char* sB, f3
 #pragma unroll
     for (int t = 0; t < NTW; ++t) {
       const int rb = wc * (NTW * 16) + t * 16 + li;
-      b[t] = *reinterpret_cast<const s16x8*>(sB + rb * 128 + ((c ^ (rb & 7)) << 4));
+      if constexpr (F8) {  // k bytes [32 s + 8 g, +8) = half (g & 1) of 16-B chunk 2 s + g / 2
+        const int pq = (2 * s + (g >> 1)) ^ ((rb >> 2) & 3);
+        const u32x2 raw = *reinterpret_cast<const u32x2*>(sB + rb * 64 + pq * 16 + (g & 1) * 8);
+        b[t] = fp8x8_to_bf16(raw[0], raw[1]);
+      } else {
+        b[t] = *reinterpret_cast<const s16x8*>(sB + rb * 128 + ((c ^ (rb & 7)) << 4));
+      }
       if (MASK && !valid) b[t] = z;
     }
 #pragma unroll
@@ -506,14 +535,14 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int BM, int BN, int NS, bool WNT>
+template <int BM, int BN, int NS, bool WNT, bool F8 = false>
 __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restrict__ A, int64_t lda,
-                                                         const bf16_t* __restrict__ B, int64_t ldb,
+                                                         const void* __restrict__ B, int64_t ldb,
                                                          const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
                                                          int64_t ldy, float* __restrict__ part, int M, int N, int K,
-                                                         int act, int glu) {
+                                                         int act, int glu, const float* __restrict__ wscale) {
   constexpr int MTW = BM / 32, NTW = BN / 32;  // 16x16 tiles per wave
-  constexpr int A_BYTES = BM * TBK * 2, B_BYTES = BN * TBK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_BYTES = BM * TBK * 2, B_BYTES = TiledB<BN, F8>::BYTES, STAGE = A_BYTES + B_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -535,7 +564,7 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
   const int t0 = blockIdx.y * per, t1 = min(nk_all, t0 + per);
   if constexpr (NS == 2) {
     if (t0 < t1) {
-      tiled_stage<BM, BN, WNT>(A, lda, M, B, ldb, N, K, m0, n0, t0 * TBK, smem, smem + A_BYTES, w, lane);
+      tiled_stage<BM, BN, WNT, F8>(A, lda, M, B, ldb, N, K, m0, n0, t0 * TBK, smem, smem + A_BYTES, w, lane);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
@@ -543,20 +572,20 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
       const int cur = (t - t0) & 1;
       char* nA = smem + (cur ^ 1) * STAGE;
       char* cA = smem + cur * STAGE;
-      if (t + 1 < t1) tiled_stage<BM, BN, WNT>(A, lda, M, B, ldb, N, K, m0, n0, (t + 1) * TBK, nA, nA + A_BYTES, w, lane);
-      if (t + 1 == nk_all && (K % TBK)) tiled_compute<MTW, NTW, true>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
-      else tiled_compute<MTW, NTW, false>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
+      if (t + 1 < t1) tiled_stage<BM, BN, WNT, F8>(A, lda, M, B, ldb, N, K, m0, n0, (t + 1) * TBK, nA, nA + A_BYTES, w, lane);
+      if (t + 1 == nk_all && (K % TBK)) tiled_compute<MTW, NTW, true, F8>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
+      else tiled_compute<MTW, NTW, false, F8>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
   } else {
     // NS-stage ring: stage t+NS-1 is issued while stage t is computed; the wait before compute
     // only covers stage t (the younger stages' LOADS instructions each stay in flight): no drain.
-    constexpr int LOADS = BM / 32 + BN / 32;  // global_load_lds per wave per stage
+    constexpr int LOADS = BM / 32 + TiledB<BN, F8>::LOADS;  // global_load_lds per wave per stage
 #pragma unroll
     for (int j = 0; j < NS - 1; ++j)
       if (t0 + j < t1)
-        tiled_stage<BM, BN, WNT>(A, lda, M, B, ldb, N, K, m0, n0, (t0 + j) * TBK, smem + j * STAGE,
+        tiled_stage<BM, BN, WNT, F8>(A, lda, M, B, ldb, N, K, m0, n0, (t0 + j) * TBK, smem + j * STAGE,
                             smem + j * STAGE + A_BYTES, w, lane);
     int cur = 0;
     for (int t = t0; t < t1; ++t) {
@@ -566,10 +595,10 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
       const int nxt = cur == 0 ? NS - 1 : cur - 1;  // (cur + NS - 1) % NS
       if (t + NS - 1 < t1) {
         char* nA = smem + nxt * STAGE;
-        tiled_stage<BM, BN, WNT>(A, lda, M, B, ldb, N, K, m0, n0, (t + NS - 1) * TBK, nA, nA + A_BYTES, w, lane);
+        tiled_stage<BM, BN, WNT, F8>(A, lda, M, B, ldb, N, K, m0, n0, (t + NS - 1) * TBK, nA, nA + A_BYTES, w, lane);
       }
-      if (t + 1 == nk_all && (K % TBK)) tiled_compute<MTW, NTW, true>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
-      else tiled_compute<MTW, NTW, false>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
+      if (t + 1 == nk_all && (K % TBK)) tiled_compute<MTW, NTW, true, F8>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
+      else tiled_compute<MTW, NTW, false, F8>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
       cur = cur == NS - 1 ? 0 : cur + 1;
     }
   }
@@ -586,7 +615,7 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
           const int n = wn0 + nt * 16 + li;
-          if (n < N) pr[n] = acc[mt][nt][i];
+          if (n < N) pr[n] = F8 ? acc[mt][nt][i] * wscale[n] : acc[mt][nt][i];
         }
       } else if (glu) {
 #pragma unroll
@@ -594,6 +623,7 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
           const int ng = wn0 + 2 * p * 16 + li, nu = ng + 16;
           if (nu < N) {
             float gv = acc[mt][2 * p][i], uv = acc[mt][2 * p + 1][i];
+            if constexpr (F8) { gv *= wscale[ng]; uv *= wscale[nu]; }
             if (bias) { gv += bf2f(bias[ng]); uv += bf2f(bias[nu]); }
             Y[(int64_t)m * ldy + wn0 / 2 + p * 16 + li] = f2bf(silu(gv) * uv);
           }
@@ -604,6 +634,7 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
           const int n = wn0 + nt * 16 + li;
           if (n < N) {
             float v = acc[mt][nt][i];
+            if constexpr (F8) v *= wscale[n];
             if (bias) v += bf2f(bias[n]);
             Y[(int64_t)m * ldy + n] = f2bf(apply_act(v, act));
           }
@@ -999,9 +1030,9 @@ int gemm_skinny_splitk(int M, int N, int K) {
   return s;
 }
 
-int launch_tiled(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, const bf16_t* B, bf16_t* Y, int64_t ldy,
+int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const bf16_t* B, bf16_t* Y, int64_t ldy,
                  int M, int N, int K, int act, int g, int tsel, int split_hint, void* workspace, int64_t ws_bytes,
-                 bool partial_out, hipStream_t st);
+                 bool partial_out, hipStream_t st, const float* wscale = nullptr);
 
 // Returns the number of fp32 partial slabs [S, M, N] left in `workspace` (partial_out and the
 // planner chose split-K: the consumer - add_norm - reduces them and adds `bias`), or 0 when Y
@@ -1046,7 +1077,10 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_f
   auto Y = (bf16_t*)y;
   auto WS = (const float*)w_scale;
   const int g = glu ? 1 : 0;
-  const bool stream = w_fp8 || (M <= 16 && (nt_hint >> 8) == 0) || (nt_hint & 0xff);
+  // weight-streaming kernel: M <= 16, explicit stream hints, and fp8 prefill panels; fp8 decode
+  // (16 < M <= 128) runs the tiled kernel with fp8 weight tiles (W8A16)
+  const int tiled_hint = nt_hint >> 8;
+  const bool stream = (nt_hint & 0xff) || (!tiled_hint && (M <= 16 || (w_fp8 && M > 128)));
   if (stream) {
     if (M > 128) {  // fp8 weights with many rows (prefill): 128-row panels through the streaming kernel
       for (int m0 = 0; m0 < M; m0 += 128) {
@@ -1079,8 +1113,8 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_f
     }
     return 0;
   }
-  return launch_tiled(X, ldx, (const bf16_t*)w, ldw, B, Y, ldy, M, N, K, act, g, nt_hint >> 8, split_hint, workspace,
-                      ws_bytes, partial_out, st);
+  return launch_tiled(X, ldx, w, ldw, B, Y, ldy, M, N, K, act, g, nt_hint >> 8, split_hint, workspace,
+                      ws_bytes, partial_out, st, w_fp8 ? WS : nullptr);
 }
 
 // Tiled-path plan. Tile: 64 rows for M <= 64 (64x64, or 64x128 when 64x64 gives > 256 tiles),
@@ -1201,9 +1235,9 @@ static bool launch_streamk(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_
   return true;
 }
 
-int launch_tiled(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, const bf16_t* B, bf16_t* Y, int64_t ldy,
+int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const bf16_t* B, bf16_t* Y, int64_t ldy,
                  int M, int N, int K, int act, int g, int tsel, int split_hint, void* workspace, int64_t ws_bytes,
-                 bool partial_out, hipStream_t st) {
+                 bool partial_out, hipStream_t st, const float* wscale) {
   const int tsel_raw = tsel;
   int s = split_hint;
   gemm_tiled_plan(M, N, K, &tsel, &s, g != 0);
@@ -1212,13 +1246,16 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, con
   tsel &= 15;
   if (tsel == 1 && ns > 3) ns = 3;  // 128x128 x 4 stages would exceed the 160 KiB LDS
   if (tsel == 2 && ns > 4) ns = 4;
+  const bool f8 = wscale != nullptr;  // fp8-e4m3 weights (W8A16): half the weight bytes of a decode step
+  if (f8 && tsel == 4) tsel = 1;
   if (tsel == 4) {
-    gemm_big_kernel<<<tiles_of(M, N, 256, 256), 512, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, M, N, K, act, g);
+    gemm_big_kernel<<<tiles_of(M, N, 256, 256), 512, 0, st>>>(X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, M, N, K, act,
+                                                              g);
     HIP_CHECK_LAUNCH();
     return 0;
   }
-  if (tsel_raw & 128) {
-    if (launch_streamk(X, ldx, W, ldw, B, Y, ldy, M, N, K, act, g, tsel, ns, s, workspace, ws_bytes,
+  if ((tsel_raw & 128) && !f8) {
+    if (launch_streamk(X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, M, N, K, act, g, tsel, ns, s, workspace, ws_bytes,
                        wnt_ok(tsel_raw, M, tsel), st))
       return 0;
     s = 1;  // workspace too small for the partial tiles: plain tiled launch
@@ -1232,14 +1269,16 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, con
   dim3 grid(nt, s);
   // non-temporal weight staging when every weight tile is read by exactly one workgroup row
   const bool wnt = wnt_ok(tsel_raw, M, tsel);
+#define LT1(BM_, BN_, NS_, WNT_, F8_)                                                                              \
+  gemm_tiled_kernel<BM_, BN_, NS_, WNT_, F8_><<<grid, 256, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N, K, act_k,  \
+                                                                    glu_k, wscale)
 #define LT(BM_, BN_, NS_)                                                                                          \
   do {                                                                                                             \
-    if (wnt)                                                                                                       \
-      gemm_tiled_kernel<BM_, BN_, NS_, true><<<grid, 256, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N, K, act_k, \
-                                                                    glu_k);                                         \
-    else                                                                                                           \
-      gemm_tiled_kernel<BM_, BN_, NS_, false><<<grid, 256, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N, K, act_k, \
-                                                                     glu_k);                                        \
+    if (f8) {                                                                                                      \
+      if (wnt) LT1(BM_, BN_, NS_, true, true); else LT1(BM_, BN_, NS_, false, true);                              \
+    } else {                                                                                                       \
+      if (wnt) LT1(BM_, BN_, NS_, true, false); else LT1(BM_, BN_, NS_, false, false);                            \
+    }                                                                                                              \
   } while (0)
   if (ns == 3) {
     if (tsel == 1) LT(128, 128, 3); else if (tsel == 2) LT(64, 128, 3); else LT(64, 64, 3);
@@ -1251,6 +1290,7 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, con
     if (tsel == 1) LT(128, 128, 2); else if (tsel == 2) LT(64, 128, 2); else LT(64, 64, 2);
   }
 #undef LT
+#undef LT1
   HIP_CHECK_LAUNCH();
   if (s > 1 && partial_out && !g && act == 0) return s;
   if (s > 1) {
@@ -1272,7 +1312,7 @@ void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk) {
     }
     return;
   }
-  if (w_fp8 || M <= 16) {
+  if (M <= 16 || (w_fp8 && M > 128)) {
     gemm_stream_plan(std::min(M, 128), N, K, nt, splitk);
   } else {
     int tsel = 0, s = 0;

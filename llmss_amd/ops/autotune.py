@@ -44,7 +44,9 @@ def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, 
     splits = (1, 2, 4, 8)
     if fp8 or M <= 32:  # weight-streaming kernels: nt + 16 * variant
         out += [(nt + 16 * v, s) for v, nt, s in itertools.product((1, 2), (1, 2), splits)]
-    if fp8:
+    if fp8:  # tiled kernel with fp8 weight tiles (no stream-K / big-tile variants)
+        if M > 16:
+            out += [((t | d) << 8, s) for t, d in ((3, 16), (3, 32), (2, 16), (2, 32)) for s in splits]
         return out
     # tiled: tile << 8 | depth code << 12   (tile 1: 128x128, 2: 64x128, 3: 64x64; depth 2/3/4/6)
     tiles = [(3, (0, 16, 32, 48)), (2, (0, 16, 32))]

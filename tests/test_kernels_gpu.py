@@ -383,3 +383,18 @@ def test_gemm_streamk(tile, stages, per_cu, M, N, K):
               R.linear(x.float(), w.float(), b.float(), act="gelu_tanh"), 2e-2)
     close(H.linear(x, w, None, glu=True, nt_hint=hint, split_hint=per_cu),
           R.linear(x.float(), w.float(), None, glu=True), 2e-2)
+
+
+@pytest.mark.parametrize("tile,stages", [(3, 2), (3, 3), (3, 4), (2, 2), (2, 3), (1, 2)])
+@pytest.mark.parametrize("split", [1, 3])
+@pytest.mark.parametrize("M,N,K", [(64, 1024, 2048), (37, 544, 2064), (128, 4096, 1376)])
+def test_gemm_fp8_tiled(tile, stages, split, M, N, K):
+    """W8A16 tiled GEMM: fp8 weight tiles staged in LDS, expanded to bf16 fragments, scale in the epilogue."""
+    torch.manual_seed(0)
+    x, w, b = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
+    q, s = H.quant_fp8_rows(w)
+    hint = (tile | {2: 0, 3: 16, 4: 32}[stages]) << 8
+    close(H.linear(x, q, b, act="gelu_tanh", w_scale=s, nt_hint=hint, split_hint=split),
+          R.linear(x.float(), q, b.float(), act="gelu_tanh", w_scale=s), 2e-2)
+    close(H.linear(x, q, None, glu=True, w_scale=s, nt_hint=hint, split_hint=split),
+          R.linear(x.float(), q, None, glu=True, w_scale=s), 2e-2)
