@@ -1,0 +1,56 @@
+"""Decode-attention micro-benchmark: paged KV read bandwidth per configuration.
+
+usage: python bench/attn_bench.py [--B 64] [--ctx 192,1024] [--heads 32:32,32:8]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from llmss_amd.ops import hip as H  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=64)
+    ap.add_argument("--ctx", default="192,1024")
+    ap.add_argument("--heads", default="32:32,32:8")
+    ap.add_argument("--D", type=int, default=128)
+    a = ap.parse_args()
+    dev, bs, D = "cuda", 16, a.D
+    for hk in a.heads.split(","):
+        nh, nkv = map(int, hk.split(":"))
+        for ctx in map(int, a.ctx.split(",")):
+            maxb = (ctx + bs - 1) // bs
+            nb = a.B * maxb
+            kc = torch.randn(nb, nkv, bs, D, device=dev).to(torch.bfloat16)
+            vc = torch.randn_like(kc)
+            bt = torch.randperm(nb, device=dev).view(a.B, maxb).to(torch.int32)
+            cl = torch.full((a.B,), ctx, dtype=torch.int32, device=dev)
+            q = torch.randn(a.B, (nh + 2 * nkv) * D, device=dev).to(torch.bfloat16)
+            out = torch.empty(a.B, nh * D, device=dev, dtype=torch.bfloat16)
+            kv_bytes = 2 * a.B * ctx * nkv * D * 2
+            res = {"B": a.B, "nh": nh, "nkv": nkv, "ctx": ctx, "MB": round(kv_bytes / 1e6, 1)}
+            for u in (1, 2, 4):
+                H.lib().attn_decode_set_unroll(u)
+                f = lambda: H.attn_decode(q, kc, vc, bt, cl, nh, nkv, D, D ** -0.5, ctx, out=out)
+                for _ in range(5):
+                    f()
+                torch.cuda.synchronize()
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(50):
+                    f()
+                e.record()
+                torch.cuda.synchronize()
+                us = s.elapsed_time(e) * 1e3 / 50
+                res[f"u{u}_us"] = round(us, 2)
+                res[f"u{u}_TBps"] = round(kv_bytes / us / 1e6, 2)
+            H.lib().attn_decode_set_unroll(2)
+            print(res, flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -323,6 +323,9 @@ __global__ __launch_bounds__(256) void attn_decode_reduce_kernel(const float* __
   }
 }
 
+static int g_decode_unroll = 2;  // tokens in flight per (wave, slot); tuning knob (attn_decode_set_unroll)
+void attn_decode_set_unroll(int u) { g_decode_unroll = (u == 1 || u == 4) ? u : 2; }
+
 template <int D, int GB>
 static void launch_decode_t(const bf16_t* q, int64_t qs, bf16_t* kc, bf16_t* vc, const int* bt, int bts,
                             const int* cl, bf16_t* out, int64_t os, float* po, float* pml, int B, int nh, int nkv,
@@ -330,7 +333,14 @@ static void launch_decode_t(const bf16_t* q, int64_t qs, bf16_t* kc, bf16_t* vc,
   const int G = nh / nkv;
   const int ngroups = (G + GB - 1) / GB;
   dim3 grid(B, nkv * ngroups, nsplit);
-  if (fr)
+  if (!fr && g_decode_unroll != 2) {
+    if (g_decode_unroll == 1)
+      attn_decode_kernel<D, GB, 1, false><<<grid, 256, 0, st>>>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, nh, nkv, G,
+                                                                ngroups, bs, psize, scale * kLog2e, FusedRope{});
+    else
+      attn_decode_kernel<D, GB, 4, false><<<grid, 256, 0, st>>>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, nh, nkv, G,
+                                                                ngroups, bs, psize, scale * kLog2e, FusedRope{});
+  } else if (fr)
     attn_decode_kernel<D, GB, 2, true><<<grid, 256, 0, st>>>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, nh, nkv, G,
                                                              ngroups, bs, psize, scale * kLog2e, *fr);
   else

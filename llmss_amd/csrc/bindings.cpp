@@ -38,6 +38,9 @@ void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk);
 void gemm_tuned_set(int M, int N, int K, bool glu, bool fp8, int nt_hint, int split);
 void gemm_tuned_clear();
 void gemm_reserve_streamk(int n);
+int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int nt_hint, int split_hint,
+                       int64_t ws_bytes);
+void attn_decode_set_unroll(int u);
 bool gemm_tuned_get(int M, int N, int K, bool glu, bool fp8, int* nt_hint, int* split);
 void launch_add_norm_partial(const void* part, int S, int64_t slab, const void* xbias, const void* res_in,
                              void* res_out, const void* w, const void* b, void* y, int64_t y_stride, int T, int H,
@@ -101,6 +104,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_tuned_set", &gemm_tuned_set);
   m.def("gemm_tuned_clear", &gemm_tuned_clear);
   m.def("gemm_reserve_streamk", &gemm_reserve_streamk);
+  m.def("gemm_partial_slabs", &gemm_partial_slabs);
+  m.def("attn_decode_set_unroll", &attn_decode_set_unroll);
   m.def("gemm_tuned_get", [](int M, int N, int K, bool glu, bool fp8) -> py::object {
     int nt, s;
     if (!gemm_tuned_get(M, N, K, glu, fp8, &nt, &s)) return py::none();

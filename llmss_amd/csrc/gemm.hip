@@ -1034,6 +1034,11 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
                  int M, int N, int K, int act, int g, int tsel, int split_hint, void* workspace, int64_t ws_bytes,
                  bool partial_out, hipStream_t st, const float* wscale = nullptr);
 
+int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int nt_hint, int split_hint,
+                       int64_t ws_bytes);
+void gemm_tiled_plan(int M, int N, int K, int* tsel_io, int* split_io, bool glu);
+void gemm_stream_plan(int M, int N, int K, int* nt_out, int* splitk_out);
+
 // Returns the number of fp32 partial slabs [S, M, N] left in `workspace` (partial_out and the
 // planner chose split-K: the consumer - add_norm - reduces them and adds `bias`), or 0 when Y
 // holds the finished bf16 output.
@@ -1070,6 +1075,8 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_f
                 int64_t ws_bytes, int nt_hint, int split_hint, bool partial_out, hipStream_t st) {
   if (M == 0 || N == 0) return 0;
   if (nt_hint == 0 && split_hint == 0) gemm_tuned_get(M, N, K, glu, w_fp8, &nt_hint, &split_hint);
+  if (!y && (!partial_out || gemm_partial_slabs(M, N, K, w_fp8, glu, act, nt_hint, split_hint, ws_bytes) == 0))
+    throw std::runtime_error("gemm: this configuration writes the output, but no output buffer was given");
   if (K % 16) throw std::runtime_error("gemm: K must be a multiple of 16");
   if (glu && (N % 32)) throw std::runtime_error("gemm: glu needs N % 32 == 0");
   auto X = (const bf16_t*)x;
@@ -1300,6 +1307,33 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
     HIP_CHECK_LAUNCH();
   }
   return 0;
+}
+
+// Number of fp32 partial slabs launch_gemm(..., partial_out=true) leaves for these hints, or 0 if
+// that call writes the finished output (stream-K, fp8 prefill panels, act / glu epilogues, no
+// split). The Python wrapper allocates Y exactly when this returns 0 - one source of truth.
+int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int nt_hint, int split_hint,
+                       int64_t ws_bytes) {
+  if (M == 0 || N == 0 || glu || act != 0) return 0;
+  if (nt_hint == 0 && split_hint == 0) gemm_tuned_get(M, N, K, glu, w_fp8, &nt_hint, &split_hint);
+  const int tiled_hint = nt_hint >> 8;
+  const bool stream = (nt_hint & 0xff) || (!tiled_hint && (M <= 16 || (w_fp8 && M > 128)));
+  int s;
+  if (stream) {
+    if (M > 128) return 0;  // 128-row panels, each finished in place
+    int nt;
+    gemm_stream_plan(M, N, K, &nt, &s);
+    if (split_hint > 0) s = split_hint;
+  } else {
+    int tsel = tiled_hint;
+    if ((tsel & 128) && !w_fp8) return 0;  // stream-K combines in-kernel
+    if (w_fp8 && (tsel & 15) == 4) tsel = (tsel & ~15) | 1;
+    s = split_hint;
+    gemm_tiled_plan(M, N, K, &tsel, &s, false);
+    if ((tsel & 15) == 4 || (tsel & 128)) return 0;
+  }
+  if ((int64_t)s * M * N * 4 > ws_bytes) s = 1;
+  return s > 1 ? s : 0;
 }
 
 void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk) {

@@ -167,9 +167,12 @@ _DECODE_WS = DecodeWorkspace()
 
 
 def decode_splits(B: int, nkv: int, max_ctx: int, block_size: int) -> tuple:
-    """(num_splits, partition_size): enough workgroups for 256 CUs, partitions >= 256 tokens."""
+    """(num_splits, partition_size): ~8 workgroups per CU (2048), partitions >= 256 tokens.
+
+    Measured (bench/attn_bench.py): with few (sequence, kv-head) pairs - GQA / TP-sharded kv heads -
+    each workgroup otherwise walks the whole context serially and the KV stream drops to 2-3 TB/s."""
     wgs = max(1, B * nkv)
-    want = max(1, math.ceil(512 / wgs))
+    want = max(1, math.ceil(2048 / wgs))
     nsplit = max(1, min(want, math.ceil(max_ctx / 256)))
     psize = math.ceil(max_ctx / nsplit)
     psize = math.ceil(psize / block_size) * block_size
@@ -351,12 +354,9 @@ def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hi
     ws = _GEMM_WS.get(64 << 20, x.device)
     partial_ok = partial_ok and not glu and act in ("none", None) and out is None
     y = out if out is not None else (None if partial_ok else torch.empty(M, nout, dtype=x.dtype, device=x.device))
-    if partial_ok:
-        nt, s = lib().gemm_plan(M, N, K, fp8)
-        if split_hint:
-            s = split_hint
-        if s <= 1 or s * M * N * 4 > ws.numel() * 4:
-            y = torch.empty(M, nout, dtype=x.dtype, device=x.device)
+    if partial_ok and lib().gemm_partial_slabs(M, N, K, fp8, False, 0, int(nt_hint), int(split_hint),
+                                               ws.numel() * 4) == 0:
+        y = torch.empty(M, nout, dtype=x.dtype, device=x.device)  # this call finishes its output itself
     if y is not None:
         _bf16_rows(y, "out", nout)
     S = lib().gemm(x.data_ptr(), x.stride(0), w.data_ptr(), K, fp8, _ptr(w_scale), _ptr(bias), _ptr(y),

@@ -398,3 +398,22 @@ def test_gemm_fp8_tiled(tile, stages, split, M, N, K):
           R.linear(x.float(), q, b.float(), act="gelu_tanh", w_scale=s), 2e-2)
     close(H.linear(x, q, None, glu=True, w_scale=s, nt_hint=hint, split_hint=split),
           R.linear(x.float(), q, None, glu=True, w_scale=s), 2e-2)
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("M,hint,split", [(256, 0x21, 4), (512, 0x12, 2), (200, (1 | 16 | 128) << 8, 2),
+                                          (96, (3 | 128) << 8, 3), (64, 0x300, 4), (64, 0x1300, 1)])
+def test_partial_capable_calls_never_lose_output(fp8, M, hint, split):
+    """partial_ok=True must return split-K slabs only when the kernel leaves them (stream-K and fp8
+    prefill panels finish their output in place): regression for a null-output fault."""
+    torch.manual_seed(0)
+    N, K = 1280, 2048
+    x, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
+    sc = None
+    if fp8:
+        w, sc = H.quant_fp8_rows(w)
+    ref = R.linear(x.float(), w if fp8 else w.float(), None, w_scale=sc)
+    r = H.linear(x, w, None, w_scale=sc, nt_hint=hint, split_hint=split, partial_ok=True)
+    if isinstance(r, H.PartialSum):
+        r = r.buf[: r.S * M * N].view(r.S, M, N).sum(0)
+    close(r, ref, 2e-2)
