@@ -38,6 +38,9 @@ void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk);
 void gemm_tuned_set(int M, int N, int K, bool glu, bool fp8, int nt_hint, int split);
 void gemm_tuned_clear();
 void gemm_reserve_streamk(int n);
+int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq, int64_t ldw, const void* wsc,
+                     const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, int tile,
+                     int depth, int split, void* workspace, int64_t ws_bytes, hipStream_t st);
 int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int nt_hint, int split_hint,
                        int64_t ws_bytes);
 void attn_decode_set_unroll(int u);
@@ -104,6 +107,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_tuned_set", &gemm_tuned_set);
   m.def("gemm_tuned_clear", &gemm_tuned_clear);
   m.def("gemm_reserve_streamk", &gemm_reserve_streamk);
+  m.def("gemm_f8f8", [](uintptr_t xq, int64_t ldx, uintptr_t xs, uintptr_t wq, int64_t ldw, uintptr_t wsc,
+                        uintptr_t bias, uintptr_t y, int64_t ldy, int M, int N, int K, int act, bool glu, int tile,
+                        int depth, int split, uintptr_t work, int64_t wbytes, uintptr_t st) {
+    return launch_gemm_f8f8(CP(xq), ldx, CP(xs), CP(wq), ldw, CP(wsc), CP(bias), P(y), ldy, M, N, K, act, glu, tile,
+                            depth, split, P(work), wbytes, S(st));
+  });
   m.def("gemm_partial_slabs", &gemm_partial_slabs);
   m.def("attn_decode_set_unroll", &attn_decode_set_unroll);
   m.def("gemm_tuned_get", [](int M, int N, int K, bool glu, bool fp8) -> py::object {

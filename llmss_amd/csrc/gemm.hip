@@ -656,10 +656,28 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
 // "Pipelining across barriers", 3-buffer-equivalent depth in 2 buffers).
 // Requires K % 64 == 0; rows beyond M / N are clamped on load and masked on store.
 // -------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16_t* __restrict__ A, int64_t lda,
-                                                          const bf16_t* __restrict__ B, int64_t ldb,
+// one MX-fp8 16x16x128 MFMA from two 16-B fragment halves per operand (unit E8M0 block scales)
+__device__ __forceinline__ f32x4 mfma_f8x2(s16x8 a0, s16x8 a1, s16x8 b0, s16x8 b1, f32x4 c) {
+  typedef int __attribute__((ext_vector_type(4))) i32x4_t;
+  typedef int __attribute__((ext_vector_type(8))) i32x8_t;
+  const i32x4_t al = __builtin_bit_cast(i32x4_t, a0), ah = __builtin_bit_cast(i32x4_t, a1);
+  const i32x4_t bl = __builtin_bit_cast(i32x4_t, b0), bh = __builtin_bit_cast(i32x4_t, b1);
+  const i32x8_t av = __builtin_shufflevector(al, ah, 0, 1, 2, 3, 4, 5, 6, 7);
+  const i32x8_t bv = __builtin_shufflevector(bl, bh, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, c, 0, 0, 0, 127, 0, 127);
+}
+
+// F8: both operands fp8-e4m3 (W8A8): a 128-element fp8 K-tile has exactly the byte layout of the
+// 64-element bf16 one, so staging / LDS image / fragment addresses are shared; each (m, n) takes one
+// MX-fp8 16x16x128 MFMA per K-tile (the two 16-B chunks 2g, 2g+1 of the lane's row), and the
+// per-token x per-channel scales are applied in the epilogue.
+template <bool F8>
+__global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict__ A, int64_t lda,
+                                                          const void* __restrict__ B, int64_t ldb,
                                                           const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
-                                                          int64_t ldy, int M, int N, int K, int act, int glu) {
+                                                          int64_t ldy, int M, int N, int K, int act, int glu,
+                                                          const float* __restrict__ xs, const float* __restrict__ ws) {
+  constexpr int ES = F8 ? 1 : 2;  // operand bytes per element
   constexpr int HALF = 16384, BUF = 4 * HALF;
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
   const int lane = threadIdx.x & 63;
@@ -669,12 +687,12 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16_t* __restri
   const int ntn = (N + 255) / 256, ntm = (M + 255) / 256;
   const int tile = xcd_remap(blockIdx.x, ntn * ntm);
   const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
-  const int nk = K / 64;
+  const int nk = K * ES / 128;  // 128-byte K-tiles
 
   // staging: half h (0,1: A rows 128h.., 2,3: B rows 128(h-2)..), 2 x 1-KiB glds per wave; lane ->
   // row inst*8 + lane/8, LDS chunk lane&7 holding global chunk (lane&7) ^ (row&7) (swizzle on source)
-  const bf16_t* src[4] = {A, A, B, B};
-  const int64_t ld[4] = {lda, lda, ldb, ldb};
+  const char* src[4] = {(const char*)A, (const char*)A, (const char*)B, (const char*)B};
+  const int64_t ld[4] = {lda * ES, lda * ES, ldb * ES, ldb * ES};  // bytes
   int64_t soff[4][2];
   int lofs[2];
 #pragma unroll
@@ -688,7 +706,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16_t* __restri
       const bool isA = h < 2;
       const int lim = isA ? M : N;
       const int r = min((isA ? m0 : n0) + (h & 1) * 128 + row, lim - 1);
-      soff[h][i] = (int64_t)r * ld[h] + gc * 8;
+      soff[h][i] = (int64_t)r * ld[h] + gc * 16;
     }
   }
   auto stage = [&](int t, char* buf) {
@@ -696,7 +714,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16_t* __restri
     for (int h = 0; h < 4; ++h)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
-        __builtin_amdgcn_global_load_lds((const void*)(src[h] + soff[h][i] + t * 64),
+        __builtin_amdgcn_global_load_lds((const void*)(src[h] + soff[h][i] + (int64_t)t * 128),
                                          (LDS_AS void*)(buf + h * HALF + lofs[i]), 16, 0, 0);
   };
 
@@ -710,7 +728,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16_t* __restri
   int aoff[8][2], boff[4][2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const int c = 4 * s + g;
+    const int c = F8 ? 2 * g + s : 4 * s + g;  // bf16: k-half s; fp8: the lane's two 16-B chunks
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int r = m * 16 + li;
@@ -739,18 +757,32 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16_t* __restri
       for (int m = 0; m < 8; ++m) a[m][s] = *reinterpret_cast<const s16x8*>(cur + aoff[m][s]);
     }
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (F8) {  // first half: n-tiles 0, 1
 #pragma unroll
-    for (int m = 0; m < 8; ++m)
+      for (int m = 0; m < 8; ++m)
 #pragma unroll
-      for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][0], b[n][0], acc[m][n], 0, 0, 0);
+        for (int n = 0; n < 2; ++n) acc[m][n] = mfma_f8x2(a[m][0], a[m][1], b[n][0], b[n][1], acc[m][n]);
+    } else {
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][0], b[n][0], acc[m][n], 0, 0, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
     lds_barrier();  // every wave's reads of this buffer are complete -> restage it
     if (t + 2 < nk) stage(t + 2, cur);
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (F8) {  // second half: n-tiles 2, 3
 #pragma unroll
-    for (int m = 0; m < 8; ++m)
+      for (int m = 0; m < 8; ++m)
 #pragma unroll
-      for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][1], b[n][1], acc[m][n], 0, 0, 0);
+        for (int n = 2; n < 4; ++n) acc[m][n] = mfma_f8x2(a[m][0], a[m][1], b[n][0], b[n][1], acc[m][n]);
+    } else {
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][1], b[n][1], acc[m][n], 0, 0, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
   }
 
@@ -762,12 +794,14 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16_t* __restri
     for (int i = 0; i < 4; ++i) {
       const int row = m0 + wr * 128 + m * 16 + 4 * g + i;
       if (row >= M) continue;
+      const float sx = F8 ? xs[row] : 1.f;
       if (glu) {
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
           const int ng = wn0 + 2 * p * 16 + li, nu = ng + 16;
           if (nu < N) {
             float gv = acc[m][2 * p][i], uv = acc[m][2 * p + 1][i];
+            if constexpr (F8) { gv *= sx * ws[ng]; uv *= sx * ws[nu]; }
             if (bias) { gv += bf2f(bias[ng]); uv += bf2f(bias[nu]); }
             Y[(int64_t)row * ldy + wn0 / 2 + p * 16 + li] = f2bf(silu(gv) * uv);
           }
@@ -778,6 +812,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const bf16_t* __restri
           const int col = wn0 + n * 16 + li;
           if (col < N) {
             float v = acc[m][n][i];
+            if constexpr (F8) v *= sx * ws[col];
             if (bias) v += bf2f(bias[col]);
             Y[(int64_t)row * ldy + col] = f2bf(apply_act(v, act));
           }
@@ -955,6 +990,217 @@ __global__ __launch_bounds__(256) void gemm_streamk_kernel(const bf16_t* __restr
     ++t;
     kk = 0;
   }
+}
+
+// -------------------------------------------------------------------------------------------
+// W8A8 GEMM on the MX-fp8 matrix cores (BASELINE: Llama-2-70B TP=8 fp8, "CDNA4 fp8 MFMA").
+// Y = (Xq . Wq^T) * xs[m] * ws[n] (+ bias, act / SwiGLU): Xq = per-token fp8-e4m3 activations
+// (quant_fp8_rows on X), Wq = per-channel fp8-e4m3 weights. The 16x16x128 f8f6f4 MFMA with unit
+// block scales (E8M0 127) runs at the fp8 peak (2x bf16; the unscaled 16x16x32 fp8 form runs at
+// the bf16 rate). Tiles: BM x BN x 128 bytes staged by glds into the same XOR-swizzled 128-B-row
+// LDS image as the bf16 tiles; lane (r = l&15, g = l>>4) takes 32 bytes = k [32g, 32g+32) of its
+// row as 2 x ds_read_b128. Used where fp8 GEMMs are compute-bound (prefill, M > 128).
+// -------------------------------------------------------------------------------------------
+typedef int __attribute__((ext_vector_type(8))) i32x8;
+constexpr int TBK8 = 128;  // k (bytes) per stage
+
+template <int BM, int BN>
+__device__ __forceinline__ void f8_stage(const unsigned char* __restrict__ A, int64_t lda, int M,
+                                         const unsigned char* __restrict__ B, int64_t ldb, int N, int K, int m0, int n0,
+                                         int k0, char* sA, char* sB, int w, int lane) {
+#pragma unroll
+  for (int it = 0; it < BM / 32; ++it) {
+    const int inst = it * 4 + w;
+    const int row = inst * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (row & 7);
+    const int kc = min(k0 + c * 16, K - 16);
+    __builtin_amdgcn_global_load_lds((const void*)(A + (int64_t)min(m0 + row, M - 1) * lda + kc),
+                                     (LDS_AS void*)(sA + inst * 1024), 16, 0, 0);
+  }
+#pragma unroll
+  for (int it = 0; it < BN / 32; ++it) {
+    const int inst = it * 4 + w;
+    const int row = inst * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (row & 7);
+    const int kc = min(k0 + c * 16, K - 16);
+    __builtin_amdgcn_global_load_lds((const void*)(B + (int64_t)min(n0 + row, N - 1) * ldb + kc),
+                                     (LDS_AS void*)(sB + inst * 1024), 16, 0, 0);
+  }
+}
+
+template <int MTW, int NTW, bool MASK>
+__device__ __forceinline__ void f8_compute(const char* sA, const char* sB, f32x4 (&acc)[MTW][NTW], int wr, int wc,
+                                           int li, int g, int k0, int K) {
+  const bool v0 = !MASK || (k0 + 32 * g < K), v1 = !MASK || (k0 + 32 * g + 16 < K);
+  i32x8 a[MTW], b[NTW];
+#pragma unroll
+  for (int t = 0; t < MTW; ++t) {
+    const int r = wr * (MTW * 16) + t * 16 + li;
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(sA + r * 128 + (((2 * g) ^ (r & 7)) << 4));
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(sA + r * 128 + (((2 * g + 1) ^ (r & 7)) << 4));
+    a[t] = i32x8{(int)(v0 ? lo[0] : 0u), (int)(v0 ? lo[1] : 0u), (int)(v0 ? lo[2] : 0u), (int)(v0 ? lo[3] : 0u),
+                 (int)(v1 ? hi[0] : 0u), (int)(v1 ? hi[1] : 0u), (int)(v1 ? hi[2] : 0u), (int)(v1 ? hi[3] : 0u)};
+  }
+#pragma unroll
+  for (int t = 0; t < NTW; ++t) {
+    const int r = wc * (NTW * 16) + t * 16 + li;
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(sB + r * 128 + (((2 * g) ^ (r & 7)) << 4));
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(sB + r * 128 + (((2 * g + 1) ^ (r & 7)) << 4));
+    b[t] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  }
+#pragma unroll
+  for (int mt = 0; mt < MTW; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt)
+      acc[mt][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[mt], b[nt], acc[mt][nt], 0, 0, 0, 127, 0, 127);
+}
+
+template <int BM, int BN, int NS>
+__global__ __launch_bounds__(256) void gemm_f8f8_kernel(const unsigned char* __restrict__ A, int64_t lda,
+                                                        const float* __restrict__ xs,
+                                                        const unsigned char* __restrict__ B, int64_t ldb,
+                                                        const float* __restrict__ ws,
+                                                        const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
+                                                        int64_t ldy, float* __restrict__ part, int M, int N, int K,
+                                                        int act, int glu) {
+  constexpr int MTW = BM / 32, NTW = BN / 32;
+  constexpr int A_BYTES = BM * TBK8, B_BYTES = BN * TBK8, STAGE = A_BYTES + B_BYTES;
+  constexpr int LOADS = BM / 32 + BN / 32;
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  const int wr = w >> 1, wc = w & 1;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
+  const int tile = xcd_remap(blockIdx.x, ntn * ntm);
+  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+  f32x4 acc[MTW][NTW];
+#pragma unroll
+  for (int a = 0; a < MTW; ++a)
+#pragma unroll
+    for (int b = 0; b < NTW; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk_all = (K + TBK8 - 1) / TBK8;
+  const int per = (nk_all + gridDim.y - 1) / gridDim.y;
+  const int t0 = blockIdx.y * per, t1 = min(nk_all, t0 + per);
+#pragma unroll
+  for (int j = 0; j < NS - 1; ++j)
+    if (t0 + j < t1)
+      f8_stage<BM, BN>(A, lda, M, B, ldb, N, K, m0, n0, (t0 + j) * TBK8, smem + j * STAGE, smem + j * STAGE + A_BYTES,
+                       w, lane);
+  int cur = 0;
+  for (int t = t0; t < t1; ++t) {
+    wait_vmcnt_upto<LOADS, NS - 2>(t1 - 1 - t);
+    lds_barrier();
+    char* cA = smem + cur * STAGE;
+    if (t + NS - 1 < t1) {
+      char* nA = smem + (cur == 0 ? NS - 1 : cur - 1) * STAGE;
+      f8_stage<BM, BN>(A, lda, M, B, ldb, N, K, m0, n0, (t + NS - 1) * TBK8, nA, nA + A_BYTES, w, lane);
+    }
+    if (t + 1 == nk_all && (K % TBK8)) f8_compute<MTW, NTW, true>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK8, K);
+    else f8_compute<MTW, NTW, false>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK8, K);
+    cur = cur == NS - 1 ? 0 : cur + 1;
+  }
+  // epilogue: per-token x per-channel scales, then the usual bias / act / SwiGLU (or split-K slabs)
+  const int wn0 = n0 + wc * (NTW * 16);
+#pragma unroll
+  for (int mt = 0; mt < MTW; ++mt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wr * (MTW * 16) + mt * 16 + 4 * g + i;
+      if (m >= M) continue;
+      const float sx = xs[m];
+      if (part) {
+        float* pr = part + ((int64_t)blockIdx.y * M + m) * N;
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) {
+          const int n = wn0 + nt * 16 + li;
+          if (n < N) pr[n] = acc[mt][nt][i] * sx * ws[n];
+        }
+      } else if (glu) {
+#pragma unroll
+        for (int p = 0; p < NTW / 2; ++p) {
+          const int ng = wn0 + 2 * p * 16 + li, nu = ng + 16;
+          if (nu < N) {
+            float gv = acc[mt][2 * p][i] * sx * ws[ng], uv = acc[mt][2 * p + 1][i] * sx * ws[nu];
+            if (bias) { gv += bf2f(bias[ng]); uv += bf2f(bias[nu]); }
+            Y[(int64_t)m * ldy + wn0 / 2 + p * 16 + li] = f2bf(silu(gv) * uv);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) {
+          const int n = wn0 + nt * 16 + li;
+          if (n < N) {
+            float v = acc[mt][nt][i] * sx * ws[n];
+            if (bias) v += bf2f(bias[n]);
+            Y[(int64_t)m * ldy + n] = f2bf(apply_act(v, act));
+          }
+        }
+      }
+    }
+  }
+}
+
+// tile: 1 = 128x128, 2 = 64x128, 3 = 64x64; ring depth 2-4; split-K over grid.y
+int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq, int64_t ldw, const void* wsc,
+                     const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, int tile,
+                     int depth, int split, void* workspace, int64_t ws_bytes, hipStream_t st) {
+  if (M == 0 || N == 0) return 0;
+  if (K % 16) throw std::runtime_error("gemm_f8f8: K must be a multiple of 16");
+  if (glu && (N % 32)) throw std::runtime_error("gemm_f8f8: glu needs N % 32 == 0");
+  if (!y) throw std::runtime_error("gemm_f8f8: output required");
+  const int bm = tile == 1 ? 128 : 64, bn = tile == 3 ? 64 : 128;
+  const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  const int nk = (K + TBK8 - 1) / TBK8;
+  if (tile == 4 || (tile == 0 && K % 128 == 0 && ((M + 255) / 256) * ((N + 255) / 256) >= 192)) {
+    if (K % 128) throw std::runtime_error("gemm_f8f8: the 256x256 tile needs K % 128 == 0");
+    gemm_big_kernel<true><<<((M + 255) / 256) * ((N + 255) / 256), 512, 0, st>>>(
+        xq, ldx, wq, ldw, (const bf16_t*)bias, (bf16_t*)y, ldy, M, N, K, act, glu ? 1 : 0, (const float*)xs,
+        (const float*)wsc);
+    HIP_CHECK_LAUNCH();
+    return 0;
+  }
+  if (tile == 0) {  // auto: 128x128 when it fills the chip, else 64x128 / 64x64, split to >= ~256 WGs
+    tile = ((M + 127) / 128) * ((N + 127) / 128) >= 240 ? 1 : (((M + 63) / 64) * ((N + 127) / 128) >= 240 ? 2 : 3);
+    return launch_gemm_f8f8(xq, ldx, xs, wq, ldw, wsc, bias, y, ldy, M, N, K, act, glu, tile, depth, split, workspace,
+                            ws_bytes, st);
+  }
+  if (split <= 0) {
+    split = 1;
+    while (tiles * split * 2 <= 512 && nk / (2 * split) >= 4 && split < 8) split *= 2;
+  }
+  split = std::max(1, std::min(split, nk));
+  if ((int64_t)split * M * N * 4 > ws_bytes) split = 1;
+  float* part = split > 1 ? (float*)workspace : nullptr;
+  const int act_k = split > 1 ? 0 : act, g = glu ? 1 : 0, glu_k = split > 1 ? 0 : g;
+  if (depth <= 0) depth = tile == 1 ? 3 : 4;
+  if (tile == 1 && depth > 3) depth = 3;
+  dim3 grid(tiles, split);
+  auto A = (const unsigned char*)xq;
+  auto Bw = (const unsigned char*)wq;
+  auto XS = (const float*)xs;
+  auto WSc = (const float*)wsc;
+  auto Bi = (const bf16_t*)bias;
+  auto Y = (bf16_t*)y;
+#define LF(BM_, BN_, NS_) \
+  gemm_f8f8_kernel<BM_, BN_, NS_><<<grid, 256, 0, st>>>(A, ldx, XS, Bw, ldw, WSc, Bi, Y, ldy, part, M, N, K, act_k, glu_k)
+  if (tile == 1) {
+    if (depth >= 3) LF(128, 128, 3); else LF(128, 128, 2);
+  } else if (tile == 2) {
+    if (depth >= 4) LF(64, 128, 4); else if (depth == 3) LF(64, 128, 3); else LF(64, 128, 2);
+  } else {
+    if (depth >= 4) LF(64, 64, 4); else if (depth == 3) LF(64, 64, 3); else LF(64, 64, 2);
+  }
+#undef LF
+  HIP_CHECK_LAUNCH();
+  if (split > 1) {
+    const int nout = glu ? N / 2 : N;
+    dim3 rgrid(std::min((nout + 255) / 256, 64), M);
+    splitk_reduce_kernel<<<rgrid, 256, 0, st>>>(part, split, M, N, Bi, Y, ldy, act, g);
+    HIP_CHECK_LAUNCH();
+  }
+  return 0;
 }
 
 // -------------------------------------------------------------------------------------------
@@ -1256,8 +1502,8 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   const bool f8 = wscale != nullptr;  // fp8-e4m3 weights (W8A16): half the weight bytes of a decode step
   if (f8 && tsel == 4) tsel = 1;
   if (tsel == 4) {
-    gemm_big_kernel<<<tiles_of(M, N, 256, 256), 512, 0, st>>>(X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, M, N, K, act,
-                                                              g);
+    gemm_big_kernel<false><<<tiles_of(M, N, 256, 256), 512, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, M, N, K, act, g,
+                                                                     nullptr, nullptr);
     HIP_CHECK_LAUNCH();
     return 0;
   }

@@ -8,6 +8,7 @@ them capturable into HIP graphs together with RCCL collectives.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -319,6 +320,30 @@ class _DequantScratch:
 _DEQ = _DequantScratch()
 
 
+_W8A8 = os.environ.get("LLMSS_FP8_W8A8", "1") != "0"
+
+
+def linear_w8a8(x, wq, w_scale, bias=None, act="none", glu=False, out=None, tile=0, depth=0, split=0):
+    """Y = (fp8(x) . wq^T) * x_scale[m] * w_scale[n] on the MX-fp8 MFMA (2x the bf16 matrix rate)."""
+    M, K = x.shape
+    N = wq.shape[0]
+    _check(wq.dtype == torch.uint8 and wq.is_contiguous() and K % 16 == 0 and wq.shape[1] == K, "fp8 weight")
+    _check(w_scale.dtype == torch.float32 and w_scale.numel() == N, "w_scale [N] fp32")
+    if glu:
+        _check(N % 32 == 0, "glu needs N % 32 == 0")
+    if bias is not None:
+        _check(bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.numel() == N, "bias [N] bf16")
+    xq, xs = quant_fp8_rows(x.contiguous())
+    nout = N // 2 if glu else N
+    y = out if out is not None else torch.empty(M, nout, dtype=torch.bfloat16, device=x.device)
+    _bf16_rows(y, "out", nout)
+    ws = _GEMM_WS.get(64 << 20, x.device)
+    lib().gemm_f8f8(xq.data_ptr(), K, xs.data_ptr(), wq.data_ptr(), K, w_scale.data_ptr(), _ptr(bias), y.data_ptr(),
+                    y.stride(0), M, N, K, _ACT[act], bool(glu), int(tile), int(depth), int(split), ws.data_ptr(),
+                    ws.numel() * 4, _stream())
+    return y
+
+
 def dequant_fp8_rows(q, scale, out=None):
     N, K = q.shape
     _check(q.dtype == torch.uint8 and q.is_contiguous() and K % 8 == 0, "fp8 weight [N, K] uint8, K % 8 == 0")
@@ -336,7 +361,10 @@ def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hi
     if fp8:
         _check(w.dtype == torch.uint8 and w.is_contiguous() and w.is_cuda, "fp8 weight stored as uint8 [N, K]")
         _check(w_scale.dtype == torch.float32 and w_scale.numel() == w.shape[0], "w_scale [N] fp32")
-        if M > _FP8_PREFILL_M and not nt_hint and not torch.cuda.is_current_stream_capturing():
+        tuned = lib().gemm_tuned_get(M, w.shape[0], K, bool(glu), True) if not nt_hint else None
+        if M > _FP8_PREFILL_M and not nt_hint and tuned is None and not torch.cuda.is_current_stream_capturing():
+            if _W8A8:  # compute-bound: per-token fp8 activations on the MX-fp8 matrix cores
+                return linear_w8a8(x, w, w_scale, bias, act, glu, out)
             wd = _DEQ.get(w.numel(), x.device)[: w.numel()].view(w.shape)
             dequant_fp8_rows(w, w_scale, out=wd)
             return linear(x, wd, bias, act, glu, None, out, 0, split_hint, partial_ok)

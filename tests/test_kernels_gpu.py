@@ -173,8 +173,9 @@ def test_gemm_fp8(M):
     assert ((a - b).abs() <= 0.125 * b.abs() + 2 ** -9).all()  # at most one e4m3 ulp of rounding difference
     ref = R.linear(x.float(), q, None, w_scale=s)
     close(H.linear(x, q, None, w_scale=s), ref, 2e-2)
-    xb = rnd(300, K)  # prefill size: fp8 weights expanded to bf16, big-tile path
-    close(H.linear(xb, q, None, w_scale=s), R.linear(xb.float(), q, None, w_scale=s), 3e-2)
+    xb = rnd(300, K)  # prefill size: W8A8 on the MX-fp8 MFMA (per-token fp8 activations)
+    xq, xs = H.quant_fp8_rows(xb)
+    close(H.linear(xb, q, None, w_scale=s), R.linear(R.dequant_fp8(xq, xs), q, None, w_scale=s), 3e-2)
     wd = H.dequant_fp8_rows(q, s)
     close(wd, R.dequant_fp8(q, s), 1e-6, rtol=1e-2)
 
@@ -417,3 +418,24 @@ def test_partial_capable_calls_never_lose_output(fp8, M, hint, split):
     if isinstance(r, H.PartialSum):
         r = r.buf[: r.S * M * N].view(r.S, M, N).sum(0)
     close(r, ref, 2e-2)
+
+
+@pytest.mark.parametrize("tile,depth", [(1, 3), (1, 2), (2, 4), (2, 3), (3, 4), (3, 2), (4, 0)])
+@pytest.mark.parametrize("split", [1, 3])
+@pytest.mark.parametrize("M,N,K", [(256, 1280, 2048), (300, 544, 2064), (129, 4096, 1376), (700, 800, 1024)])
+def test_gemm_w8a8_mx_fp8(tile, depth, split, M, N, K):
+    """W8A8 on the MX-fp8 MFMA: exact vs fp32 math on the same fp8 operands (per-token x, per-row w)."""
+    if tile == 4 and (K % 128 or split > 1):
+        pytest.skip("the 256x256 fp8 tile needs K % 128 == 0 and has no split-K")
+    torch.manual_seed(0)
+    x, w, b = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
+    q, s = H.quant_fp8_rows(w)
+    xq, xs = H.quant_fp8_rows(x)
+    xd = R.dequant_fp8(xq, xs)  # the activations the kernel actually multiplies
+    y = H.linear_w8a8(x, q, s, b, act="gelu_tanh", tile=tile, depth=depth, split=split)
+    close(y, R.linear(xd, q, b.float(), act="gelu_tanh", w_scale=s), 2e-2)
+    yg = H.linear_w8a8(x, q, s, None, glu=True, tile=tile, depth=depth, split=split)
+    close(yg, R.linear(xd, q, None, glu=True, w_scale=s), 2e-2)
+    # and close to the bf16-activation result: per-token fp8 activation error only (~3% relative RMS)
+    ya, yr = H.linear(x, q, b, w_scale=s).float(), R.linear(x.float(), q, b.float(), w_scale=s)
+    assert ((ya - yr).norm() / yr.norm()).item() < 0.05
