@@ -8,16 +8,20 @@
 //   rows [16p, 16p+16), group 2p+1 = up rows [16p, 16p+16); the kernel writes
 //   Y[:, 16p + i] = silu(gate) * up, so the [M, 2F] intermediate never reaches HBM.
 //
-// Two kernels, one choice per call (M is the only selector):
-//  * gemm_skinny (M <= 64: decode / small batches). Weight-streaming: every weight byte is read
-//    once, straight into VGPRs (no LDS round trip - guide §5 'GEMV / M <= 16' row), 32 B per
-//    lane = full 128-B lines per 4 lanes; X fragments come from L2. A workgroup = 4 waves that
-//    split K and reduce through LDS; more K splitting across workgroups (fp32 partial slabs +
-//    splitk_reduce, which also applies the epilogue) only when N alone cannot fill 256 CUs.
-//  * gemm_tiled (M > 64: prefill). 128x128x64 tile, 4 waves (2x2, 64x64 each, 16 mfma 16x16x32
-//    accumulators), both operands staged global->LDS with 16-B global_load_lds into an
-//    XOR-swizzled image (chunk ^= row & 7: conflict-free ds_read_b128, checked with a bank
-//    simulator), double-buffered, XCD-aware tile order (guide T1).
+// Kernel family (launch_gemm picks one per call; explicit hints and the autotuned plan table,
+// ops/autotune.py, override the static planner):
+//  * gemm_stream / gemm_stream2 (M <= 16, fp8 decode candidates): weight streaming straight into
+//    VGPRs (non-temporal), X staged once per chunk in LDS, 3-deep register ring, split-K slabs.
+//  * gemm_tiled<BM, BN, NS, WNT, F8> (decode / mid M): 64x64, 64x128 or 128x128 tiles, 4 waves,
+//    both operands by global_load_lds into XOR-swizzled 128-B-row LDS images, an NS-stage ring
+//    (2-6) waited with counted vmcnt across raw barriers, split-K over grid.y with fp32 slabs that
+//    the NEXT kernel sums (add_norm, rope) or splitk_reduce; F8 = fp8 weight tiles (W8A16).
+//  * gemm_streamk: persistent stream-K variant of the tiled kernel (in-kernel last-arriver combine).
+//  * gemm_big<F8> (prefill, M >= ~1K): 256x256 tile, 8 waves, 128 KiB double buffer whose K-tile
+//    t+2 is restaged while t is still being multiplied; F8 = W8A8 on the MX-fp8 matrix cores.
+//  * gemm_f8f8: tiled W8A8 for fp8 shapes too small for the 256x256 tile.
+// Split-K partial slabs never leave a call unless gemm_partial_slabs() says so (one source of
+// truth shared with the Python wrapper).
 #include "common.h"
 
 #include <mutex>
