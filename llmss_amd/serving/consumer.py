@@ -38,7 +38,8 @@ class Consumer:
         m = h.metrics or {}
         resp = {"prompt": req.prompt, "continuation": self.tok.decode(h.output_ids)}
         if req.request_id:
-            resp.update(request_id=req.request_id, output_tokens=len(h.output_ids), finish_reason=h.finish_reason,
+            resp.update(request_id=req.request_id, output_tokens=len(h.output_ids), token_ids=list(h.output_ids),
+                        finish_reason=h.finish_reason,
                         ttft_s=m.get("ttft_s"), e2e_s=m.get("e2e_s"))
         self.broker.lpush(reply_key(req.request_id), dump_response(resp))
         self.served += 1

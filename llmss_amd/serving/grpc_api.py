@@ -192,7 +192,7 @@ class BrokerServicer:
             ctx.abort(grpc.StatusCode.DEADLINE_EXCEEDED, "no reply from consumer")
         d = json.loads(msg)
         return GenerateResponse(prompt=d.get("prompt", ""), continuation=d.get("continuation", ""), request_id=rid,
-                                finish_reason=d.get("finish_reason", ""), ttft_s=float(d.get("ttft_s") or 0.0),
+                                token_ids=d.get("token_ids") or [], finish_reason=d.get("finish_reason", ""), ttft_s=float(d.get("ttft_s") or 0.0),
                                 e2e_s=float(time.perf_counter() - t0))
 
     def GenerateStream(self, req, ctx):
