@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--ctx", default="192,1024")
     ap.add_argument("--heads", default="32:32,32:8")
     ap.add_argument("--D", type=int, default=128)
+    ap.add_argument("--random-pages", action="store_true", help="scatter pages (default: engine-like sequential)")
     a = ap.parse_args()
     dev, bs, D = "cuda", 16, a.D
     for hk in a.heads.split(","):
@@ -25,17 +26,23 @@ def main():
         for ctx in map(int, a.ctx.split(",")):
             maxb = (ctx + bs - 1) // bs
             nb = a.B * maxb
-            kc = torch.randn(nb, nkv, bs, D, device=dev).to(torch.bfloat16)
-            vc = torch.randn_like(kc)
-            bt = torch.randperm(nb, device=dev).view(a.B, maxb).to(torch.int32)
+            kv_bytes = 2 * a.B * ctx * nkv * D * 2
+            ncopy = max(1, int(700e6 // kv_bytes) + 1)  # rotate copies past the 256 MiB Infinity Cache
+            kcs = [torch.randn(nb, nkv, bs, D, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
+            vcs = [torch.randn_like(kcs[0]) for _ in range(ncopy)]
+            pages = torch.randperm(nb, device=dev) if a.random_pages else torch.arange(nb, device=dev)
+            bt = pages.view(a.B, maxb).to(torch.int32)
             cl = torch.full((a.B,), ctx, dtype=torch.int32, device=dev)
             q = torch.randn(a.B, (nh + 2 * nkv) * D, device=dev).to(torch.bfloat16)
             out = torch.empty(a.B, nh * D, device=dev, dtype=torch.bfloat16)
-            kv_bytes = 2 * a.B * ctx * nkv * D * 2
             res = {"B": a.B, "nh": nh, "nkv": nkv, "ctx": ctx, "MB": round(kv_bytes / 1e6, 1)}
-            for u in (1, 2, 4):
+            for u in (1, 2, 4, 11, 12, 14):
                 H.lib().attn_decode_set_unroll(u)
-                f = lambda: H.attn_decode(q, kc, vc, bt, cl, nh, nkv, D, D ** -0.5, ctx, out=out)
+                it = [0]
+
+                def f():
+                    i = it[0] = (it[0] + 1) % ncopy
+                    H.attn_decode(q, kcs[i], vcs[i], bt, cl, nh, nkv, D, D ** -0.5, ctx, out=out)
                 for _ in range(5):
                     f()
                 torch.cuda.synchronize()

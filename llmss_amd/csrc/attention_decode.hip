@@ -117,8 +117,34 @@ __device__ __forceinline__ void fused_rotate(float (&x)[8], const FusedRope& fr,
   for (int j = 0; j < 8; ++j) x[j] = bf2f(f2bf(y[j]));
 }
 
-template <int D, int GB, int UNROLL, bool FUSED>
-__global__ __launch_bounds__(256) void attn_decode_kernel(
+
+// Sum over the LPT lanes that hold one token (LPT = D / 8 consecutive lanes) with DPP lane moves
+// instead of ds_bpermute shuffles (no LDS round trip in the per-token dependency chain).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
+}
+template <int LPT>
+__device__ __forceinline__ float token_sum(float s) {
+  if constexpr (LPT >= 16) {  // row_ror:8,4,2,1 inside each 16-lane row
+    s += dpp_f<0x128>(s);
+    s += dpp_f<0x124>(s);
+    s += dpp_f<0x122>(s);
+    s += dpp_f<0x121>(s);
+    if constexpr (LPT == 32) s += __shfl_xor(s, 16, 64);
+  } else if constexpr (LPT == 8) {  // row_half_mirror, then quad_perm xor 2, xor 1
+    s += dpp_f<0x141>(s);
+    s += dpp_f<0x4e>(s);   // quad_perm [2,3,0,1]
+    s += dpp_f<0xb1>(s);   // quad_perm [1,0,3,2]
+  } else {
+#pragma unroll
+    for (int o = 1; o < LPT; o <<= 1) s += __shfl_xor(s, o, 64);
+  }
+  return s;
+}
+
+template <int D, int GB, int UNROLL, bool FUSED, bool PIPE = false>
+__global__ __launch_bounds__(256, (!FUSED && GB == 1) ? 8 : 1) void attn_decode_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, bf16_t* __restrict__ out,
     int64_t out_stride, float* __restrict__ part_o, float* __restrict__ part_ml, int nh, int nkv, int G, int ngroups,
@@ -212,21 +238,35 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     }
   }
 
-  for (int tb = start + w * TPW + slot; tb < lend; tb += STEP * UNROLL) {
-    u16x8 kv[UNROLL], vv[UNROLL];
-    bool ok[UNROLL];
+  // page ids of this workgroup's context range, staged once in LDS: the token loop then needs no
+  // dependent block-table load (an L2 round trip) in front of every K/V load
+  constexpr int kMaxPages = 256;
+  __shared__ int s_pages[kMaxPages];
+  const int pg0 = start / block_size;
+  const int npg = end > start ? (end - 1) / block_size - pg0 + 1 : 0;
+  const bool lds_pages = npg <= kMaxPages;
+  if (lds_pages) {
+    for (int i = threadIdx.x; i < npg; i += blockDim.x) s_pages[i] = bt[pg0 + i];
+    __syncthreads();
+  }
+  auto kv_addr = [&](int t) -> int64_t {
+    const int pi = t / block_size;
+    const int page = lds_pages ? s_pages[pi - pg0] : bt[pi];
+    return page * page_stride + head_off + (int64_t)(t % block_size) * D;
+  };
+  auto load_tokens = [&](int tb, u16x8 (&kv)[UNROLL], u16x8 (&vv)[UNROLL]) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const int t = tb + u * STEP;
-      ok[u] = t < lend;
-      const int tt = ok[u] ? t : start;
-      const int page = bt[tt / block_size];
-      const int64_t a = page * page_stride + head_off + (int64_t)(tt % block_size) * D;
+      const int64_t a = kv_addr(t < lend ? t : start);
       kv[u] = *reinterpret_cast<const u16x8*>(kc + a);
       vv[u] = *reinterpret_cast<const u16x8*>(vc + a);
     }
+  };
+  auto consume = [&](int tb, const u16x8 (&kv)[UNROLL], const u16x8 (&vv)[UNROLL]) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
+      const bool ok = tb + u * STEP < lend;
       float kf[8], vf[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) { kf[j] = bf2f(kv[u][j]); vf[j] = bf2f(vv[u][j]); }
@@ -235,9 +275,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
         float s = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) s = fmaf(qv[h][j], kf[j], s);
-#pragma unroll
-        for (int o = 1; o < LPT; o <<= 1) s += __shfl_xor(s, o, 64);
-        if (ok[u]) {
+        s = token_sum<LPT>(s);
+        if (ok) {
           const float mn = fmaxf(m[h], s);
           const float alpha = exp2f(m[h] - mn), p = exp2f(s - mn);
           l[h] = l[h] * alpha + p;
@@ -246,6 +285,27 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
           m[h] = mn;
         }
       }
+    }
+  };
+  if constexpr (PIPE) {
+    // two register sets: the loads of the next UNROLL tokens per slot are in flight while the
+    // current ones are consumed (the compiler's counted vmcnt waits only for the set it reads)
+    constexpr int CH = STEP * UNROLL;
+    u16x8 kA[UNROLL], vA[UNROLL], kB[UNROLL], vB[UNROLL];
+    int tb = start + w * TPW + slot;
+    if (start < lend) load_tokens(tb, kA, vA);
+    for (; tb - slot - w * TPW < lend; tb += 2 * CH) {
+      load_tokens(tb + CH, kB, vB);
+      consume(tb, kA, vA);
+      if (tb + CH - slot - w * TPW >= lend) break;
+      load_tokens(tb + 2 * CH, kA, vA);
+      consume(tb + CH, kB, vB);
+    }
+  } else {
+    for (int tb = start + w * TPW + slot; tb < lend; tb += STEP * UNROLL) {
+      u16x8 kv[UNROLL], vv[UNROLL];
+      load_tokens(tb, kv, vv);
+      consume(tb, kv, vv);
     }
   }
 
@@ -323,8 +383,10 @@ __global__ __launch_bounds__(256) void attn_decode_reduce_kernel(const float* __
   }
 }
 
-static int g_decode_unroll = 2;  // tokens in flight per (wave, slot); tuning knob (attn_decode_set_unroll)
-void attn_decode_set_unroll(int u) { g_decode_unroll = (u == 1 || u == 4) ? u : 2; }
+// tokens in flight per (wave, slot): 1 / 2 / 4 = one register set; 11 / 12 / 14 = two register sets,
+// the next set's loads issued before the current set is consumed (tuning knob attn_decode_set_unroll)
+static int g_decode_unroll = 2;
+void attn_decode_set_unroll(int u) { g_decode_unroll = (u == 1 || u == 4 || u == 11 || u == 12 || u == 14) ? u : 2; }
 
 template <int D, int GB>
 static void launch_decode_t(const bf16_t* q, int64_t qs, bf16_t* kc, bf16_t* vc, const int* bt, int bts,
@@ -333,19 +395,24 @@ static void launch_decode_t(const bf16_t* q, int64_t qs, bf16_t* kc, bf16_t* vc,
   const int G = nh / nkv;
   const int ngroups = (G + GB - 1) / GB;
   dim3 grid(B, nkv * ngroups, nsplit);
-  if (!fr && g_decode_unroll != 2) {
-    if (g_decode_unroll == 1)
-      attn_decode_kernel<D, GB, 1, false><<<grid, 256, 0, st>>>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, nh, nkv, G,
-                                                                ngroups, bs, psize, scale * kLog2e, FusedRope{});
-    else
-      attn_decode_kernel<D, GB, 4, false><<<grid, 256, 0, st>>>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, nh, nkv, G,
-                                                                ngroups, bs, psize, scale * kLog2e, FusedRope{});
-  } else if (fr)
-    attn_decode_kernel<D, GB, 2, true><<<grid, 256, 0, st>>>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, nh, nkv, G,
-                                                             ngroups, bs, psize, scale * kLog2e, *fr);
-  else
-    attn_decode_kernel<D, GB, 2, false><<<grid, 256, 0, st>>>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, nh, nkv, G,
-                                                              ngroups, bs, psize, scale * kLog2e, FusedRope{});
+  const float sl2 = scale * kLog2e;
+#define AD(U_, FUSED_, PIPE_)                                                                                   \
+  attn_decode_kernel<D, GB, U_, FUSED_, PIPE_><<<grid, 256, 0, st>>>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, nh, \
+                                                                    nkv, G, ngroups, bs, psize, sl2,             \
+                                                                    fr ? *fr : FusedRope{})
+  if (fr) {
+    AD(2, true, false);
+  } else {
+    switch (g_decode_unroll) {
+      case 1: AD(1, false, false); break;
+      case 4: AD(4, false, false); break;
+      case 11: AD(1, false, true); break;
+      case 12: AD(2, false, true); break;
+      case 14: AD(4, false, true); break;
+      default: AD(2, false, false); break;
+    }
+  }
+#undef AD
   HIP_CHECK_LAUNCH();
   if (nsplit > 1) {
     attn_decode_reduce_kernel<D><<<dim3(B, nh), std::min(D, 256), 0, st>>>(po, pml, out, os, nh, nsplit);
