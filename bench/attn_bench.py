@@ -55,7 +55,7 @@ def main():
                 us = s.elapsed_time(e) * 1e3 / 50
                 res[f"u{u}_us"] = round(us, 2)
                 res[f"u{u}_TBps"] = round(kv_bytes / us / 1e6, 2)
-            H.lib().attn_decode_set_unroll(2)
+            H.lib().attn_decode_set_unroll(0)  # back to the default
             print(res, flush=True)
 
 
