@@ -26,9 +26,32 @@ SHAPES = {
 }
 
 
+GRAPH = True
+
+
 def timeit(fn, iters=50):
-    for _ in range(5):
-        fn(0)
+    """Per-call GPU time: the calls are captured into one HIP graph and replayed, so host launch
+    overhead (~10 us per call from Python) does not hide kernels shorter than that."""
+    for i in range(3):
+        fn(i)
+    torch.cuda.synchronize()
+    if GRAPH:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for i in range(iters):
+                fn(i)
+        g.replay()
+        torch.cuda.synchronize()
+        best = float("inf")
+        for _ in range(3):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            g.replay()
+            e.record()
+            torch.cuda.synchronize()
+            best = min(best, s.elapsed_time(e) / iters * 1e3)
+        del g
+        return best
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
@@ -45,13 +68,17 @@ def main():
     ap.add_argument("--shapes", default="llama7b")
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--fp8", action="store_true")
+    ap.add_argument("--hot", action="store_true", help="one weight copy (cache-resident), not HBM-streamed")
+    ap.add_argument("--no-graph", action="store_true", help="time a host loop of launches instead of a HIP graph")
     a = ap.parse_args()
+    global GRAPH
+    GRAPH = not a.no_graph
     dev = torch.device("cuda")
     out = []
     for sname in a.shapes.split(","):
         for name, N, K in SHAPES[sname]:
             wbytes = N * K * (1 if a.fp8 else 2)
-            ncopy = max(2, int(600e6 // wbytes) + 1)
+            ncopy = 1 if a.hot else max(2, int(600e6 // wbytes) + 1)
             ws = [(torch.randn(N, K, device=dev) * K ** -0.5).to(torch.bfloat16) for _ in range(ncopy)]
             scales = None
             if a.fp8:
@@ -82,6 +109,9 @@ def main():
                              for g in (1, 2, 3)]
                 if a.sweep and M >= 256 and not a.fp8:
                     cfgs += [(4 << 8, 1), (1 << 8, 1)]
+                if a.sweep and M >= 128 and not a.fp8:  # 8-wave 256x128 (5) / 256x64 (6) tiles, depth code 0/16/32
+                    cfgs += [((t | d) << 8, sp) for t, d in ((5, 0), (5, 16), (6, 16), (6, 32))
+                             for sp in (1, 2, 4, 6, 8, 12, 16)]
                 best = None
                 for nt, sp in cfgs:
                     try:

@@ -101,6 +101,24 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// Split-K tiled GEMMs: linear block id -> (m0, n0, split z). Items are ordered z-major, then
+// N-tile, with the M-tiles of one N-tile adjacent, and each XCD receives a contiguous item range
+// (dispatch is round-robin over the linear id). An XCD therefore works on whole weight columns and
+// one K-slice: its L2 fetches each weight tile once for every M-tile and only its K-slice of the
+// activations. Measured on the TP=8 QKV shape (M=512, N=1536, K=4096): the M-major order fetched
+// 59 MB from the fabric for 16.6 MB of unique operands.
+struct TileWork {
+  int m0, n0, z;
+};
+__device__ __forceinline__ TileWork tile_work(int ntm, int ntn, int bm, int bn) {
+  const int G = gridDim.x * gridDim.y;
+  const int w = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, G);
+  const int per = ntm * ntn;
+  const int z = w / per, t = w - z * per;
+  const int nt = t / ntm;
+  return {(t - nt * ntm) * bm, nt * bn, z};
+}
+
 #define HIP_CHECK_LAUNCH()                                                               \
   do {                                                                                   \
     hipError_t e__ = hipGetLastError();                                                  \

@@ -431,21 +431,22 @@ constexpr int TBK = 64;
 
 // F8: B (weights) is fp8-e4m3, one byte per element: its LDS image is [BN][64 B] with the 16-B chunk
 // q of row r stored at q ^ ((r >> 2) & 3) (ds_read_b64 fragment reads conflict-free, bank-simulated).
-template <int BN, bool F8>
+template <int BN, bool F8, int NW = 4>
 struct TiledB {
   static constexpr int ROWB = F8 ? 64 : 128;  // LDS bytes per B row per 64-k stage
   static constexpr int BYTES = BN * ROWB;
-  static constexpr int LOADS = F8 ? BN / 64 : BN / 32;  // glds per wave per stage
+  static constexpr int LOADS = F8 ? BN / (16 * NW) : BN / (8 * NW);  // glds per wave per stage
 };
 
-template <int BM, int BN, bool WNT = false, bool F8 = false>
+template <int BM, int BN, bool WNT = false, bool F8 = false, int NW = 4>
 __device__ __forceinline__ void tiled_stage(const bf16_t* __restrict__ A, int64_t lda, int M, const void* __restrict__ Bv,
                                             int64_t ldb, int N, int K, int m0, int n0, int k0, char* sA, char* sB,
                                             int w, int lane) {
-  // one wave-instruction = 1 KiB = 8 rows x 128 B; A needs BM/8 of them, B BN/8 (4 waves share)
+  // one wave-instruction = 1 KiB = 8 rows x 128 B; A needs BM/8 of them, B BN/8 (NW waves share)
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows must split evenly over the waves");
 #pragma unroll
-  for (int it = 0; it < BM / 32; ++it) {
-    const int inst = it * 4 + w;
+  for (int it = 0; it < BM / (8 * NW); ++it) {
+    const int inst = it * NW + w;
     const int row = inst * 8 + (lane >> 3);
     const int c = (lane & 7) ^ (row & 7);
     const int kc = min(k0 + c * 8, K - 8);
@@ -455,8 +456,8 @@ __device__ __forceinline__ void tiled_stage(const bf16_t* __restrict__ A, int64_
   if constexpr (F8) {
     const unsigned char* B = reinterpret_cast<const unsigned char*>(Bv);
 #pragma unroll
-    for (int it = 0; it < BN / 64; ++it) {  // one wave-instruction = 16 rows x 64 B
-      const int inst = it * 4 + w;
+    for (int it = 0; it < BN / (16 * NW); ++it) {  // one wave-instruction = 16 rows x 64 B
+      const int inst = it * NW + w;
       const int row = inst * 16 + (lane >> 2);
       const int gq = (lane & 3) ^ ((row >> 2) & 3);
       const int kc = min(k0 + gq * 16, K - 16);
@@ -466,8 +467,8 @@ __device__ __forceinline__ void tiled_stage(const bf16_t* __restrict__ A, int64_
   } else {
     const bf16_t* B = reinterpret_cast<const bf16_t*>(Bv);
 #pragma unroll
-    for (int it = 0; it < BN / 32; ++it) {
-      const int inst = it * 4 + w;
+    for (int it = 0; it < BN / (8 * NW); ++it) {
+      const int inst = it * NW + w;
       const int row = inst * 8 + (lane >> 3);
       const int c = (lane & 7) ^ (row & 7);
       const int kc = min(k0 + c * 8, K - 8);
@@ -539,22 +540,26 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int BM, int BN, int NS, bool WNT, bool F8 = false>
-__global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restrict__ A, int64_t lda,
+// NW = 4: waves 2 (M) x 2 (N); NW = 8 (256-row tiles, one workgroup per CU): waves 4 (M) x 2 (N),
+// each 64 x BN/2 - mid-M shapes (TP-sharded decode at M = 256-512) are per-CU load-latency bound,
+// so a wider tile moves fewer bytes per output through each CU's load path (guide: "Projection GEMM
+// at M = 256").
+template <int BM, int BN, int NS, bool WNT, bool F8 = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void gemm_tiled_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                          const void* __restrict__ B, int64_t ldb,
                                                          const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
                                                          int64_t ldy, float* __restrict__ part, int M, int N, int K,
                                                          int act, int glu, const float* __restrict__ wscale) {
-  constexpr int MTW = BM / 32, NTW = BN / 32;  // 16x16 tiles per wave
-  constexpr int A_BYTES = BM * TBK * 2, B_BYTES = TiledB<BN, F8>::BYTES, STAGE = A_BYTES + B_BYTES;
+  constexpr int MTW = BM / (8 * NW), NTW = BN / 32;  // 16x16 tiles per wave (waves NW/2 x 2)
+  constexpr int A_BYTES = BM * TBK * 2, B_BYTES = TiledB<BN, F8, NW>::BYTES, STAGE = A_BYTES + B_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int li = lane & 15, g = lane >> 4;
   const int wr = w >> 1, wc = w & 1;
   const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
-  const int tile = xcd_remap(blockIdx.x, ntn * ntm);
-  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+  const TileWork tw = tile_work(ntm, ntn, BM, BN);
+  const int m0 = tw.m0, n0 = tw.n0, zk = tw.z;
 
   f32x4 acc[MTW][NTW];
 #pragma unroll
@@ -565,10 +570,10 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
   // split-K (grid.y): slice z covers k-tiles [t0, t1); partial sums go to part[z] (fp32)
   const int nk_all = (K + TBK - 1) / TBK;
   const int per = (nk_all + gridDim.y - 1) / gridDim.y;
-  const int t0 = blockIdx.y * per, t1 = min(nk_all, t0 + per);
+  const int t0 = zk * per, t1 = min(nk_all, t0 + per);
   if constexpr (NS == 2) {
     if (t0 < t1) {
-      tiled_stage<BM, BN, WNT, F8>(A, lda, M, B, ldb, N, K, m0, n0, t0 * TBK, smem, smem + A_BYTES, w, lane);
+      tiled_stage<BM, BN, WNT, F8, NW>(A, lda, M, B, ldb, N, K, m0, n0, t0 * TBK, smem, smem + A_BYTES, w, lane);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
@@ -576,7 +581,7 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
       const int cur = (t - t0) & 1;
       char* nA = smem + (cur ^ 1) * STAGE;
       char* cA = smem + cur * STAGE;
-      if (t + 1 < t1) tiled_stage<BM, BN, WNT, F8>(A, lda, M, B, ldb, N, K, m0, n0, (t + 1) * TBK, nA, nA + A_BYTES, w, lane);
+      if (t + 1 < t1) tiled_stage<BM, BN, WNT, F8, NW>(A, lda, M, B, ldb, N, K, m0, n0, (t + 1) * TBK, nA, nA + A_BYTES, w, lane);
       if (t + 1 == nk_all && (K % TBK)) tiled_compute<MTW, NTW, true, F8>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
       else tiled_compute<MTW, NTW, false, F8>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -585,11 +590,11 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
   } else {
     // NS-stage ring: stage t+NS-1 is issued while stage t is computed; the wait before compute
     // only covers stage t (the younger stages' LOADS instructions each stay in flight): no drain.
-    constexpr int LOADS = BM / 32 + TiledB<BN, F8>::LOADS;  // global_load_lds per wave per stage
+    constexpr int LOADS = BM / (8 * NW) + TiledB<BN, F8, NW>::LOADS;  // global_load_lds per wave per stage
 #pragma unroll
     for (int j = 0; j < NS - 1; ++j)
       if (t0 + j < t1)
-        tiled_stage<BM, BN, WNT, F8>(A, lda, M, B, ldb, N, K, m0, n0, (t0 + j) * TBK, smem + j * STAGE,
+        tiled_stage<BM, BN, WNT, F8, NW>(A, lda, M, B, ldb, N, K, m0, n0, (t0 + j) * TBK, smem + j * STAGE,
                             smem + j * STAGE + A_BYTES, w, lane);
     int cur = 0;
     for (int t = t0; t < t1; ++t) {
@@ -599,7 +604,7 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
       const int nxt = cur == 0 ? NS - 1 : cur - 1;  // (cur + NS - 1) % NS
       if (t + NS - 1 < t1) {
         char* nA = smem + nxt * STAGE;
-        tiled_stage<BM, BN, WNT, F8>(A, lda, M, B, ldb, N, K, m0, n0, (t + NS - 1) * TBK, nA, nA + A_BYTES, w, lane);
+        tiled_stage<BM, BN, WNT, F8, NW>(A, lda, M, B, ldb, N, K, m0, n0, (t + NS - 1) * TBK, nA, nA + A_BYTES, w, lane);
       }
       if (t + 1 == nk_all && (K % TBK)) tiled_compute<MTW, NTW, true, F8>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
       else tiled_compute<MTW, NTW, false, F8>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
@@ -615,7 +620,7 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(const bf16_t* __restric
       const int m = m0 + wr * (MTW * 16) + mt * 16 + 4 * g + i;
       if (m >= M) continue;
       if (part) {
-        float* pr = part + ((int64_t)blockIdx.y * M + m) * N;
+        float* pr = part + ((int64_t)zk * M + m) * N;
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
           const int n = wn0 + nt * 16 + li;
@@ -1076,8 +1081,8 @@ __global__ __launch_bounds__(256) void gemm_f8f8_kernel(const unsigned char* __r
   const int li = lane & 15, g = lane >> 4;
   const int wr = w >> 1, wc = w & 1;
   const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
-  const int tile = xcd_remap(blockIdx.x, ntn * ntm);
-  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+  const TileWork tw = tile_work(ntm, ntn, BM, BN);
+  const int m0 = tw.m0, n0 = tw.n0, zk = tw.z;
   f32x4 acc[MTW][NTW];
 #pragma unroll
   for (int a = 0; a < MTW; ++a)
@@ -1086,7 +1091,7 @@ __global__ __launch_bounds__(256) void gemm_f8f8_kernel(const unsigned char* __r
 
   const int nk_all = (K + TBK8 - 1) / TBK8;
   const int per = (nk_all + gridDim.y - 1) / gridDim.y;
-  const int t0 = blockIdx.y * per, t1 = min(nk_all, t0 + per);
+  const int t0 = zk * per, t1 = min(nk_all, t0 + per);
 #pragma unroll
   for (int j = 0; j < NS - 1; ++j)
     if (t0 + j < t1)
@@ -1115,7 +1120,7 @@ __global__ __launch_bounds__(256) void gemm_f8f8_kernel(const unsigned char* __r
       if (m >= M) continue;
       const float sx = xs[m];
       if (part) {
-        float* pr = part + ((int64_t)blockIdx.y * M + m) * N;
+        float* pr = part + ((int64_t)zk * M + m) * N;
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
           const int n = wn0 + nt * 16 + li;
@@ -1379,9 +1384,11 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_f
 // per CU, keeping >= 512 k per slice. Measured on the Llama-2-7B shapes at M = 64..512
 // (bench/gemm_bench.py --sweep): within ~5% of the best (tile, split) of the sweep everywhere.
 static int tiles_of(int M, int N, int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); }
+// tsel: 1 = 128x128, 2 = 64x128, 3 = 64x64 (4 waves); 5 = 256x128, 6 = 256x64 (8 waves, 1 WG/CU);
+// 4 = the big-tile kernel
 static int tile_dims(int tsel, int* bm, int* bn) {
-  *bm = tsel == 1 ? 128 : 64;
-  *bn = tsel == 3 ? 64 : 128;
+  *bm = tsel >= 5 ? 256 : (tsel == 1 ? 128 : 64);
+  *bn = (tsel == 3 || tsel == 6) ? 64 : 128;
   return 0;
 }
 void gemm_tiled_plan(int M, int N, int K, int* tsel_io, int* split_io, bool glu) {
@@ -1398,8 +1405,9 @@ void gemm_tiled_plan(int M, int N, int K, int* tsel_io, int* split_io, bool glu)
     else tsel = M <= 64 ? (tiles_of(M, N, 64, 64) > 256 ? 2 : 3) : 1;
   }
   if (tsel == 4 && K % 64) tsel = 1;
-  const int hint_bits = tsel & ~15;
+  int hint_bits = tsel & ~15;
   tsel &= 15;
+  if (tsel >= 5) hint_bits &= ~128;  // no stream-K variant of the 8-wave tiles
   if (hint_bits & 128) {  // stream-K: output is final (no slabs); split_io carries workgroups per CU
     *tsel_io = tsel | hint_bits;
     if (*split_io <= 0) *split_io = 2;
@@ -1415,7 +1423,7 @@ void gemm_tiled_plan(int M, int N, int K, int* tsel_io, int* split_io, bool glu)
   const int nt = tiles_of(M, N, bm, bn);
   int s = *split_io;
   if (s <= 0) {
-    const int bound = bm == 64 ? 800 : 537;
+    const int bound = bm == 64 ? 800 : (bm == 128 ? 537 : 300);
     s = 1;
     while (nt * s * 2 <= bound && s < 8 && K / (2 * s) >= 512) s *= 2;
   }
@@ -1497,13 +1505,14 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
                  bool partial_out, hipStream_t st, const float* wscale) {
   const int tsel_raw = tsel;
   int s = split_hint;
+  const bool f8 = wscale != nullptr;  // fp8-e4m3 weights (W8A16): half the weight bytes of a decode step
+  if (f8 && (tsel & 15) >= 5) tsel = (tsel & ~15) | 1;  // 8-wave tiles are bf16-only
   gemm_tiled_plan(M, N, K, &tsel, &s, g != 0);
   static constexpr int kDepth[4] = {2, 3, 4, 6};
   int ns = kDepth[(tsel >> 4) & 3];  // LDS ring depth (hint bits 4-5); bit 6: default-policy weights
   tsel &= 15;
-  if (tsel == 1 && ns > 3) ns = 3;  // 128x128 x 4 stages would exceed the 160 KiB LDS
-  if (tsel == 2 && ns > 4) ns = 4;
-  const bool f8 = wscale != nullptr;  // fp8-e4m3 weights (W8A16): half the weight bytes of a decode step
+  if ((tsel == 1 || tsel == 5) && ns > 3) ns = 3;  // 128x128 / 256x128 x 4 stages exceed the 160 KiB LDS
+  if ((tsel == 2 || tsel == 6) && ns > 4) ns = 4;
   if (f8 && tsel == 4) tsel = 1;
   if (tsel == 4) {
     gemm_big_kernel<false><<<tiles_of(M, N, 256, 256), 512, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, M, N, K, act, g,
@@ -1511,7 +1520,7 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
     HIP_CHECK_LAUNCH();
     return 0;
   }
-  if ((tsel_raw & 128) && !f8) {
+  if ((tsel_raw & 128) && !f8 && tsel < 5) {
     if (launch_streamk(X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, M, N, K, act, g, tsel, ns, s, workspace, ws_bytes,
                        wnt_ok(tsel_raw, M, tsel), st))
       return 0;
@@ -1526,6 +1535,23 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   dim3 grid(nt, s);
   // non-temporal weight staging when every weight tile is read by exactly one workgroup row
   const bool wnt = wnt_ok(tsel_raw, M, tsel);
+  if (tsel >= 5) {  // 8-wave tiles (bf16 weights)
+#define LT8(BM_, BN_, NS_)                                                                                          \
+  do {                                                                                                             \
+    if (wnt)                                                                                                       \
+      gemm_tiled_kernel<BM_, BN_, NS_, true, false, 8><<<grid, 512, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N, K, \
+                                                                             act_k, glu_k, nullptr);               \
+    else                                                                                                           \
+      gemm_tiled_kernel<BM_, BN_, NS_, false, false, 8><<<grid, 512, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N,  \
+                                                                              K, act_k, glu_k, nullptr);           \
+  } while (0)
+    if (tsel == 5) {
+      if (ns == 3) LT8(256, 128, 3); else LT8(256, 128, 2);
+    } else {
+      if (ns == 4) LT8(256, 64, 4); else if (ns == 3) LT8(256, 64, 3); else LT8(256, 64, 2);
+    }
+#undef LT8
+  } else {
 #define LT1(BM_, BN_, NS_, WNT_, F8_)                                                                              \
   gemm_tiled_kernel<BM_, BN_, NS_, WNT_, F8_><<<grid, 256, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N, K, act_k,  \
                                                                     glu_k, wscale)
@@ -1545,6 +1571,7 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
     LT(64, 64, 6);
   } else {
     if (tsel == 1) LT(128, 128, 2); else if (tsel == 2) LT(64, 128, 2); else LT(64, 64, 2);
+  }
   }
 #undef LT
 #undef LT1
@@ -1576,8 +1603,8 @@ int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int n
     if (split_hint > 0) s = split_hint;
   } else {
     int tsel = tiled_hint;
-    if ((tsel & 128) && !w_fp8) return 0;  // stream-K combines in-kernel
-    if (w_fp8 && (tsel & 15) == 4) tsel = (tsel & ~15) | 1;
+    if ((tsel & 128) && !w_fp8 && (tsel & 15) < 5) return 0;  // stream-K combines in-kernel
+    if (w_fp8 && ((tsel & 15) == 4 || (tsel & 15) >= 5)) tsel = (tsel & ~15) | 1;
     s = split_hint;
     gemm_tiled_plan(M, N, K, &tsel, &s, false);
     if ((tsel & 15) == 4 || (tsel & 128)) return 0;

@@ -54,6 +54,10 @@ class Request:
     def all_ids(self) -> List[int]:
         return self.prompt_ids + self.output_ids
 
+    @property
+    def last_id(self) -> int:
+        return self.output_ids[-1] if self.output_ids else self.prompt_ids[-1]
+
     def metrics(self) -> Dict[str, float]:
         ttft = self.t_first - self.t_arrival if self.t_first else float("nan")
         n = len(self.output_ids)
@@ -316,7 +320,7 @@ class LLMEngine:
 
     def _decode(self, batch, reqs: List[Request]) -> List[int]:
         n = len(reqs)
-        ids = np.array([r.all_ids[-1] for r in reqs], dtype=np.int64)
+        ids = np.array([r.last_id for r in reqs], dtype=np.int64)
         temp, topk, topp, seeds = self._sampling_arrays(reqs)
         if not self.is_gpu:
             dev = self.device

@@ -60,20 +60,32 @@ def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, 
             out += [((t | d | 128) << 8, g) for g in (1, 2, 3)]
     if M >= 256 and K % 64 == 0:
         out.append((4 << 8, 1))
+    if M >= 128:  # 8-wave 256x128 (5) / 256x64 (6) tiles: one workgroup per CU, deep split-K
+        out += [((t | d) << 8, s) for t, d in ((5, 16), (6, 16), (6, 32)) for s in (2, 4, 8, 12, 16)]
     return out
 
 
 def _time(fn, iters: int) -> float:
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for i in range(iters):
-        fn(i)
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) * 1e3 / iters  # us
+    """GPU time per call. The calls are captured into one HIP graph and replayed (as the decode graphs
+    run them): timing a host loop instead measures Python launch overhead (~10 us per call) for
+    every kernel shorter than that, which is most TP-sharded decode GEMMs."""
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for i in range(iters):
+            fn(i)
+    g.replay()
+    best = float("inf")
+    for _ in range(2):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        g.replay()
+        e.record()
+        e.synchronize()
+        best = min(best, s.elapsed_time(e) * 1e3 / iters)  # us
+    return best
 
 
-def tune_shape(M: int, shape: GemmShape, device, weight_budget: int = 600 << 20, iters: int = 6,
+def tune_shape(M: int, shape: GemmShape, device, weight_budget: int = 600 << 20, iters: int = 16,
                cands: Optional[Sequence[Tuple[int, int]]] = None) -> Tuple[int, int, float, float]:
     """Best (nt_hint, split, us, default_us) for one shape."""
     from . import hip as H
@@ -109,7 +121,8 @@ def tune_shape(M: int, shape: GemmShape, device, weight_budget: int = 600 << 20,
         slabs = r.S if isinstance(r, H.PartialSum) else 0
         for i in range(2):
             f(i)
-        t = min(_time(f, iters), _time(f, iters))
+        torch.cuda.synchronize(device)
+        t = _time(f, iters)
         return t + (slabs * M * N * 4 / _SLAB_READ_BPS * 1e6 if slabs else 0.0)
 
     default = cost(0, 0)

@@ -151,13 +151,15 @@ def test_gemm(M, N, K):
         close(H.linear(x, w, None, glu=True), R.linear(x.float(), w.float(), None, glu=True), 2e-2)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4])  # 128x128, 64x128, 64x64, 256x256 (8 waves)
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6])  # 128x128, 64x128, 64x64, 256x256, 256x128 / 256x64 (8 waves)
 @pytest.mark.parametrize("stages", [2, 3, 4, 6])
 @pytest.mark.parametrize("split", [1, 3, 8])
 @pytest.mark.parametrize("M,N,K", [(64, 1536, 4096), (200, 4800, 1600), (37, 256, 64 * 5 + 16), (700, 1312, 192)])
 def test_gemm_tiled_variants(tile, stages, split, M, N, K):
     if tile == 4 and (stages != 2 or split > 1):
         pytest.skip("the 256x256 kernel has one pipeline and no split-K")
+    if tile >= 5 and stages == 6:
+        pytest.skip("8-wave tiles ring at most 3 (256x128) / 4 (256x64) stages (clamped)")
     torch.manual_seed(0)
     x, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
     b = rnd(N, scale=0.1)
@@ -410,7 +412,9 @@ def test_gemm_fp8_tiled(tile, stages, split, M, N, K):
 
 @pytest.mark.parametrize("fp8", [False, True])
 @pytest.mark.parametrize("M,hint,split", [(256, 0x21, 4), (512, 0x12, 2), (200, (1 | 16 | 128) << 8, 2),
-                                          (96, (3 | 128) << 8, 3), (64, 0x300, 4), (64, 0x1300, 1)])
+                                          (96, (3 | 128) << 8, 3), (64, 0x300, 4), (64, 0x1300, 1),
+                                          (512, (5 | 16) << 8, 8), (300, (6 | 32) << 8, 12),
+                                          (256, (5 | 128) << 8, 4)])
 def test_partial_capable_calls_never_lose_output(fp8, M, hint, split):
     """partial_ok=True must return split-K slabs only when the kernel leaves them (stream-K and fp8
     prefill panels finish their output in place): regression for a null-output fault."""
