@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--simulate-tp", type=int, default=0,
                     help="dev tool: one process computes rank 0 of a TP=N shard plan with no communication "
                          "(per-rank compute time at TP=N shapes; not a headline number)")
+    ap.add_argument("--sim-comm", default="",
+                    help="with --simulate-tp: model each all-reduce / all-gather as LAT_US,GBPS (latency + bytes / "
+                         "algorithmic bandwidth, a spin kernel on the collective's stream) to measure comm overlap")
     args = ap.parse_args()
 
     from llmss_amd.engine import LLMEngine, SamplingParams, build_model
@@ -55,7 +58,8 @@ def main():
 
         if world != 1:
             raise SystemExit("--simulate-tp runs in a single process")
-        tp = TPGroup(0, args.simulate_tp, fake=True)
+        sim = tuple(float(v) for v in args.sim_comm.split(",")) if args.sim_comm else None
+        tp = TPGroup(0, args.simulate_tp, fake=True, sim_comm=sim)
     dev = torch.device("cuda", torch.cuda.current_device())
     batch = args.batch_per_gpu * max(world, args.simulate_tp)
     model = build_model(args.model, tp, "bf16", dev, fp8=args.fp8, random_init=True)
@@ -133,7 +137,7 @@ def main():
             "p50_ttft_ms": round(float(ttft), 3),
             "p50_request_latency_ms": round(float(e2e), 3),
             "config": {"model": args.model, "global_batch": batch, "seq_len": args.prompt_len + args.gen_len,
-                       "prompt_len": args.prompt_len, "gen_len": args.gen_len, "parallelism": (f"tp{args.simulate_tp}-simulated-no-comm" if args.simulate_tp > 1 else f"tp{world}"),
+                       "prompt_len": args.prompt_len, "gen_len": args.gen_len, "parallelism": (f"tp{args.simulate_tp}-simulated-" + (f"comm-model-{args.sim_comm}" if args.sim_comm else "no-comm") if args.simulate_tp > 1 else f"tp{world}"),
                        "sampling": "greedy" if args.greedy else "temperature=1.0,top_p=0.95,top_k=50",
                        "engine_stats": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()},
                        **({"phase_ms": eng.phase_summary()} if eng.timer.enabled else {})},

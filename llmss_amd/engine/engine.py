@@ -154,7 +154,7 @@ class LLMEngine:
         self.buf = _DecodeBuffers(self.buckets[-1], self.max_blocks, self.device) if self.is_gpu else None
         if self.is_gpu:
             _hip_ops.reserve_workspace(self.device, 64 << 20)
-            for b in self.buckets:
+            for b in self.decode_batch_sizes():
                 nsplit, _ = self._splits(b)
                 if nsplit > 1:
                     _hip_ops._DECODE_WS.get(b, model.plan.nh_l, nsplit, self.cfg.head_dim, self.device)
@@ -164,7 +164,7 @@ class LLMEngine:
         if self.is_gpu and autotune:  # per-shape GEMM plans for every decode bucket (ops/autotune.py)
             from ..ops.autotune import tune_model
 
-            self.tuned = tune_model(model, self.buckets)
+            self.tuned = tune_model(model, self.decode_batch_sizes())
         if self.use_graphs and os.environ.get("LLMSS_GRAPHS", "1") == "0":
             self.use_graphs = False
         if self.use_graphs:
@@ -194,6 +194,16 @@ class LLMEngine:
             n = max(64, budget // per)
             return int(min(n, want))
         return int(min(want, max(64, (2 << 30) // per)))
+
+    def decode_batch_sizes(self) -> List[int]:
+        """Row counts the decode kernels run at: every bucket, plus both micro-batch halves of the
+        buckets that DecoderLM splits for all-reduce / compute overlap."""
+        out = set(self.buckets)
+        for b in self.buckets:
+            h = self.model.overlap_split(b)
+            if h:
+                out.update((h, b - h))
+        return sorted(out)
 
     def _splits(self, b):
         return _hip_ops.decode_splits(b, self.model.plan.nkv_l, self.max_model_len, self.block_size)

@@ -68,6 +68,13 @@ class DecoderLM:
         # fused RoPE+KV-write+attention decode: correct, but measured slower (its prologue halves the
         # attention kernel's occupancy), so opt-in
         self.fused_decode = os.environ.get("LLMSS_FUSED_DECODE", "0") == "1"
+        # decode steps of at least this many sequences run as two interleaved micro-batches so each
+        # one's all-reduces overlap the other's compute; only when collectives cost time. Opt-in
+        # (0 = off): measured on MI355X (bench/tbo_probe.py, Llama-2-7B TP=8 shard, batch 512, 8
+        # layers) the split alone costs +51% (half-batch decode kernels are nearly as long as
+        # full-batch ones) and each cross-stream hand-off inside a HIP graph ~10 us, more than a
+        # modelled 52 us all-reduce hides: 2639 vs 2519 us per step (profiles/r1_tbo/)
+        self.tbo_min = int(os.environ.get("LLMSS_TP_DECODE_OVERLAP_MIN", "0"))
         self._comm_stream = None
 
     @property
@@ -109,6 +116,11 @@ class DecoderLM:
         return ops.attn_decode(qkv, kc, vc, inp.block_tables, inp.ctx_lens, p.nh_l, p.nkv_l, D, self.scale,
                                inp.max_ctx, splits=inp.decode_splits)
 
+    def _comm(self, device):
+        if self._comm_stream is None:
+            self._comm_stream = torch.cuda.Stream(device=device, priority=-1)
+        return self._comm_stream
+
     def _reduce_rows(self, fn, *inputs) -> torch.Tensor:
         """``all_reduce(fn(*inputs))`` for a row-parallel projection (or a whole MLP).
 
@@ -117,7 +129,7 @@ class DecoderLM:
         all-reduce hides behind the next GEMM (prefill at TP=8 moves ~0.5 GB per all-reduce). Decode
         steps (a few MB, latency-bound) keep one all-reduce.
         """
-        if not self.tp.is_real:
+        if not self.tp.comm_active:
             return fn(*inputs)
         M = inputs[0].shape[0]
         step = self.overlap_rows
@@ -126,9 +138,7 @@ class DecoderLM:
         if not inputs[0].is_cuda:  # gloo / CPU: same chunking (numerics), no streams
             return torch.cat([self.tp.all_reduce(fn(*(t[r:r + step] for t in inputs))) for r in range(0, M, step)])
         cur = torch.cuda.current_stream()
-        if self._comm_stream is None:
-            self._comm_stream = torch.cuda.Stream(device=inputs[0].device, priority=-1)
-        comm = self._comm_stream
+        comm = self._comm(inputs[0].device)
         outs = []
         for r in range(0, M, step):
             y = fn(*(t[r:r + step] for t in inputs))
@@ -140,7 +150,97 @@ class DecoderLM:
         cur.wait_stream(comm)
         return torch.cat(outs)
 
+    # ------------------------------------------------------- two-micro-batch decode overlap
+    def overlap_split(self, B: int) -> int:
+        """Rows in the first micro-batch of a B-row decode step (0 = no split)."""
+        if self.tbo_min <= 0 or B < max(2, self.tbo_min) or not self.tp.comm_active:
+            return 0
+        return (B // 2 + 7) // 8 * 8 if B >= 32 else B // 2
+
+    def _sub_step(self, inp: StepInput, r0: int, r1: int, block_size: int) -> StepInput:
+        splits = inp.decode_splits
+        if splits is not None and inp.input_ids.is_cuda:
+            splits = _hip_ops().decode_splits(r1 - r0, self.plan.nkv_l, inp.max_ctx, block_size)
+        return StepInput("decode", inp.input_ids[r0:r1], inp.positions[r0:r1], inp.slots[r0:r1],
+                         block_tables=inp.block_tables[r0:r1], ctx_lens=inp.ctx_lens[r0:r1], max_ctx=inp.max_ctx,
+                         decode_splits=splits)
+
+    def _hidden_states_overlap(self, inp: StepInput, kv_caches, h: int) -> torch.Tensor:
+        """Decode step as two micro-batches (rows [0, h) and [h, B)) interleaved layer by layer.
+
+        Compute-stream order per layer: A.attn, B.attn, A.mlp, B.mlp. Each block's all-reduce goes
+        to the high-priority comm stream and the compute stream waits for it (event) only right
+        before that micro-batch's next use, i.e. after the other micro-batch's block has been
+        queued. RCCL therefore runs while the matrix cores work on the other half of the batch,
+        instead of in series with them; the price is reading each layer's weight shard twice.
+        All ranks queue the collectives in the same order (A before B), as RCCL requires.
+        """
+        cfg, w = self.cfg, self.w
+        eps, rms = cfg.norm_eps, self.rms
+        B = inp.input_ids.shape[0]
+        bs = kv_caches[0][0].shape[2]
+        subs = (self._sub_step(inp, 0, h, bs), self._sub_step(inp, h, B, bs))
+        rows = ((0, h), (h, B))
+        on_gpu = inp.input_ids.is_cuda
+        cur = torch.cuda.current_stream() if on_gpu else None
+        comm = self._comm(inp.input_ids.device) if on_gpu else None
+
+        diag = os.environ.get("LLMSS_TBO_DIAG", "")
+
+        def reduce(t):  # all-reduce t on the comm stream; returns the event to wait on before reading t
+            if not on_gpu or diag == "onestream":
+                self.tp.all_reduce(t)
+                return None
+            comm.wait_stream(cur)
+            with torch.cuda.stream(comm):
+                self.tp.all_reduce(t)
+                ev = torch.cuda.Event()
+                ev.record(comm)
+            if diag != "norecord":
+                t.record_stream(comm)
+            return ev
+
+        def ready(ev):
+            if ev is not None:
+                cur.wait_event(ev)
+
+        x = ops.embed(inp.input_ids, w.wte, inp.positions if w.wpe is not None else None, w.wpe)
+        delta = [x[r0:r1] for r0, r1 in rows]
+        res: List[Optional[torch.Tensor]] = [None, None]
+        pend = [None, None]
+        for i, L in enumerate(w.layers):
+            kc, vc = kv_caches[i]
+            if cfg.parallel_block:  # GPT-J: one all-reduce per layer and micro-batch
+                for j in (0, 1):
+                    ready(pend[j])
+                    y, res[j] = ops.add_norm(delta[j], L.ln1_w, L.ln1_b, eps, rms, res[j])
+                    a = self._attention(L.qkv(y, partial_ok=True), subs[j], kc, vc)
+                    delta[j] = L.o(a).add_(L.down(L.up(y, self.act)))
+                    pend[j] = reduce(delta[j])
+                continue
+            o = [None, None]
+            for j in (0, 1):
+                ready(pend[j])
+                y, res[j] = ops.add_norm(delta[j], L.ln1_w, L.ln1_b, eps, rms, res[j])
+                a = self._attention(L.qkv(y, partial_ok=True), subs[j], kc, vc)
+                o[j] = L.o(a)
+                pend[j] = reduce(o[j])
+            for j in (0, 1):
+                ready(pend[j])
+                y2, res[j] = ops.add_norm(o[j], L.ln2_w, L.ln2_b, eps, rms, res[j])
+                delta[j] = L.down(L.up(y2, self.act))
+                pend[j] = reduce(delta[j])
+        out = torch.empty_like(x)
+        for j, (r0, r1) in enumerate(rows):
+            ready(pend[j])
+            ops.add_norm(delta[j], w.lnf_w, w.lnf_b, eps, rms, res[j], out=out[r0:r1])
+        return out
+
     def hidden_states(self, inp: StepInput, kv_caches) -> torch.Tensor:
+        if inp.kind == "decode":
+            h = self.overlap_split(inp.input_ids.shape[0])
+            if h:
+                return self._hidden_states_overlap(inp, kv_caches, h)
         cfg, w = self.cfg, self.w
         eps, rms = cfg.norm_eps, self.rms
         x = ops.embed(inp.input_ids, w.wte, inp.positions if w.wpe is not None else None, w.wpe)

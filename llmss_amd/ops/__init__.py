@@ -25,10 +25,14 @@ def _hip():
     return hip
 
 
-def add_norm(x, weight, bias, eps, rms, residual=None):
+def add_norm(x, weight, bias, eps, rms, residual=None, out=None):
     if x.is_cuda:
-        return _hip().add_norm(x, weight, bias, eps, rms, residual)
-    return ref.add_norm(x, weight, bias, eps, rms, residual)
+        return _hip().add_norm(x, weight, bias, eps, rms, residual, out=out)
+    y, r = ref.add_norm(x, weight, bias, eps, rms, residual)
+    if out is not None:
+        out.copy_(y)
+        y = out
+    return y, r
 
 
 def embed(ids, wte, positions=None, wpe=None):

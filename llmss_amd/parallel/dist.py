@@ -18,7 +18,7 @@ from __future__ import annotations
 
 import os
 from datetime import timedelta
-from typing import List, Optional
+from typing import List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -31,11 +31,17 @@ log = get_logger(__name__)
 class TPGroup:
     """Tensor-parallel communicator (size 1, real, or fake)."""
 
-    def __init__(self, rank: int = 0, size: int = 1, group=None, fake: bool = False):
+    def __init__(self, rank: int = 0, size: int = 1, group=None, fake: bool = False,
+                 sim_comm: Optional[Tuple[float, float]] = None):
         self.rank = rank
         self.size = size
         self.group = group
         self.fake = fake
+        # fake groups only: (latency us, algorithmic GB/s) of a modelled all-reduce. Each all-reduce
+        # then occupies the issuing stream for latency + bytes/bandwidth (a spin kernel on one
+        # workgroup), so the comm/compute overlap of a TP=N schedule can be measured on one GPU.
+        self.sim_comm = sim_comm if fake and size > 1 else None
+        self._cycles_per_us = None
 
     # reference-compatible accessors (FakeGroup.size()/rank())
     def world_size(self) -> int:
@@ -45,15 +51,43 @@ class TPGroup:
     def is_real(self) -> bool:
         return self.size > 1 and not self.fake
 
+    @property
+    def comm_active(self) -> bool:
+        """Collectives take time on a stream (real communicator, or a fake one modelling comm)."""
+        return self.is_real or self.sim_comm is not None
+
+    def _sim_wait(self, nbytes: int):
+        if self._cycles_per_us is None:  # calibrate the spin kernel's clock once (outside capture)
+            torch.cuda._sleep(1000)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            torch.cuda._sleep(2_000_000)
+            e.record()
+            e.synchronize()
+            self._cycles_per_us = 2_000_000 / (s.elapsed_time(e) * 1e3)
+        lat, gbps = self.sim_comm
+        us = lat + nbytes / (gbps * 1e3)
+        if os.environ.get("LLMSS_SIM_COMM_OP") == "touch":  # diagnostic: a tiny real kernel instead of a spin
+            self._touch = getattr(self, "_touch", None)
+            if self._touch is None:
+                self._touch = torch.zeros(64, device="cuda")
+            self._touch.add_(1.0)
+            return
+        torch.cuda._sleep(max(1, int(us * self._cycles_per_us)))
+
     # ------------------------------------------------------------ data plane
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.is_real:
             dist.all_reduce(t, group=self.group)
+        elif self.sim_comm is not None and t.is_cuda:
+            self._sim_wait(t.numel() * t.element_size())
         return t
 
     def all_gather_last_dim(self, t: torch.Tensor) -> torch.Tensor:
         """Gather shards along the last dim: [..., n] -> [..., size*n]."""
         if not self.is_real:
+            if self.sim_comm is not None and t.is_cuda:
+                self._sim_wait(self.size * t.numel() * t.element_size())
             return t
         t = t.contiguous()
         out = torch.empty((self.size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)

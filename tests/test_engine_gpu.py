@@ -174,3 +174,78 @@ def test_rccl_collectives_inside_decode_graphs():
     del e_graph
     e_eager = LLMEngine(m, max_num_seqs=4, block_size=16, use_graphs=False, autotune=False)
     assert e_eager.generate(prompts, sp) == out_g
+
+
+def _one_member_tp():
+    import os
+
+    import torch.distributed as dist
+
+    from llmss_amd.parallel.dist import TPGroup
+
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+
+    class OneMemberTP(TPGroup):  # TP=2 shard plan over a 1-rank communicator (collectives run, sum = identity)
+        def all_gather_last_dim(self, t):
+            out = torch.empty((t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+            return torch.cat([out, out], -1)
+
+    return OneMemberTP(0, 2, group=dist.group.WORLD)
+
+
+@pytest.mark.parametrize("fam", ["tiny-llama", "tiny-gptj"])
+def test_decode_microbatch_overlap(fam):
+    """Two-micro-batch decode (each half's RCCL all-reduces on the comm stream while the other half
+    computes) == the single-batch decode step, for sequential (Llama) and parallel (GPT-J) blocks."""
+    tp = _one_member_tp()
+    par = fam == "tiny-gptj"
+    cfg = get_preset(fam, hidden_size=256, num_heads=4, head_dim=64, rotary_dim=16 if par else 64,
+                     intermediate_size=512, max_position_embeddings=256, **({} if par else {"num_kv_heads": 2}))
+    m = DecoderLM(cfg, random_weights(cfg, 2, 0, device="cuda", dtype=torch.bfloat16, seed=4, std=0.05), tp)
+    bs, nseq, per = 16, 24, 4  # 24 sequences, 4 blocks (64 tokens) each
+    kv = m.allocate_kv_cache(nseq * per, bs)
+    lens = [5 + (7 * i) % 40 for i in range(nseq)]
+    ids = torch.randint(0, cfg.vocab_size, (sum(lens),), device="cuda")
+    pos = torch.cat([torch.arange(n) for n in lens]).cuda()
+    slots = torch.cat([torch.arange(n) + i * per * bs for i, n in enumerate(lens)]).cuda()
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device="cuda")
+    m.hidden_states(StepInput("prefill", ids, pos, slots, cu_seqlens=cu, max_seqlen=max(lens)), kv)
+    bt = torch.arange(nseq * per, dtype=torch.int32, device="cuda").view(nseq, per)
+    L = torch.tensor(lens, device="cuda")
+    dec = StepInput("decode", torch.randint(0, cfg.vocab_size, (nseq,), device="cuda"), L.clone(),
+                    L + torch.arange(nseq, device="cuda") * per * bs, block_tables=bt,
+                    ctx_lens=(L + 1).to(torch.int32), max_ctx=per * bs)
+    m.tbo_min = 0
+    ref = m.hidden_states(dec, kv)
+    m.tbo_min = 2
+    assert m.overlap_split(nseq) == 12
+    out = m.hidden_states(dec, kv)  # rewrites the same KV slots with the same values
+    torch.cuda.synchronize()
+    err = (out.float() - ref.float()).abs().max().item()
+    assert err < 5e-2, err
+
+
+def test_decode_microbatch_overlap_in_graphs():
+    """The micro-batch decode schedule (two streams, event joins, RCCL) captures into HIP graphs and
+    replays exactly like eager; also with the modelled-comm fake group used by bench --sim-comm."""
+    from llmss_amd.parallel.dist import TPGroup
+
+    cfg = get_preset("tiny-llama", hidden_size=256, num_heads=4, num_kv_heads=2, head_dim=64, rotary_dim=64,
+                     intermediate_size=512, max_position_embeddings=256)
+    w = random_weights(cfg, 2, 0, device="cuda", dtype=torch.bfloat16, seed=3, std=0.05)
+    prompts = [[int(x) for x in torch.randint(0, cfg.vocab_size, (n,))] for n in (5, 17, 33, 9, 12, 40, 3, 21)]
+    sp = SamplingParams(max_new_tokens=10, is_greedy=True, ignore_eos=True)
+    for tp in (_one_member_tp(), TPGroup(0, 2, fake=True, sim_comm=(3.0, 100.0))):
+        m = DecoderLM(cfg, w, tp)
+        m.tbo_min = 4
+        e_graph = LLMEngine(m, max_num_seqs=8, block_size=16, use_graphs=True, autotune=False)
+        assert e_graph.use_graphs and len(e_graph.graphs) > 0
+        assert 4 in e_graph.decode_batch_sizes()  # halves of the 8-row bucket
+        out_g = e_graph.generate(prompts, sp)
+        del e_graph
+        e_eager = LLMEngine(m, max_num_seqs=8, block_size=16, use_graphs=False, autotune=False)
+        assert e_eager.generate(prompts, sp) == out_g
