@@ -11,6 +11,7 @@
 // index, so every tensor-parallel rank - which holds the same all-gathered logits - draws the
 // same token with no broadcast (reference broadcasts the sampled token every step, C7/C11).
 #include "common.h"
+#include <cstdlib>
 
 __device__ __forceinline__ unsigned fkey(float f) {  // order-preserving (ascending) uint key
   unsigned u = __float_as_uint(f);
@@ -211,13 +212,20 @@ __device__ void sv3_find(const T* arr, unsigned long long target, int limit, Sv3
   __syncthreads();
 }
 
-template <int CPT>
+// LROW: the packed row lives in LDS instead of VGPRs. At CPT = 8 (vocab 32K-57K, e.g. GPT-2's
+// padded 50304) a register-resident row exceeds the 128-VGPR budget of a 1024-thread block: the
+// compiler spills to scratch and the kernel takes ~100 us per call even for argmax; every pass
+// over the row re-reads it from LDS (ds_read_b128, conflict-free lane-linear chunks) instead.
+constexpr int SV3_LROW_CHUNKS = 7168;  // 112 KiB row + ~40 KiB Sv3Smem < 160 KiB LDS
+
+template <int CPT, bool LROW>
 __global__ __launch_bounds__(1024) void sample_v3_kernel(const bf16_t* __restrict__ logits, int64_t ld, int V,
                                                          const float* __restrict__ temperature,
                                                          const int* __restrict__ top_k, const float* __restrict__ top_p,
                                                          const int64_t* __restrict__ seeds, int64_t* __restrict__ out,
                                                          int64_t* __restrict__ out2) {
   __shared__ Sv3Smem sm;
+  __shared__ __attribute__((aligned(16))) u16x8 srow[LROW ? SV3_LROW_CHUNKS : 1];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
   const bf16_t* row = logits + b * ld;
@@ -228,32 +236,46 @@ __global__ __launch_bounds__(1024) void sample_v3_kernel(const bf16_t* __restric
   const float scale = greedy ? 1.f : 1.f / temp;
 
   // the row stays packed (bf16) in registers; X(i) = scaled logit of element slot i, -inf past V
-  u16x8 raw[CPT];
+  u16x8 raw[LROW ? 1 : CPT];
 #pragma unroll
   for (int c = 0; c < CPT; ++c) {
     const int ch = tid + c * 1024;
-    raw[c] = ch * 8 < V ? *reinterpret_cast<const u16x8*>(row + ch * 8) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    const u16x8 v = ch * 8 < V ? *reinterpret_cast<const u16x8*>(row + ch * 8) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if constexpr (LROW) {
+      if (ch < SV3_LROW_CHUNKS) srow[ch] = v;
+    } else {
+      raw[c] = v;
+    }
   }
-#define X(i) (((tid + ((i) >> 3) * 1024) * 8 + ((i) & 7) < V) ? bf2f(raw[(i) >> 3][(i) & 7]) * scale : -INFINITY)
+  if constexpr (LROW) __syncthreads();
+#define CHUNK(c) (LROW ? srow[tid + (c) * 1024] : raw[LROW ? 0 : (c)])
+// element loops: FOR_ELEMS(i) { ... X(i) ... } END_ELEMS - one chunk read per 8 elements; the chunk loop
+// stays rolled for an LDS row (else the compiler hoists every pass's 64 LDS values into VGPRs)
+constexpr int UNR = LROW ? 1 : CPT;
+#define FOR_ELEMS(i)                                 \
+  _Pragma("unroll UNR") for (int c_ = 0; c_ < CPT; ++c_) { \
+    const u16x8 rc_ = CHUNK(c_);                     \
+    _Pragma("unroll") for (int j_ = 0; j_ < 8; ++j_) { \
+      const int i = c_ * 8 + j_;
+#define END_ELEMS }}
+#define X(i) (((tid + ((i) >> 3) * 1024) * 8 + ((i) & 7) < V) ? bf2f(rc_[(i) & 7]) * scale : -INFINITY)
   float thr = -INFINITY;
   if (!greedy) {
     float mx = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < CPT * 8; ++i) mx = fmaxf(mx, X(i));
+    FOR_ELEMS(i) mx = fmaxf(mx, X(i)); END_ELEMS
     mx = block_max(mx, sm.red);
     const bool do_k = k > 0 && k < V, do_p = p < 1.f;
     if (do_k || do_p) {
       for (int i = tid; i < SV3_BINS; i += 1024) { sm.cnt[i] = 0u; sm.mass[i] = 0ull; }
       __syncthreads();
-#pragma unroll
-      for (int i = 0; i < CPT * 8; ++i) {
+FOR_ELEMS(i) {
         const float xi = X(i);
         if (xi > -INFINITY) {
           const int bn = sv3_bin(xi, mx);
           atomicAdd(&sm.cnt[bn], 1u);
           if (do_p) atomicAdd(&sm.mass[bn], sv3_mass(xi, mx));
         }
-      }
+      } END_ELEMS
       __syncthreads();
     }
     int bk = SV3_BINS;  // top-k boundary bin (bins > bk are cut)
@@ -264,14 +286,13 @@ __global__ __launch_bounds__(1024) void sample_v3_kernel(const bf16_t* __restric
       const int r = k - (int)sm.excl;  // 1-based rank of the k-th largest inside bin bk
       if (tid == 0) { sm.ncand = 0; sm.acc = 0; }
       __syncthreads();
-#pragma unroll
-      for (int i = 0; i < CPT * 8; ++i) {
+FOR_ELEMS(i) {
         const float xi = X(i);
         if (xi > -INFINITY && sv3_bin(xi, mx) == bk) {
           const int slot = atomicAdd(&sm.ncand, 1);
           if (slot < SV3_MAXC) { sm.cv[slot] = xi; sm.ci[slot] = (tid + (i >> 3) * 1024) * 8 + (i & 7); }
         }
-      }
+      } END_ELEMS
       __syncthreads();
       const int n = sm.ncand;
       if (n > SV3_MAXC) {  // pathological tie mass: keep the whole bin
@@ -315,14 +336,13 @@ __global__ __launch_bounds__(1024) void sample_v3_kernel(const bf16_t* __restric
       const unsigned long long above = sm.excl;
       if (tid == 0) sm.ncand = 0;
       __syncthreads();
-#pragma unroll
-      for (int i = 0; i < CPT * 8; ++i) {
+FOR_ELEMS(i) {
         const float xi = X(i);
         if (xi > -INFINITY && xi >= thr && sv3_bin(xi, mx) == bp) {
           const int slot = atomicAdd(&sm.ncand, 1);
           if (slot < SV3_MAXC) { sm.cv[slot] = xi; sm.ci[slot] = (tid + (i >> 3) * 1024) * 8 + (i & 7); }
         }
-      }
+      } END_ELEMS
       __syncthreads();
       const int n = sm.ncand;
       float tp = -INFINITY;
@@ -353,8 +373,7 @@ __global__ __launch_bounds__(1024) void sample_v3_kernel(const bf16_t* __restric
   const unsigned s0 = (unsigned)seed, s1 = (unsigned)(seed >> 32);
   float best = -INFINITY;
   int besti = 0x7fffffff;
-#pragma unroll
-  for (int i = 0; i < CPT * 8; ++i) {
+FOR_ELEMS(i) {
     const int idx = (tid + (i >> 3) * 1024) * 8 + (i & 7);
     float v = X(i);
     if (!(v > -INFINITY)) continue;
@@ -365,7 +384,7 @@ __global__ __launch_bounds__(1024) void sample_v3_kernel(const bf16_t* __restric
       v = v - __logf(-__logf(u));
     }
     if (v > best || (v == best && idx < besti)) { best = v; besti = idx; }
-  }
+  } END_ELEMS
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float ob = __shfl_xor(best, o, 64);
@@ -385,20 +404,27 @@ __global__ __launch_bounds__(1024) void sample_v3_kernel(const bf16_t* __restric
     if (out2) out2[b] = bi;
   }
 #undef X
+#undef CHUNK
+#undef FOR_ELEMS
+#undef END_ELEMS
 }
 
 void launch_sample(const void* logits, int64_t ld, bool fp32_logits, int B, int V, const void* temperature,
                    const void* top_k, const void* top_p, const void* seeds, void* out, void* out2, hipStream_t st) {
   if (B == 0) return;
   const int chunks = (V + 7) / 8;
-  if (!fp32_logits && ld % 8 == 0 && (uintptr_t)logits % 16 == 0 && chunks <= 8 * 1024) {
-#define SV3(CPT_)                                                                                                  \
-  sample_v3_kernel<CPT_><<<B, 1024, 0, st>>>((const bf16_t*)logits, ld, V, (const float*)temperature,             \
-                                             (const int*)top_k, (const float*)top_p, (const int64_t*)seeds,       \
-                                             (int64_t*)out, (int64_t*)out2)
-    if (chunks <= 2048) SV3(2);
-    else if (chunks <= 4096) SV3(4);
-    else SV3(8);
+  if (!fp32_logits && ld % 8 == 0 && (uintptr_t)logits % 16 == 0 && chunks <= SV3_LROW_CHUNKS) {
+#define SV3(CPT_, LROW_)                                                                                            \
+  sample_v3_kernel<CPT_, LROW_><<<B, 1024, 0, st>>>((const bf16_t*)logits, ld, V, (const float*)temperature,      \
+                                                    (const int*)top_k, (const float*)top_p, (const int64_t*)seeds, \
+                                                    (int64_t*)out, (int64_t*)out2)
+    static const bool lrow_small = [] {  // LLMSS_SAMPLER_LROW=1: LDS-resident rows at CPT 2 / 4 too
+      const char* e = getenv("LLMSS_SAMPLER_LROW");
+      return e && e[0] == '1';
+    }();
+    if (chunks <= 2048) { if (lrow_small) SV3(2, true); else SV3(2, false); }
+    else if (chunks <= 4096) { if (lrow_small) SV3(4, true); else SV3(4, false); }
+    else SV3(8, true);
 #undef SV3
     HIP_CHECK_LAUNCH();
     return;
