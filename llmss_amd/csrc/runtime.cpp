@@ -141,6 +141,15 @@ class Scheduler {
     if (finished || s.num_tokens - s.prompt_len >= s.max_new) finish(id);
   }
 
+  // Batched on_token for a whole decode step (one call instead of one per sequence).
+  void on_tokens(py::array_t<int64_t, py::array::c_style | py::array::forcecast> ids,
+                 py::array_t<bool, py::array::c_style | py::array::forcecast> finished) {
+    if (ids.size() != finished.size()) throw std::invalid_argument("Scheduler.on_tokens: length mismatch");
+    const int64_t* pi = ids.data();
+    const bool* pf = finished.data();
+    for (ssize_t i = 0; i < ids.size(); ++i) on_token(pi[i], pf[i]);
+  }
+
   void finish(int64_t id) {
     auto it = seqs_.find(id);
     if (it == seqs_.end()) return;
@@ -581,6 +590,7 @@ void register_runtime(py::module_& m) {
            py::arg("max_batched_tokens"), py::arg("max_model_len"))
       .def("add", &Scheduler::add)
       .def("on_token", &Scheduler::on_token)
+      .def("on_tokens", &Scheduler::on_tokens)
       .def("finish", &Scheduler::finish)
       .def("abort", &Scheduler::abort)
       .def("schedule", &Scheduler::schedule)

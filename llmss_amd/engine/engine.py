@@ -16,6 +16,7 @@ Here:
 """
 from __future__ import annotations
 
+import collections
 import math
 import os
 import time
@@ -31,7 +32,7 @@ from ..ops import hip as _hip_ops
 from ..utils.logging import get_logger
 from ..utils.tracing import PhaseTimer
 from ..utils.tracing import range as trace_range
-from .sampling import SamplingParams, step_seed
+from .sampling import SamplingParams, step_seeds
 
 log = get_logger(__name__)
 
@@ -74,33 +75,43 @@ class StepEvent:
 
 
 class _DecodeBuffers:
-    """Static device buffers (+ pinned host mirrors) feeding the captured decode graphs."""
+    """Static device buffers feeding the captured decode graphs, filled by ONE host-to-device copy
+    per step from one of two pinned staging sets: with decode steps pipelined (LLMEngine.step),
+    the host fills step t+1's set while step t's copy may still be queued, so a set is rewritten
+    only after the step that used it has been collected. Token ids come back through two pinned
+    output buffers for the same reason."""
 
     def __init__(self, max_b: int, max_blocks: int, device):
-        self.max_b, self.max_blocks = max_b, max_blocks
+        B, MB = max_b, max_blocks
+        self.max_b, self.max_blocks = B, MB
         pin = torch.cuda.is_available() and device.type == "cuda"
-        self.h_i64 = torch.zeros(4 * max_b, dtype=torch.int64, pin_memory=pin)  # ids|pos|slots|seeds
-        self.h_i32 = torch.zeros(2 * max_b + max_b * max_blocks, dtype=torch.int32, pin_memory=pin)  # ctx|topk|bt
-        self.h_f32 = torch.zeros(2 * max_b, dtype=torch.float32, pin_memory=pin)  # temp|topp
-        self.d_i64 = torch.zeros_like(self.h_i64, device=device)
-        self.d_i32 = torch.zeros_like(self.h_i32, device=device)
-        self.d_f32 = torch.zeros_like(self.h_f32, device=device)
+        self.o32 = 4 * B * 8  # ids|pos|slots|seeds (i64) | ctx|topk|bt (i32) | temp|topp (f32)
+        self.of32 = self.o32 + (2 * B + B * MB) * 4
+        nbytes = self.of32 + 2 * B * 4
+        self.h = [torch.zeros(nbytes, dtype=torch.uint8, pin_memory=pin) for _ in range(2)]
+        self.d = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+        self.d_i64 = self.d[:self.o32].view(torch.int64)
+        self.d_i32 = self.d[self.o32:self.of32].view(torch.int32)
+        self.d_f32 = self.d[self.of32:].view(torch.float32)
         self.out = torch.zeros(max_b, dtype=torch.int64, device=device)
-        self.h_out = torch.zeros(max_b, dtype=torch.int64, pin_memory=pin)
-        B = max_b
+        self.h_out = [torch.zeros(max_b, dtype=torch.int64, pin_memory=pin) for _ in range(2)]
         self.ids, self.pos, self.slots, self.seeds = (self.d_i64[i * B:(i + 1) * B] for i in range(4))
         self.ctx, self.topk = self.d_i32[:B], self.d_i32[B:2 * B]
         self.bt = self.d_i32[2 * B:].view(B, max_blocks)
         self.temp, self.topp = self.d_f32[:B], self.d_f32[B:]
 
-    def fill(self, b_pad, ids, pos, slots, seeds, ctx, topk, bt, temp, topp):
-        n = len(ids)
+    def fill(self, k, b_pad, ids, pos, slots, seeds, ctx, topk, bt, temp, topp):
+        """Stage one step's inputs in set k and copy them to the device. ``ids=None``: the input ids
+        are the previous step's sampled tokens, copied on the device (same rows)."""
+        n = len(pos)
         B, MB = self.max_b, self.max_blocks
-        hi = self.h_i64.numpy()
-        hi32 = self.h_i32.numpy()
-        hf = self.h_f32.numpy()
+        h = self.h[k]
+        hi = h[:self.o32].view(torch.int64).numpy()
+        hi32 = h[self.o32:self.of32].view(torch.int32).numpy()
+        hf = h[self.of32:].view(torch.float32).numpy()
         for j, arr in enumerate((ids, pos, slots, seeds)):
-            hi[j * B:j * B + n] = arr
+            if arr is not None:
+                hi[j * B:j * B + n] = arr
             hi[j * B + n:j * B + b_pad] = -1 if j == 2 else 0  # padded rows: no cache write
         hi32[:n] = ctx
         hi32[n:b_pad] = 0
@@ -113,9 +124,9 @@ class _DecodeBuffers:
         hf[n:b_pad] = 0
         hf[B:B + n] = topp
         hf[B + n:B + b_pad] = 1
-        self.d_i64.copy_(self.h_i64, non_blocking=True)
-        self.d_i32.copy_(self.h_i32, non_blocking=True)
-        self.d_f32.copy_(self.h_f32, non_blocking=True)
+        self.d.copy_(h, non_blocking=True)
+        if ids is None:
+            self.ids[:n].copy_(self.out[:n])
 
 
 class LLMEngine:
@@ -141,6 +152,12 @@ class LLMEngine:
                                          self.max_model_len)
         self.requests: Dict[int, Request] = {}
         self._next_id = 0
+        self._pending = collections.deque()  # launched GPU decode steps whose tokens are not yet processed
+        self._last_rec = None  # last collected decode step (per-request constants for reuse)
+        self._last_fins = None
+        self._stage = 0  # pinned staging set of the next launch
+        self.async_decode = os.environ.get("LLMSS_ASYNC_DECODE", "1") != "0"
+        self._host_prof = os.environ.get("LLMSS_HOST_PROFILE") == "1"  # host-side time per engine phase
         self.check_tokens = check_tokens if check_tokens is not None else os.environ.get("LLMSS_CHECK_TOKENS") == "1"
         self.stats = {"steps": 0, "prefill_steps": 0, "decode_steps": 0, "tokens": 0, "prefill_tokens": 0,
                       "preemptions": 0, "decode_time_s": 0.0, "prefill_time_s": 0.0}
@@ -234,7 +251,7 @@ class LLMEngine:
             r.finished, r.finish_reason = True, "abort"
 
     def has_unfinished(self) -> bool:
-        return self.sched.has_work()
+        return self.sched.has_work() or bool(self._pending)
 
     def pop_finished(self) -> List[Request]:
         done = [r for r in self.requests.values() if r.finished]
@@ -247,55 +264,108 @@ class LLMEngine:
         temp = np.array([r.params.k_temperature for r in reqs], dtype=np.float32)
         topk = np.array([r.params.k_top_k for r in reqs], dtype=np.int32)
         topp = np.array([r.params.k_top_p for r in reqs], dtype=np.float32)
-        seeds = np.array([step_seed(r.seed, len(r.output_ids)) for r in reqs], dtype=np.int64)
+        seeds = step_seeds(np.array([r.seed for r in reqs], dtype=np.uint64),
+                           np.array([len(r.output_ids) for r in reqs], dtype=np.int64))
         return temp, topk, topp, seeds
 
     def step(self) -> List[StepEvent]:
+        """One engine iteration; returns the token events it completed.
+
+        GPU decode steps are pipelined with the host. While the running set only advances (no
+        waiting prompt, no sequence entering a new KV block) the NEXT decode step is launched
+        before the current one is collected: its input ids are the current step's sampled
+        tokens, copied on the device, and its positions / slots / context lengths / Philox keys
+        are the current ones + 1, so the GPU never waits for Python bookkeeping. A sequence
+        that stops on EOS / a stop token in step t has computed one extra token in step t+1,
+        which is dropped. Otherwise (prefill admission, a block boundary, preemption) the
+        scheduler runs between the two steps as usual.
+        """
+        hp = self._host_prof
+        t_a = time.perf_counter() if hp else 0.0
+        done = None
+        if self._pending:
+            if self.async_decode and self.sched.num_waiting() == 0:
+                self._speculate(self._pending[-1])
+            done = self._collect_decode()
+            if self._pending:  # the next step is already in flight
+                if hp:
+                    self.stats["host_collect_apply_s"] = self.stats.get("host_collect_apply_s", 0.0) + \
+                        time.perf_counter() - t_a
+                return self._emit(*done)
+        t_b = time.perf_counter() if hp else 0.0
         with trace_range("schedule"):
             batch = self.sched.schedule()
-        if batch.kind == 0:
-            return []
-        for rid in batch.preempted.tolist():
-            self.stats["preemptions"] += 1
-        ids = batch.ids.tolist()
-        reqs = [self.requests[i] for i in ids]
-        t0 = time.perf_counter()
-        if batch.kind == 1:
-            with self.timer.phase("prefill"):
-                tokens = self._prefill(batch, reqs)
-            self.stats["prefill_steps"] += 1
-            self.stats["prefill_tokens"] += int(batch.query_lens.sum())
-        else:
-            with self.timer.phase("decode"):
-                tokens = self._decode(batch, reqs)
-            self.stats["decode_steps"] += 1
+        if hp:
+            t_c = time.perf_counter()
+            self.stats["host_collect_apply_s"] = self.stats.get("host_collect_apply_s", 0.0) + t_b - t_a
+            self.stats["host_schedule_s"] = self.stats.get("host_schedule_s", 0.0) + t_c - t_b
+        new_events: List[StepEvent] = []
+        if batch.kind != 0:
+            self.stats["preemptions"] += len(batch.preempted)
+            ids = batch.ids
+            reqs = [self.requests[i] for i in ids.tolist()]
+            if batch.kind == 1:
+                t0 = time.perf_counter()
+                with self.timer.phase("prefill"):
+                    tokens = self._prefill(batch, reqs)
+                self.stats["prefill_steps"] += 1
+                self.stats["prefill_tokens"] += int(batch.query_lens.sum())
+                self.stats["prefill_time_s"] += time.perf_counter() - t0
+                new_events = self._emit(*self._apply(ids, reqs, tokens))
+            elif self.is_gpu:
+                self._launch_decode(self._record_from_batch(batch, ids, reqs))
+            else:
+                t0 = time.perf_counter()
+                tokens = self._decode_cpu(batch, reqs)
+                self.stats["decode_steps"] += 1
+                self.stats["decode_time_s"] += time.perf_counter() - t0
+                new_events = self._emit(*self._apply(ids, reqs, tokens))
+        if hp:
+            t_d = time.perf_counter()
+            self.stats["host_launch_s"] = self.stats.get("host_launch_s", 0.0) + t_d - t_c
+        events = (self._emit(*done) if done is not None else []) + new_events
+        if hp:
+            self.stats["host_emit_s"] = self.stats.get("host_emit_s", 0.0) + time.perf_counter() - t_d
+        return events
+
+    def _apply(self, ids: np.ndarray, reqs: List[Request], tokens: List[int]):
+        """Critical-path bookkeeping of one step's tokens: append, stop checks, scheduler update."""
         if self.check_tokens and self.tp.is_real:
             allt = self.tp.all_gather_object(tokens)
             if any(t != tokens for t in allt):
                 raise RuntimeError(f"rank {self.tp.rank}: sampled tokens diverged across TP ranks: {allt}")
-        now = time.perf_counter()
-        self.stats["decode_time_s" if batch.kind == 2 else "prefill_time_s"] += now - t0
+        eos = self.eos
+        reasons = [""] * len(reqs)
+        fins = np.zeros(len(reqs), dtype=bool)
+        for i, (r, tok) in enumerate(zip(reqs, tokens)):
+            out = r.output_ids
+            out.append(tok)
+            p = r.params
+            if len(out) >= p.max_new_tokens:
+                reasons[i] = "length"
+            elif not p.ignore_eos and eos is not None and tok == eos:
+                reasons[i] = "eos"
+            elif p.stop_token_ids and tok in p.stop_token_ids:
+                reasons[i] = "stop"
+            else:
+                continue
+            fins[i] = True
+        self.sched.on_tokens(ids, fins)
+        self._last_fins = fins
         self.stats["steps"] += 1
+        return reqs, tokens, reasons, time.perf_counter()
+
+    def _emit(self, reqs, tokens, reasons, now) -> List[StepEvent]:
         events = []
-        for r, tok in zip(reqs, tokens):
-            r.output_ids.append(tok)
+        for r, tok, reason in zip(reqs, tokens, reasons):
             if not r.t_first:
                 r.t_first = now
             r.t_last = now
             r.token_times.append(now)
-            self.stats["tokens"] += 1
-            reason = ""
-            if len(r.output_ids) >= r.params.max_new_tokens:
-                reason = "length"
-            elif not r.params.ignore_eos and self.eos is not None and tok == self.eos:
-                reason = "eos"
-            elif tok in r.params.stop_token_ids:
-                reason = "stop"
-            fin = bool(reason)
-            self.sched.on_token(r.id, fin)
-            if fin:
+            if reason:
                 r.finished, r.finish_reason = True, reason
-            events.append(StepEvent(r.id, tok, fin, reason))
+            events.append(StepEvent(r.id, tok, bool(reason), reason))
+        self.stats["tokens"] += len(events)
         return events
 
     def _prefill(self, batch, reqs: List[Request]) -> List[int]:
@@ -328,27 +398,111 @@ class LLMEngine:
         _hip_ops.sample(logits, buf.temp[:b], buf.topk[:b], buf.topp[:b], buf.seeds[:b],
                         vocab=min(self.cfg.vocab_size, logits.shape[-1]), out=buf.out[:b])
 
-    def _decode(self, batch, reqs: List[Request]) -> List[int]:
-        n = len(reqs)
+    def _decode_cpu(self, batch, reqs: List[Request]) -> List[int]:
         ids = np.array([r.last_id for r in reqs], dtype=np.int64)
         temp, topk, topp, seeds = self._sampling_arrays(reqs)
-        if not self.is_gpu:
-            dev = self.device
-            inp = StepInput(kind="decode", input_ids=torch.from_numpy(ids), positions=torch.from_numpy(batch.positions),
-                            slots=torch.from_numpy(batch.slots),
-                            block_tables=torch.from_numpy(batch.block_table.astype(np.int32)),
-                            ctx_lens=torch.from_numpy(batch.ctx_lens.astype(np.int32)), max_ctx=self.max_model_len)
-            logits = self.model(inp, self.kv)
-            return ops.sample(logits, temp, topk, topp, seeds, vocab=min(self.cfg.vocab_size, logits.shape[-1])).tolist()
-        b = next(x for x in self.buckets if x >= n)
-        self.buf.fill(b, ids, batch.positions, batch.slots, seeds, batch.ctx_lens, topk, batch.block_table, temp, topp)
-        if self.use_graphs and b in self.graphs:
-            self.graphs[b].replay()
+        inp = StepInput(kind="decode", input_ids=torch.from_numpy(ids), positions=torch.from_numpy(batch.positions),
+                        slots=torch.from_numpy(batch.slots),
+                        block_tables=torch.from_numpy(batch.block_table.astype(np.int32)),
+                        ctx_lens=torch.from_numpy(batch.ctx_lens.astype(np.int32)), max_ctx=self.max_model_len)
+        logits = self.model(inp, self.kv)
+        return ops.sample(logits, temp, topk, topp, seeds, vocab=min(self.cfg.vocab_size, logits.shape[-1])).tolist()
+
+    # ------------------------------------------------------------------ pipelined GPU decode
+    def _record_from_batch(self, batch, ids: np.ndarray, reqs: List[Request]) -> dict:
+        """Decode step record for a scheduled batch. Per-request constants are reused from the last
+        collected step when the running set is unchanged (every member then got one token)."""
+        last = self._last_rec
+        if last is not None and last["ids"].shape == ids.shape and np.array_equal(last["ids"], ids) \
+                and last["keep"].all():
+            c = {k: last[k] for k in ("temp", "topk", "topp", "seed", "maxnew")}
+            c["nout"] = last["nout"] + 1
+            c["last"] = last["tokens"]
         else:
-            self._decode_forward(b, self.buf)
-        self.buf.h_out[:n].copy_(self.buf.out[:n], non_blocking=True)
-        torch.cuda.current_stream().synchronize()
-        return self.buf.h_out[:n].tolist()
+            c = {"temp": np.array([r.params.k_temperature for r in reqs], dtype=np.float32),
+                 "topk": np.array([r.params.k_top_k for r in reqs], dtype=np.int32),
+                 "topp": np.array([r.params.k_top_p for r in reqs], dtype=np.float32),
+                 "seed": np.array([r.seed for r in reqs], dtype=np.uint64),
+                 "maxnew": np.array([r.params.max_new_tokens for r in reqs], dtype=np.int64),
+                 "nout": np.array([len(r.output_ids) for r in reqs], dtype=np.int64),
+                 "last": np.array([r.last_id for r in reqs], dtype=np.int64)}
+        c.update(ids=ids, reqs=reqs, n=len(reqs), pos=batch.positions, ctx=batch.ctx_lens.astype(np.int32),
+                 slots=batch.slots, bt=batch.block_table, keep=np.ones(len(reqs), dtype=bool))
+        return c
+
+    def _launch_decode(self, rec: dict, device_ids: bool = False):
+        n = rec["n"]
+        rec["t0"] = time.perf_counter()
+        b = next(x for x in self.buckets if x >= n)
+        k = self._stage
+        self._stage ^= 1
+        buf = self.buf
+        with self.timer.phase("decode"):
+            buf.fill(k, b, None if device_ids else rec.pop("last"), rec["pos"], rec["slots"],
+                     step_seeds(rec["seed"], rec["nout"]), rec["ctx"], rec["topk"], rec["bt"], rec["temp"],
+                     rec["topp"])
+            if self.use_graphs and b in self.graphs:
+                self.graphs[b].replay()
+            else:
+                self._decode_forward(b, buf)
+            buf.h_out[k][:n].copy_(buf.out[:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        rec.update(k=k, ev=ev)
+        self._pending.append(rec)
+
+    def _speculate(self, cur: dict):
+        """Launch the step after ``cur`` (still in flight) if it needs no scheduler decision."""
+        alive = cur["keep"] & (cur["nout"] + 1 < cur["maxnew"])
+        if not alive.any():
+            return
+        nxt_pos = cur["pos"] + 1
+        if (nxt_pos[alive] % self.block_size == 0).any():  # a sequence enters a new KV block
+            return
+        dead = ~alive
+        rec = {k: cur[k] for k in ("ids", "reqs", "n", "temp", "topk", "topp", "seed", "maxnew", "bt")}
+        rec["pos"] = nxt_pos
+        rec["ctx"] = np.where(alive, cur["ctx"] + 1, 0).astype(np.int32)
+        rec["slots"] = np.where(alive, cur["slots"] + 1, -1)
+        rec["nout"] = cur["nout"] + 1
+        rec["keep"] = alive
+        if dead.any():
+            rec["topk"] = np.where(alive, cur["topk"], 1).astype(np.int32)
+        self._launch_decode(rec, device_ids=True)
+
+    def _collect_decode(self):
+        rec = self._pending.popleft()
+        ev = rec["ev"]
+        if self._host_prof:
+            t = time.perf_counter()
+            ev.synchronize()
+            self.stats["host_gpu_wait_s"] = self.stats.get("host_gpu_wait_s", 0.0) + time.perf_counter() - t
+        else:
+            ev.synchronize()
+        toks = self.buf.h_out[rec["k"]][:rec["n"]].numpy().copy()
+        reqs = rec["reqs"]
+        keep = rec["keep"]
+        gone = [i for i in np.flatnonzero(keep) if reqs[i].finished]  # aborted while in flight
+        if gone:
+            keep = keep.copy()
+            keep[gone] = False
+            rec["keep"] = keep
+        rows = np.flatnonzero(keep)
+        ids = rec["ids"][rows]
+        sel = [reqs[i] for i in rows]
+        tokens = toks[rows].tolist()
+        self.stats["decode_steps"] += 1
+        self.stats["decode_time_s"] += time.perf_counter() - rec["t0"]
+        out = self._apply(ids, sel, tokens)
+        fins = self._last_fins
+        nxt = self._pending[0] if self._pending else None
+        if nxt is not None:  # the speculated successor drops rows that stopped (eos / stop / abort) here
+            nk = nxt["keep"] & keep
+            nk[rows[fins]] = False
+            nxt["keep"] = nk
+        rec["tokens"] = toks
+        self._last_rec = rec
+        return out
 
     def phase_summary(self) -> Dict[str, Dict[str, float]]:
         """Per-phase device time (LLMSS_TIMING=1) - {"prefill": {...}, "decode": {...}}."""

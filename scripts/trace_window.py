@@ -13,11 +13,17 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--skip-frac", type=float, default=0.7)
     ap.add_argument("--span-us", type=float, default=20000)
+    ap.add_argument("--anchor", default="", help="start the window at the end of the middle occurrence of "
+                                               "this kernel name (e.g. sample_v3: between two decode steps)")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     t_first, t_last = int(rows[0]["Start_Timestamp"]), int(rows[-1]["End_Timestamp"])
     t0 = t_first + a.skip_frac * (t_last - t_first)
+    if a.anchor:
+        hits = [r for r in rows if a.anchor in r["Kernel_Name"]]
+        if hits:
+            t0 = int(hits[int(len(hits) * a.skip_frac)]["End_Timestamp"]) - 1000
     t1 = t0 + a.span_us * 1e3
     keys = [k for k in ("Queue_Id", "Stream_Id") if k in rows[0]]
     with open(a.out, "w", newline="") as f:

@@ -249,3 +249,46 @@ def test_decode_microbatch_overlap_in_graphs():
         del e_graph
         e_eager = LLMEngine(m, max_num_seqs=8, block_size=16, use_graphs=False, autotune=False)
         assert e_eager.generate(prompts, sp) == out_g
+
+
+def _async_engine_run(m, prompts, sps, async_decode, eos=None, abort_after=None):
+    # one graph bucket: every decode step runs M = 8 rows, so a row's numerics never depend on how
+    # many other rows are live (sync and async modes shrink the batch at different steps)
+    eng = LLMEngine(m, max_num_seqs=8, block_size=4, use_graphs=True, autotune=False, eos_token_id=eos,
+                    graph_buckets=[8])
+    eng.async_decode = async_decode
+    rids = [eng.add_request(p, sp) for p, sp in zip(prompts, sps)]
+    n = 0
+    while eng.has_unfinished():
+        eng.step()
+        n += 1
+        if abort_after is not None and n == abort_after:
+            eng.abort(rids[0])
+    out = {r.id: (list(r.output_ids), r.finish_reason) for r in eng.pop_finished()}
+    return [out[r] for r in rids]
+
+
+def test_async_decode_matches_sync():
+    """Pipelined decode (next step launched before the current one is collected, device-side input
+    ids, dropped rows for EOS stops) produces exactly the tokens of the synchronous engine: staggered
+    max_new_tokens, KV block boundaries every 4 tokens, sampling, EOS stops and an abort."""
+    cfg = get_preset("tiny-llama", hidden_size=256, num_heads=4, num_kv_heads=2, head_dim=64, rotary_dim=64,
+                     intermediate_size=512, max_position_embeddings=256, vocab_size=64)
+    m = DecoderLM(cfg, random_weights(cfg, device="cuda", dtype=torch.bfloat16, seed=5, std=0.08))
+    g = torch.Generator().manual_seed(0)
+    prompts = [torch.randint(0, 64, (n,), generator=g).tolist() for n in (3, 9, 5, 14, 6, 2, 11, 7)]
+    sps = [SamplingParams(max_new_tokens=4 + 3 * i, temperature=0.9, top_k=20, top_p=0.9, seed=100 + i)
+           for i in range(len(prompts))]
+    ref = _async_engine_run(m, prompts, sps, False)
+    assert _async_engine_run(m, prompts, sps, True) == ref
+    # EOS: the most frequent generated token stops sequences mid-stream
+    toks = [t for o, _ in ref for t in o]
+    eos = max(set(toks), key=toks.count)
+    ref_e = _async_engine_run(m, prompts, sps, False, eos=eos)
+    assert any(r == "eos" for _, r in ref_e)
+    assert _async_engine_run(m, prompts, sps, True, eos=eos) == ref_e
+    # abort mid-run: every other request is unaffected
+    a = _async_engine_run(m, prompts, sps, False, abort_after=4)
+    b = _async_engine_run(m, prompts, sps, True, abort_after=4)
+    assert a[0][1] == b[0][1] == "abort"
+    assert a[1:] == b[1:] == ref[1:]

@@ -87,3 +87,36 @@ def test_safetensors_reader(native, tmp_path):
     assert torch.equal(r.cols("b.c", 1, 3), t["b.c"][:, 1:3])
     assert torch.equal(r.cols("h", 3, 9), t["h"][:, 3:9])
     assert r.shape("b.c") == [2, 3, 4]
+
+
+def test_step_seeds_vectorised_matches_scalar():
+    import random
+
+    import numpy as np
+
+    from llmss_amd.engine.sampling import step_seed, step_seeds
+
+    rng = random.Random(3)
+    seeds = [rng.getrandbits(64) for _ in range(500)] + [0, (1 << 64) - 1]
+    steps = [rng.randint(0, 10_000) for _ in range(500)] + [0, 7]
+    got = step_seeds(np.array(seeds, dtype=np.uint64), np.array(steps, dtype=np.int64)).tolist()
+    assert got == [step_seed(s, t) for s, t in zip(seeds, steps)]
+
+
+def test_scheduler_on_tokens_batched():
+    import numpy as np
+
+    from llmss_amd import _native
+
+    S = _native().Scheduler(64, 4, 8, 64, 32)
+    for i in range(3):
+        S.add(i, 5, 3)
+    b = S.schedule()
+    assert b.kind == 1
+    S.on_tokens(b.ids, np.array([False, True, False]))  # request 1 stops early (eos)
+    b = S.schedule()
+    assert b.kind == 2 and b.ids.tolist() == [0, 2]
+    S.on_tokens(b.ids, np.zeros(2, dtype=bool))
+    b = S.schedule()
+    S.on_tokens(b.ids, np.zeros(2, dtype=bool))  # third token: max_new reached -> finished
+    assert not S.has_work()
