@@ -16,14 +16,17 @@
 // torch.cat (gptj_modeling.py:229-236); weights via safetensors' Python safe_open
 // (utils/weights.py:9-115).
 #include <fcntl.h>
+#ifndef LLMSS_HOST_TEST  // tests/native builds this file alone (no Python) under ASan/UBSan
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#endif
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdint>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -33,7 +36,9 @@
 #include <unordered_map>
 #include <vector>
 
+#ifndef LLMSS_HOST_TEST
 namespace py = pybind11;
+#endif
 
 // ============================================================================ BlockAllocator
 class BlockAllocator {
@@ -142,12 +147,8 @@ class Scheduler {
   }
 
   // Batched on_token for a whole decode step (one call instead of one per sequence).
-  void on_tokens(py::array_t<int64_t, py::array::c_style | py::array::forcecast> ids,
-                 py::array_t<bool, py::array::c_style | py::array::forcecast> finished) {
-    if (ids.size() != finished.size()) throw std::invalid_argument("Scheduler.on_tokens: length mismatch");
-    const int64_t* pi = ids.data();
-    const bool* pf = finished.data();
-    for (ssize_t i = 0; i < ids.size(); ++i) on_token(pi[i], pf[i]);
+  void on_tokens(const int64_t* ids, const bool* finished, int64_t n) {
+    for (int64_t i = 0; i < n; ++i) on_token(ids[i], finished[i]);
   }
 
   void finish(int64_t id) {
@@ -377,12 +378,17 @@ class JsonCursor {
   size_t i_ = 0;
 };
 
-static int dtype_size(const std::string& d) {
+static int dtype_size_or0(const std::string& d) {
   if (d == "F64" || d == "I64" || d == "U64") return 8;
   if (d == "F32" || d == "I32" || d == "U32") return 4;
   if (d == "F16" || d == "BF16" || d == "I16" || d == "U16") return 2;
   if (d == "I8" || d == "U8" || d == "BOOL" || d == "F8_E4M3" || d == "F8_E5M2") return 1;
-  throw std::runtime_error("safetensors: unsupported dtype " + d);
+  return 0;
+}
+static int dtype_size(const std::string& d) {
+  const int n = dtype_size_or0(d);
+  if (!n) throw std::runtime_error("safetensors: unsupported dtype " + d);
+  return n;
 }
 
 class SafetensorsFile {
@@ -412,10 +418,7 @@ class SafetensorsFile {
     for (auto& kv : tensors_) k.push_back(kv.first);
     return k;
   }
-  py::tuple info(const std::string& name) const {
-    const auto& t = at(name);
-    return py::make_tuple(t.dtype, t.shape, t.begin, t.end);
-  }
+  const TensorInfo& info(const std::string& name) const { return at(name); }
   std::map<std::string, std::string> metadata() const { return meta_; }
 
   // Copy rows [start, stop) along `dim` (0 or 1) of tensor `name` into dst (contiguous).
@@ -527,8 +530,16 @@ class SafetensorsFile {
           break;
         }
         c.expect('}');
-        if (t.end < t.begin || (int64_t)(data_ - map_) + t.end > size_)
+        if (t.begin < 0 || t.end < t.begin || (int64_t)(data_ - map_) + t.end > size_)
           throw std::runtime_error("safetensors: tensor " + key + " out of file bounds");
+        int64_t numel = 1;
+        for (int64_t d : t.shape) {
+          if (d < 0 || (d > 0 && numel > INT64_MAX / d)) throw std::runtime_error("safetensors: bad shape of " + key);
+          numel *= d;
+        }
+        const int es = dtype_size_or0(t.dtype);  // unknown dtypes fail on access instead
+        if (es && (numel > INT64_MAX / 8 || numel * es != t.end - t.begin))  // copy_slice trusts shape x dtype
+          throw std::runtime_error("safetensors: shape/dtype of " + key + " disagree with its data_offsets");
         tensors_[key] = t;
       }
       if (c.peek() == ',') { c.advance(); continue; }
@@ -547,6 +558,7 @@ class SafetensorsFile {
 };
 
 // ============================================================================ bindings
+#ifndef LLMSS_HOST_TEST
 template <typename T>
 static py::array_t<T> to_np(const std::vector<T>& v) {
   py::array_t<T> a(v.size());
@@ -590,7 +602,12 @@ void register_runtime(py::module_& m) {
            py::arg("max_batched_tokens"), py::arg("max_model_len"))
       .def("add", &Scheduler::add)
       .def("on_token", &Scheduler::on_token)
-      .def("on_tokens", &Scheduler::on_tokens)
+      .def("on_tokens",
+           [](Scheduler& sc, py::array_t<int64_t, py::array::c_style | py::array::forcecast> ids,
+              py::array_t<bool, py::array::c_style | py::array::forcecast> fin) {
+             if (ids.size() != fin.size()) throw std::invalid_argument("Scheduler.on_tokens: length mismatch");
+             sc.on_tokens(ids.data(), fin.data(), ids.size());
+           })
       .def("finish", &Scheduler::finish)
       .def("abort", &Scheduler::abort)
       .def("schedule", &Scheduler::schedule)
@@ -606,9 +623,14 @@ void register_runtime(py::module_& m) {
   py::class_<SafetensorsFile>(m, "SafetensorsFile")
       .def(py::init<const std::string&>())
       .def("keys", &SafetensorsFile::keys)
-      .def("info", &SafetensorsFile::info)
+      .def("info",
+           [](const SafetensorsFile& f, const std::string& name) {
+             const auto& t = f.info(name);
+             return py::make_tuple(t.dtype, t.shape, t.begin, t.end);
+           })
       .def("metadata", &SafetensorsFile::metadata)
       .def("nbytes", &SafetensorsFile::nbytes)
       .def("copy_slice", &SafetensorsFile::copy_slice, py::arg("name"), py::arg("dim"), py::arg("start"),
            py::arg("stop"), py::arg("dst"), py::arg("threads") = 8);
 }
+#endif  // LLMSS_HOST_TEST

@@ -1,0 +1,25 @@
+"""The native host runtime (csrc/runtime.cpp: block allocator, scheduler, safetensors reader)
+compiled alone under AddressSanitizer + UndefinedBehaviorSanitizer and driven by a C++ test
+(tests/native/runtime_host_test.cpp) - SURVEY 5.2's host-code sanitizer run. CPU only."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_runtime_under_asan_ubsan(tmp_path):
+    exe = str(tmp_path / "runtime_host_test")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+           "-fno-sanitize-recover=undefined", os.path.join(HERE, "native", "runtime_host_test.cpp"), "-o", exe,
+           "-pthread"]
+    subprocess.run(cmd, check=True, capture_output=True, timeout=300)
+    # verify_asan_link_order=0: the environment may preload other libraries ahead of the ASan runtime
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ALL OK" in r.stdout
