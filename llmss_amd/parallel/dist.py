@@ -75,9 +75,25 @@ class TPGroup:
             return
         torch.cuda._sleep(max(1, int(us * self._cycles_per_us)))
 
+    @property
+    def host_staged(self) -> bool:
+        """gloo group: device tensors go through host copies (gloo has no device all-gather).
+
+        Only the multi-rank-on-one-GPU tests use this (several TP ranks sharing the development
+        box's single MI355X); the RCCL data plane never stages.
+        """
+        st = getattr(self, "_host_staged", None)
+        if st is None:
+            st = self._host_staged = self.is_real and dist.get_backend(self.group) == "gloo"
+        return st
+
     # ------------------------------------------------------------ data plane
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
-        if self.is_real:
+        if self.is_real and t.is_cuda and self.host_staged:
+            h = t.cpu()
+            dist.all_reduce(h, group=self.group)
+            t.copy_(h)
+        elif self.is_real:
             dist.all_reduce(t, group=self.group)
         elif self.sim_comm is not None and t.is_cuda:
             self._sim_wait(t.numel() * t.element_size())
@@ -90,13 +106,23 @@ class TPGroup:
                 self._sim_wait(self.size * t.numel() * t.element_size())
             return t
         t = t.contiguous()
-        out = torch.empty((self.size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t, group=self.group)
+        if t.is_cuda and self.host_staged:
+            h = t.cpu()
+            out = torch.empty((self.size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype)
+            dist.all_gather_into_tensor(out, h, group=self.group)
+            out = out.to(t.device)
+        else:
+            out = torch.empty((self.size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            dist.all_gather_into_tensor(out, t, group=self.group)
         out = out.view((self.size,) + tuple(t.shape))
         return out.movedim(0, -2).reshape(*t.shape[:-1], self.size * t.shape[-1])
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
-        if self.is_real:
+        if self.is_real and t.is_cuda and self.host_staged:
+            h = t.cpu()
+            dist.broadcast(h, src=src, group=self.group)
+            t.copy_(h)
+        elif self.is_real:
             dist.broadcast(t, src=src, group=self.group)
         return t
 

@@ -1,0 +1,109 @@
+"""Multi-rank tensor parallelism through the native GPU path on the one-GPU development box.
+
+Two TP ranks share ``cuda:0`` over a gloo group (device tensors staged through the host,
+``TPGroup.host_staged``): sharded loading, column/row/vocab-parallel GEMMs, the GPT-J single
+all-reduce, the padded vocab-parallel head gather and the cross-rank sampling contract
+(``check_tokens``: every rank must sample the same token) all run on the HIP kernels. RCCL itself
+needs one GPU per rank and is exercised by the driver's multi-GPU bench; the CPU twin of this test
+is ``test_tp_gloo.py``.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _save(name, path, vocab=1001):
+    from transformers import GPTJConfig, GPTJForCausalLM, LlamaConfig, LlamaForCausalLM
+
+    torch.manual_seed(0)
+    if name == "llama":  # GQA 4 q / 2 kv heads of D=64 -> 1 kv head per rank at TP=2
+        m = LlamaForCausalLM(LlamaConfig(hidden_size=256, num_hidden_layers=2, num_attention_heads=4,
+                                         num_key_value_heads=2, intermediate_size=512, vocab_size=vocab,
+                                         max_position_embeddings=256, initializer_range=0.1,
+                                         bos_token_id=vocab - 1, eos_token_id=vocab - 1))
+    else:  # GPT-J: parallel block (one all-reduce per layer), D=256 with a 64-wide interleaved rotary
+        m = GPTJForCausalLM(GPTJConfig(n_embd=512, n_layer=2, n_head=2, n_positions=256, vocab_size=vocab,
+                                       rotary_dim=64, initializer_range=0.1, bos_token_id=vocab - 1,
+                                       eos_token_id=vocab - 1))
+    m.eval().save_pretrained(path, safe_serialization=True)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _prompts():
+    return [[(13 * i + 7 * j) % 1000 for j in range(9 + 11 * i)] for i in range(4)]
+
+
+def _greedy():
+    from llmss_amd.engine import SamplingParams
+
+    return SamplingParams(max_new_tokens=12, is_greedy=True, ignore_eos=True)
+
+
+def _sampled():
+    from llmss_amd.engine import SamplingParams
+
+    return [SamplingParams(max_new_tokens=12, temperature=0.9, top_k=40, top_p=0.9, seed=3 + i, ignore_eos=True)
+            for i in range(4)]
+
+
+def _worker(rank, world, port, ckpt, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    from llmss_amd.engine import LLMEngine, build_model
+    from llmss_amd.ops import hip
+    from llmss_amd.parallel.dist import initialize_distributed
+
+    tp, r, _ = initialize_distributed(backend="gloo")
+    assert tp.host_staged
+    m = build_model(ckpt, tp, "bf16", torch.device("cuda", 0))
+    eng = LLMEngine(m, max_num_seqs=4, block_size=16, use_graphs=False, check_tokens=True)
+    g = eng.generate(_prompts(), _greedy())
+    s = eng.generate(_prompts(), _sampled())
+    if r == 0:
+        q.put((g, s, hip.lib().__file__))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["llama", "gptj"])
+def test_tp2_native_matches_tp1(tmp_path, name):
+    from llmss_amd.engine import LLMEngine, build_model
+
+    d = str(tmp_path / name)
+    _save(name, d)
+    ref = LLMEngine(build_model(d, None, "bf16", torch.device("cuda", 0)), max_num_seqs=4, block_size=16,
+                    use_graphs=False)
+    ref_g = ref.generate(_prompts(), _greedy())
+    del ref
+    torch.cuda.empty_cache()
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, d, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    g, s, lib = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert "llmss_amd" in lib
+    # bf16 partial sums are added in a different order at TP=2: allow rare argmax flips (and the
+    # divergence that follows one), but the continuations must essentially agree
+    first = sum(a[0] == b[0] for a, b in zip(g, ref_g))
+    agree = sum(x == y for a, b in zip(g, ref_g) for x, y in zip(a, b)) / sum(len(a) for a in ref_g)
+    assert first >= 3 and agree > 0.6, (first, agree, g, ref_g)
+    assert all(len(x) == 12 for x in s)
