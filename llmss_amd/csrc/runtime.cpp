@@ -394,25 +394,17 @@ static int dtype_size(const std::string& d) {
 class SafetensorsFile {
  public:
   explicit SafetensorsFile(const std::string& path) : path_(path) {
-    fd_ = ::open(path.c_str(), O_RDONLY);
-    if (fd_ < 0) throw std::runtime_error("safetensors: cannot open " + path);
-    struct stat st;
-    fstat(fd_, &st);
-    size_ = st.st_size;
-    if (size_ < 8) throw std::runtime_error("safetensors: file too small");
-    map_ = (const char*)mmap(nullptr, size_, PROT_READ, MAP_PRIVATE, fd_, 0);
-    if (map_ == MAP_FAILED) throw std::runtime_error("safetensors: mmap failed");
-    uint64_t hlen;
-    std::memcpy(&hlen, map_, 8);
-    if (8 + hlen > (uint64_t)size_) throw std::runtime_error("safetensors: bad header length");
-    data_ = map_ + 8 + hlen;
-    std::string header(map_ + 8, hlen);
-    parse(header);
+    // the destructor does not run when the constructor throws: release the fd and the mapping here
+    try {
+      open_and_parse(path);
+    } catch (...) {
+      release();
+      throw;
+    }
   }
-  ~SafetensorsFile() {
-    if (map_ && map_ != MAP_FAILED) munmap((void*)map_, size_);
-    if (fd_ >= 0) ::close(fd_);
-  }
+  ~SafetensorsFile() { release(); }
+  SafetensorsFile(const SafetensorsFile&) = delete;
+  SafetensorsFile& operator=(const SafetensorsFile&) = delete;
   std::vector<std::string> keys() const {
     std::vector<std::string> k;
     for (auto& kv : tensors_) k.push_back(kv.first);
@@ -458,6 +450,29 @@ class SafetensorsFile {
   }
 
  private:
+  void open_and_parse(const std::string& path) {
+    fd_ = ::open(path.c_str(), O_RDONLY);
+    if (fd_ < 0) throw std::runtime_error("safetensors: cannot open " + path);
+    struct stat st;
+    if (fstat(fd_, &st) != 0) throw std::runtime_error("safetensors: cannot stat " + path);
+    size_ = st.st_size;
+    if (size_ < 8) throw std::runtime_error("safetensors: file too small");
+    const void* m = mmap(nullptr, size_, PROT_READ, MAP_PRIVATE, fd_, 0);
+    if (m == MAP_FAILED) throw std::runtime_error("safetensors: mmap failed");
+    map_ = (const char*)m;
+    uint64_t hlen;
+    std::memcpy(&hlen, map_, 8);
+    if (hlen > (uint64_t)size_ - 8) throw std::runtime_error("safetensors: bad header length");  // no 8 + hlen wrap
+    data_ = map_ + 8 + hlen;
+    std::string header(map_ + 8, hlen);
+    parse(header);
+  }
+  void release() {
+    if (map_) munmap((void*)map_, size_);
+    map_ = nullptr;
+    if (fd_ >= 0) ::close(fd_);
+    fd_ = -1;
+  }
   static void parallel_copy(char* dst, const char* src, int64_t n, int threads) {
     const int64_t chunk = 8 << 20;
     if (threads <= 1 || n < 2 * chunk) {

@@ -146,7 +146,10 @@ class LLMEngine:
         self.max_batched_tokens = max(max_batched_tokens, self.max_model_len)
         self.eos = eos_token_id if eos_token_id is not None else self.cfg.eos_token_id
         self.max_blocks = math.ceil(self.max_model_len / block_size)
-        self.num_blocks = num_blocks or self._auto_blocks(kv_fraction)
+        # every rank runs its own scheduler on the same request stream, so the KV pool (admission,
+        # preemption) must be identical everywhere: each rank sizes it from its own free HBM, then all
+        # take the minimum
+        self.num_blocks = self.tp.all_reduce_int(num_blocks or self._auto_blocks(kv_fraction), "min")
         self.kv = model.allocate_kv_cache(self.num_blocks, block_size)
         self.sched = _native().Scheduler(self.num_blocks, block_size, max_num_seqs, self.max_batched_tokens,
                                          self.max_model_len)
@@ -163,11 +166,14 @@ class LLMEngine:
                       "preemptions": 0, "decode_time_s": 0.0, "prefill_time_s": 0.0}
         self.timer = PhaseTimer()  # LLMSS_TIMING=1: HIP-event device time per phase; LLMSS_ROCTX=1: roctx ranges
         self.use_graphs = self.is_gpu if use_graphs is None else (use_graphs and self.is_gpu)
+        if self.tp.is_real and self.tp.host_staged:  # gloo-staged device collectives cannot be captured
+            self.use_graphs = False
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.buckets = sorted(set(graph_buckets or self._default_buckets()))
         self.buckets = [b for b in self.buckets if b <= max_num_seqs] or [max_num_seqs]
         if self.buckets[-1] < max_num_seqs:
             self.buckets.append(max_num_seqs)
+        self.tp.check_consistent("LLMEngine", self.fingerprint())
         self.buf = _DecodeBuffers(self.buckets[-1], self.max_blocks, self.device) if self.is_gpu else None
         if self.is_gpu:
             _hip_ops.reserve_workspace(self.device, 64 << 20)
@@ -194,6 +200,18 @@ class LLMEngine:
                 self.use_graphs = False
 
     # -------------------------------------------------------------------------- sizing
+    def fingerprint(self) -> dict:
+        """Everything that steers scheduling or the collective sequence; must match on all TP ranks."""
+        cfg = self.cfg
+        return {"model": repr(sorted((k, str(v)) for k, v in cfg.__dict__.items())),
+                "dtype": str(self.model.dtype), "tp": self.tp.size, "block_size": self.block_size,
+                "num_blocks": self.num_blocks, "max_model_len": self.max_model_len,
+                "max_num_seqs": self.max_num_seqs, "max_batched_tokens": self.max_batched_tokens,
+                "buckets": list(self.buckets), "graphs": bool(self.use_graphs),
+                "async_decode": self.async_decode, "eos": self.eos,
+                "overlap_rows": self.model.overlap_rows, "tbo_min": self.model.tbo_min,
+                "fp8": any(L.qkv.w_scale is not None for L in self.model.w.layers[:1])}
+
     def _default_buckets(self):
         out, b = [], 1
         while b < self.max_num_seqs:

@@ -195,9 +195,13 @@ def random_weights(cfg: ModelConfig, tp: int = 1, rank: int = 0, device="cpu", d
     gen_dev = torch.device(device)
     g = torch.Generator(device=gen_dev)
     g.manual_seed(seed * 1000 + rank)
+    # replicated tensors (embeddings, norm biases, rank-0 row-parallel biases, the final norm) come
+    # from a rank-independent stream: every rank must hold the same copy, as after a checkpoint load
+    g_rep = torch.Generator(device=gen_dev)
+    g_rep.manual_seed(seed * 1000 + 999)
 
-    def rn(*shape, s=std):
-        return (torch.randn(*shape, generator=g, device=gen_dev, dtype=torch.float32) * s).to(dtype)
+    def rn(*shape, s=std, rep=False):
+        return (torch.randn(*shape, generator=g_rep if rep else g, device=gen_dev, dtype=torch.float32) * s).to(dtype)
 
     def ones(n):
         return torch.ones(n, device=gen_dev, dtype=dtype)
@@ -206,15 +210,17 @@ def random_weights(cfg: ModelConfig, tp: int = 1, rank: int = 0, device="cpu", d
     qkv_n = (plan.nh_l + 2 * plan.nkv_l) * D
     for _ in range(cfg.num_layers):
         d = dict(
-            ln1_w=ones(H), ln1_b=rn(H) if cfg.norm == "layernorm" else None,
+            ln1_w=ones(H), ln1_b=rn(H, rep=True) if cfg.norm == "layernorm" else None,
             qkv_w=rn(qkv_n, H), qkv_b=rn(qkv_n) if cfg.qkv_bias else None,
             o_w=rn(H, plan.nh_l * D, s=std / math.sqrt(2 * cfg.num_layers)),
-            o_b=rn(H) if cfg.out_bias and rank == 0 else None,
+            o_b=rn(H, rep=True) if cfg.out_bias else None,
             down_w=rn(H, plan.F_l, s=std / math.sqrt(2 * cfg.num_layers)),
-            down_b=rn(H) if cfg.mlp_bias and rank == 0 else None,
+            down_b=rn(H, rep=True) if cfg.mlp_bias else None,
         )
+        if rank != 0:  # drawn on every rank (keeps the replicated stream aligned), kept on rank 0 only
+            d["o_b"] = d["down_b"] = None
         if not cfg.parallel_block:
-            d["ln2_w"], d["ln2_b"] = ones(H), (rn(H) if cfg.norm == "layernorm" else None)
+            d["ln2_w"], d["ln2_b"] = ones(H), (rn(H, rep=True) if cfg.norm == "layernorm" else None)
         if cfg.gated_mlp:
             d["gate_w"], d["up_w"] = rn(plan.F_l, H), rn(plan.F_l, H)
             if cfg.mlp_bias:
@@ -223,8 +229,8 @@ def random_weights(cfg: ModelConfig, tp: int = 1, rank: int = 0, device="cpu", d
             d["up_w"] = rn(plan.F_l, H)
             d["up_b"] = rn(plan.F_l) if cfg.mlp_bias else None
         layers.append(d)
-    wte = rn(cfg.vocab_size, H)
-    wpe = rn(cfg.max_position_embeddings, H, s=0.01) if cfg.position == "learned" else None
+    wte = rn(cfg.vocab_size, H, rep=True)
+    wpe = rn(cfg.max_position_embeddings, H, s=0.01, rep=True) if cfg.position == "learned" else None
     if cfg.tie_word_embeddings:
         head_w_full = wte
     else:
@@ -244,7 +250,7 @@ def random_weights(cfg: ModelConfig, tp: int = 1, rank: int = 0, device="cpu", d
         head_b = torch.zeros(plan.vocab_padded, dtype=dtype, device=gen_dev)
         if n:
             head_b[lo:lo + n] = rn(n)
-    lnf_b = rn(H) if cfg.norm == "layernorm" else None
+    lnf_b = rn(H, rep=True) if cfg.norm == "layernorm" else None
     return _finish(cfg, plan, wte, wpe, layers, ones(H), lnf_b, head_w, head_b, device, dtype, fp8)
 
 

@@ -47,6 +47,10 @@ def _check(cond: bool, msg: str):
 
 def _bf16_rows(t: torch.Tensor, name: str, cols: Optional[int] = None):
     _check(t.is_cuda, f"{name} must be on the GPU")
+    # kernels launch on the CURRENT device's stream: a tensor of another device would be addressed
+    # through the wrong GPU's page tables
+    _check(t.device.index == torch.cuda.current_device(),
+           f"{name} is on {t.device} but the current device is cuda:{torch.cuda.current_device()}")
     _check(t.dtype == torch.bfloat16, f"{name} must be bfloat16, got {t.dtype}")
     _check(t.dim() == 2, f"{name} must be 2-D")
     _check(t.stride(1) == 1, f"{name} rows must be contiguous")

@@ -87,9 +87,16 @@ class TPGroup:
             st = self._host_staged = self.is_real and dist.get_backend(self.group) == "gloo"
         return st
 
+    @staticmethod
+    def _no_capture():
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("host-staged (gloo) collectives cannot be captured into a HIP graph; "
+                               "run the engine with use_graphs=False on this group")
+
     # ------------------------------------------------------------ data plane
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.is_real and t.is_cuda and self.host_staged:
+            self._no_capture()
             h = t.cpu()
             dist.all_reduce(h, group=self.group)
             t.copy_(h)
@@ -107,6 +114,7 @@ class TPGroup:
             return t
         t = t.contiguous()
         if t.is_cuda and self.host_staged:
+            self._no_capture()
             h = t.cpu()
             out = torch.empty((self.size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype)
             dist.all_gather_into_tensor(out, h, group=self.group)
@@ -119,6 +127,7 @@ class TPGroup:
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.is_real and t.is_cuda and self.host_staged:
+            self._no_capture()
             h = t.cpu()
             dist.broadcast(h, src=src, group=self.group)
             t.copy_(h)
@@ -144,6 +153,35 @@ class TPGroup:
         if self.is_real:
             dist.barrier(group=self.group)
 
+    # ------------------------------------------------------------ host-side agreement
+    def _host_tensor_device(self):
+        if dist.get_backend(self.group) == "nccl":
+            return torch.device("cuda", torch.cuda.current_device())
+        return torch.device("cpu")
+
+    def all_reduce_int(self, v: int, op: str = "min") -> int:
+        """Agree on one integer across ranks (``op`` = min | max | sum). Used for decisions every
+        rank must take identically although each computes its own input (e.g. the KV pool size from
+        its own free HBM: ranks that disagree would schedule differently and then deadlock in
+        mismatched collectives)."""
+        if not self.is_real:
+            return int(v)
+        t = torch.tensor([int(v)], dtype=torch.int64, device=self._host_tensor_device())
+        rop = {"min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX, "sum": dist.ReduceOp.SUM}[op]
+        dist.all_reduce(t, op=rop, group=self.group)
+        return int(t.item())
+
+    def check_consistent(self, what: str, fingerprint: dict) -> None:
+        """Raise on every rank if any rank's ``fingerprint`` differs from rank 0's (a mismatched
+        model / engine config would otherwise surface as a hang in the first diverging collective)."""
+        if not self.is_real:
+            return
+        allfp = self.all_gather_object(fingerprint)
+        bad = {r: {k: (fp.get(k), allfp[0].get(k)) for k in set(fp) | set(allfp[0]) if fp.get(k) != allfp[0].get(k)}
+               for r, fp in enumerate(allfp) if fp != allfp[0]}
+        if bad:
+            raise RuntimeError(f"{what}: tensor-parallel ranks disagree (rank: {{key: (value, rank0 value)}}): {bad}")
+
     def __repr__(self):
         kind = "fake" if self.fake else ("local" if self.size == 1 else "rccl/gloo")
         return f"TPGroup(rank={self.rank}, size={self.size}, {kind})"
@@ -154,12 +192,14 @@ def _env_int(name: str, default: int) -> int:
     return int(v) if v not in (None, "") else default
 
 
-def initialize_distributed(timeout_s: int = 120, backend: Optional[str] = None):
+def initialize_distributed(timeout_s: Optional[int] = None, backend: Optional[str] = None):
     """Initialise torch.distributed from torchrun env vars.
 
     Returns ``(tp_group, rank, world_size)`` like the reference
     (``dist.py:40``); ``tp_group`` is a :class:`TPGroup`.
     """
+    if timeout_s is None:  # engine start-up (weight load, per-rank GEMM autotuning) runs between collectives
+        timeout_s = _env_int("LLMSS_DIST_TIMEOUT_S", 600)
     rank = _env_int("RANK", 0)
     world_size = _env_int("WORLD_SIZE", 1)
     local_rank = _env_int("LOCAL_RANK", rank)

@@ -102,6 +102,7 @@ class EngineDriver:
         self.fault = fault if fault is not None else FaultSpec.from_env()
         self.error: Optional[BaseException] = None
         self._last_bcast = time.perf_counter()
+        self.stats = {"ctrl_bcasts": 0, "ctrl_payloads": 0}
 
     # --------------------------------------------------------------------- leader API
     def submit(self, prompt_ids: List[int], params: SamplingParams,
@@ -138,12 +139,34 @@ class EngineDriver:
         return self
 
     # --------------------------------------------------------------------- loop
+    _EMPTY = {"new": [], "abort": [], "stop": False}
+
     def _bcast(self, msg):
+        """Leader -> followers, once per engine step. The common case (nothing new) costs one 16-byte
+        gloo broadcast of a fixed-size header; the pickled payload follows only when the step
+        admits or aborts requests (the reference pickles a broadcast_object_list on every idle poll,
+        consumer_server.py:108)."""
         if not self.tp.is_real:
             return msg
-        box = [msg]
-        dist.broadcast_object_list(box, src=0, group=self.cg)
-        return box[0]
+        import pickle
+
+        hdr = torch.zeros(2, dtype=torch.int64)
+        payload = None
+        if self.leader:
+            empty = not msg["new"] and not msg["abort"] and not msg["stop"]
+            if not empty:
+                payload = pickle.dumps(msg, protocol=pickle.HIGHEST_PROTOCOL)
+                hdr[0] = len(payload)
+            hdr[1] = 1 if msg.get("hb") else 0
+        dist.broadcast(hdr, src=0, group=self.cg)
+        n = int(hdr[0])
+        self.stats["ctrl_bcasts"] += 1
+        if n == 0:
+            return dict(self._EMPTY, hb=bool(hdr[1]))
+        self.stats["ctrl_payloads"] += 1
+        buf = torch.frombuffer(bytearray(payload), dtype=torch.uint8) if self.leader else torch.empty(n, dtype=torch.uint8)
+        dist.broadcast(buf, src=0, group=self.cg)
+        return msg if self.leader else pickle.loads(buf.numpy().tobytes())
 
     def _collect(self, block: bool):
         """Leader: drain the inbox (blocking when idle). Returns a control message."""

@@ -114,6 +114,21 @@ static void test_safetensors(const std::string& dir) {
   CHECK(throws([&] { SafetensorsFile x(bad1); }));
   CHECK(throws([&] { SafetensorsFile x(bad2); }));
   CHECK(throws([&] { SafetensorsFile x(bad3); }));
+  // a header length near 2^64 must be rejected (8 + hlen would wrap), not reach std::string
+  {
+    std::ofstream f(dir + "/bad4.safetensors", std::ios::binary);
+    uint64_t n = ~uint64_t(0) - 3;
+    f.write(reinterpret_cast<const char*>(&n), 8);
+    f.write(data.data(), data.size());
+  }
+  CHECK(throws([&] { SafetensorsFile x(dir + "/bad4.safetensors"); }));
+  // a throwing constructor must not leak its fd / mapping: far more failures than the fd limit
+  for (int i = 0; i < 3000; ++i) {
+    CHECK(throws([&] { SafetensorsFile x(bad1); }));
+    CHECK(throws([&] { SafetensorsFile x(dir + "/bad4.safetensors"); }));
+  }
+  SafetensorsFile again(p);  // fds still available
+  CHECK(again.keys().size() == 1);
 }
 
 int main(int argc, char** argv) {

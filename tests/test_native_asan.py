@@ -20,6 +20,12 @@ def test_runtime_under_asan_ubsan(tmp_path):
     # verify_asan_link_order=0: the environment may preload other libraries ahead of the ASan runtime
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0",
                UBSAN_OPTIONS="print_stacktrace=1")
-    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=120, env=env)
+    import resource
+
+    def _few_fds():  # 3000 failing opens below leak-check the reader's fd / mapping cleanup
+        resource.setrlimit(resource.RLIMIT_NOFILE, (512, 512))
+
+    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=120, env=env,
+                       preexec_fn=_few_fds)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ALL OK" in r.stdout

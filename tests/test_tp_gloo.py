@@ -79,3 +79,71 @@ def test_tp_matches_single(tmp_path, name, world, overlap):
     g, s = _run(world, d, prompts, overlap)
     assert g == ref_g
     assert s == ref_s
+
+
+def _consistency_worker(rank, world, port, ckpt, mode, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from llmss_amd.engine import LLMEngine, SamplingParams, build_model
+    from llmss_amd.parallel.dist import initialize_distributed
+
+    tp, r, w = initialize_distributed(backend="gloo")
+    m = build_model(ckpt, tp, "fp32", "cpu")
+    try:
+        if mode == "blocks":
+            # each rank sizes its KV pool from its own (here: deliberately different) free memory;
+            # 9 blocks of 4 tokens on rank 0 forces preemption for these 3 prompts x 13 tokens
+            LLMEngine._auto_blocks = lambda self, frac: 9 if r == 0 else 200 + 50 * r
+            eng = LLMEngine(m, max_num_seqs=4, block_size=4, check_tokens=True)
+            prompts = [[(3 * i + 7 * j) % 100 for j in range(5 + 2 * i)] for i in range(3)]
+            out = eng.generate(prompts, SamplingParams(max_new_tokens=8, is_greedy=True, ignore_eos=True))
+            q.put((r, eng.num_blocks, eng.stats["preemptions"], out))
+        else:  # rank 1 runs a different engine config: must raise on every rank, not hang
+            LLMEngine(m, max_num_seqs=4 if r == 0 else 8, block_size=4, num_blocks=64)
+            q.put((r, "no error"))
+    except RuntimeError as e:
+        q.put((r, "raised", str(e)[:200]))
+    torch.distributed.destroy_process_group()
+
+
+def _run_consistency(world, ckpt, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_consistency_worker, args=(r, world, port, ckpt, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+        for p in procs:
+            p.join(timeout=60)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
+                p.join(10)
+    return res, [p.exitcode for p in procs]
+
+
+def test_kv_pool_agreed_across_ranks(tmp_path):
+    d = str(tmp_path / "llama")
+    save_hf_model("llama", d, vocab=101)
+    from llmss_amd.engine import LLMEngine, SamplingParams, build_model
+
+    prompts = [[(3 * i + 7 * j) % 100 for j in range(5 + 2 * i)] for i in range(3)]
+    ref = LLMEngine(build_model(d, None, "fp32", "cpu"), max_num_seqs=4, block_size=4, num_blocks=64)
+    ref_g = ref.generate(prompts, SamplingParams(max_new_tokens=8, is_greedy=True, ignore_eos=True))
+    res, codes = _run_consistency(2, d, "blocks")
+    assert codes == [0, 0], res
+    assert [x[1] for x in res] == [9, 9]  # the minimum of the ranks' own sizes
+    assert res[0][2] > 0 and res[0][2] == res[1][2]  # same preemption decisions on both ranks
+    assert res[0][3] == res[1][3] == ref_g
+
+
+def test_mismatched_engine_config_raises(tmp_path):
+    d = str(tmp_path / "gpt2")
+    save_hf_model("gpt2", d, vocab=101)
+    res, codes = _run_consistency(2, d, "mismatch")
+    assert [x[1] for x in res] == ["raised", "raised"], res
+    assert "max_num_seqs" in res[0][2]

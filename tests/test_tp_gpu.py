@@ -58,9 +58,26 @@ def _sampled():
             for i in range(4)]
 
 
+def _prefill_logits(m):
+    """All-gathered last-token logits of one prefill step over the prompt batch (no sampling)."""
+    from llmss_amd.models.decoder import StepInput
+
+    dev = m.device
+    ps = _prompts()
+    ids = torch.tensor([t for p in ps for t in p], device=dev)
+    pos = torch.cat([torch.arange(len(p)) for p in ps]).to(dev)
+    cu = torch.tensor([0] + list(torch.tensor([len(p) for p in ps]).cumsum(0)), dtype=torch.int32, device=dev)
+    kv = m.allocate_kv_cache(16, 16)
+    inp = StepInput("prefill", ids, pos, torch.full_like(ids, -1), cu_seqlens=cu, max_seqlen=max(map(len, ps)),
+                    last_idx=(cu[1:] - 1).long())
+    return m(inp, kv)[:, :m.cfg.vocab_size].float().cpu()
+
+
 def _worker(rank, world, port, ckpt, q):
+    # both ranks share the box's one GPU: device 0 for both (LOCAL_RANK=rank would make rank 1's current
+    # device cuda:1 on a multi-GPU box while its tensors live on cuda:0)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+                      LOCAL_RANK="0")
     torch.set_num_threads(2)
     from llmss_amd.engine import LLMEngine, build_model
     from llmss_amd.ops import hip
@@ -72,8 +89,9 @@ def _worker(rank, world, port, ckpt, q):
     eng = LLMEngine(m, max_num_seqs=4, block_size=16, use_graphs=False, check_tokens=True)
     g = eng.generate(_prompts(), _greedy())
     s = eng.generate(_prompts(), _sampled())
+    lg = _prefill_logits(m)
     if r == 0:
-        q.put((g, s, hip.lib().__file__))
+        q.put((g, s, hip.lib().__file__, lg))
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()
 
@@ -87,6 +105,7 @@ def test_tp2_native_matches_tp1(tmp_path, name):
     ref = LLMEngine(build_model(d, None, "bf16", torch.device("cuda", 0)), max_num_seqs=4, block_size=16,
                     use_graphs=False)
     ref_g = ref.generate(_prompts(), _greedy())
+    ref_lg = _prefill_logits(ref.model)
     del ref
     torch.cuda.empty_cache()
 
@@ -96,13 +115,24 @@ def test_tp2_native_matches_tp1(tmp_path, name):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, d, q)) for r in range(2)]
     for p in procs:
         p.start()
-    g, s, lib = q.get(timeout=240)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    try:
+        g, s, lib, lg = q.get(timeout=240)
+        for p in procs:
+            p.join(timeout=60)
+    finally:  # a failed or hung rank must not outlive the test holding GPU memory
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
+                p.join(10)
+    assert [p.exitcode for p in procs] == [0, 0]
     assert "llmss_amd" in lib
-    # bf16 partial sums are added in a different order at TP=2: allow rare argmax flips (and the
-    # divergence that follows one), but the continuations must essentially agree
+    # primary check: the sharded forward's logits equal TP=1's to bf16 rounding (partial sums are
+    # added in a different order at TP=2)
+    scale = ref_lg.abs().max()
+    err = (lg - ref_lg).abs().max() / scale
+    cos = torch.nn.functional.cosine_similarity(lg, ref_lg, dim=-1).min()
+    assert err < 2e-2 and cos > 0.9995, (float(err), float(cos))
+    # secondary: greedy continuations essentially agree (a rare argmax flip diverges the rest)
     first = sum(a[0] == b[0] for a, b in zip(g, ref_g))
     agree = sum(x == y for a, b in zip(g, ref_g) for x, y in zip(a, b)) / sum(len(a) for a in ref_g)
     assert first >= 3 and agree > 0.6, (first, agree, g, ref_g)
