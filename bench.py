@@ -148,7 +148,7 @@ def run_config(args, model_name, tp, batch, progress, dp=False):
     if args.simulate_tp > 1:
         par = f"tp{args.simulate_tp}-simulated-" + (f"comm-model-{args.sim_comm}" if args.sim_comm else "no-comm")
     else:
-        par = f"dp{world}" if dp else f"tp{world}"
+        par = (f"dp{world}xtp1" if world > 1 else "tp1") if dp else f"tp{world}"
     out = {
         "metric": "output_tokens_per_sec",
         "value": round(value, 2),

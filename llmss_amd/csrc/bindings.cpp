@@ -25,6 +25,10 @@ void launch_attn_decode(const void* q, int64_t q_stride, const void* kc, const v
 void launch_attn_prefill(const void* qkv, int64_t row_stride, const void* cu_seqlens, void* out, int64_t out_stride,
                          int B, int max_seqlen, int nh, int nkv, int D, int k_off, int v_off, float scale,
                          hipStream_t st);
+void launch_attn_extend(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
+                        const void* block_tables, int max_blocks, const void* cu_q, const void* ctx_lens, void* out,
+                        int64_t out_stride, int B, int max_qlen, int nh, int nkv, int D, int bs, float scale,
+                        hipStream_t st);
 void launch_attn_decode_fused(const void* qkv, int64_t q_stride, const void* part, int S, int64_t slab,
                               const void* bias, int N, const void* pos, const void* cos_t, const void* sin_t,
                               const void* slots, int rot, int style, int k_off, int v_off, void* kc, void* vc,
@@ -92,6 +96,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_prefill", [](uintptr_t qkv, int64_t rs, uintptr_t cu, uintptr_t out, int64_t os, int B, int maxlen,
                            int nh, int nkv, int D, int k_off, int v_off, float scale, uintptr_t st) {
     launch_attn_prefill(CP(qkv), rs, CP(cu), P(out), os, B, maxlen, nh, nkv, D, k_off, v_off, scale, S(st));
+  });
+  m.def("attn_extend", [](uintptr_t q, int64_t qs, uintptr_t kc, uintptr_t vc, uintptr_t bt, int maxb, uintptr_t cu,
+                          uintptr_t cl, uintptr_t out, int64_t os, int B, int maxq, int nh, int nkv, int D, int bs,
+                          float scale, uintptr_t st) {
+    launch_attn_extend(CP(q), qs, CP(kc), CP(vc), CP(bt), maxb, CP(cu), CP(cl), P(out), os, B, maxq, nh, nkv, D, bs,
+                       scale, S(st));
   });
   m.def("gemm", [](uintptr_t x, int64_t ldx, uintptr_t w, int64_t ldw, bool fp8, uintptr_t ws, uintptr_t bias,
                    uintptr_t y, int64_t ldy, int M, int N, int K, int act, bool glu, uintptr_t work, int64_t wbytes,

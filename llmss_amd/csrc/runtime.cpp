@@ -98,7 +98,8 @@ struct SeqState {
   int64_t id;
   int prompt_len;
   int max_new;
-  int num_tokens;  // prompt + generated
+  int num_tokens;    // prompt + generated tokens known
+  int num_computed;  // tokens whose K/V are in the cache (scheduled into a step)
   std::vector<int> blocks;
   int status;  // 0 waiting, 1 running, 2 finished
   int64_t order;
@@ -106,10 +107,12 @@ struct SeqState {
 };
 
 struct StepBatch {
-  int kind = 0;  // 0 idle, 1 prefill, 2 decode
+  int kind = 0;        // 0 idle, 1 extend (prefill chunks, optionally mixed with decodes), 2 decode only
+  int num_decode = 0;  // kind 1: items [0, num_decode) are single-token decodes, the rest prompt chunks
   std::vector<int64_t> ids;
   std::vector<int> query_lens;  // new tokens fed this step per sequence
   std::vector<int> ctx_lens;    // KV length after this step per sequence
+  std::vector<uint8_t> sample;  // the step completes the sequence's known tokens -> sample one
   std::vector<int64_t> positions;
   std::vector<int64_t> slots;
   std::vector<int> block_table;  // [B, max_blocks] padded with 0
@@ -117,15 +120,26 @@ struct StepBatch {
   std::vector<int64_t> preempted;
 };
 
+// Continuous batching with chunked prefill. Every step spends a budget of max_batched_tokens:
+//   1. one token for every running sequence that is decoding (oldest first); when the KV pool runs
+//      dry the newest running sequence is preempted (blocks freed, recomputed later);
+//   2. the next chunk of every partially prefilled running sequence;
+//   3. FCFS admission of waiting prompts, each with as much of its prompt as the budget allows
+//      (prefill_chunk > 0 caps one chunk; prefill_chunk < 0 keeps prompts whole).
+// Decodes therefore never stall behind a long prompt (the prompt is cut into chunks that ride along
+// with the decode tokens), and a chunk's attention reads its own prefix from the paged cache.
 class Scheduler {
  public:
-  Scheduler(int num_blocks, int block_size, int max_num_seqs, int max_batched_tokens, int max_model_len)
+  Scheduler(int num_blocks, int block_size, int max_num_seqs, int max_batched_tokens, int max_model_len,
+            int prefill_chunk = 0)
       : alloc_(num_blocks, block_size),
         bs_(block_size),
         max_seqs_(max_num_seqs),
         max_tokens_(max_batched_tokens),
-        max_len_(max_model_len) {
+        max_len_(max_model_len),
+        chunk_(prefill_chunk) {
     max_blocks_per_seq_ = (max_model_len + block_size - 1) / block_size;
+    if (max_batched_tokens <= 0) throw std::invalid_argument("Scheduler: max_batched_tokens must be > 0");
   }
 
   void add(int64_t id, int prompt_len, int max_new) {
@@ -133,20 +147,26 @@ class Scheduler {
     if (prompt_len <= 0) throw std::invalid_argument("Scheduler.add: empty prompt");
     if (prompt_len + max_new > max_len_)
       throw std::invalid_argument("Scheduler.add: prompt_len + max_new_tokens exceeds max_model_len");
-    SeqState s{id, prompt_len, max_new, prompt_len, {}, 0, counter_++};
+    if (chunk_ < 0 && prompt_len > max_tokens_)
+      throw std::invalid_argument("Scheduler.add: prompt longer than max_batched_tokens (whole-prompt mode)");
+    SeqState s{id, prompt_len, max_new, prompt_len, 0, {}, 0, counter_++};
     seqs_.emplace(id, s);
     waiting_.push_back(id);
   }
 
-  // A token was sampled for `id`; `finished` releases its blocks.
+  // A token was sampled for `id` (its step had sample=1); `finished` releases its blocks.
   void on_token(int64_t id, bool finished) {
     auto& s = get(id);
     if (s.status != 1) throw std::runtime_error("Scheduler.on_token: sequence not running");
+    // the sampled token's step computed every known token (a step the engine launched on its own,
+    // pipelined decode, computed the last one without a schedule() call)
+    if (s.num_computed < s.num_tokens - 1) throw std::runtime_error("Scheduler.on_token: sequence still prefilling");
+    s.num_computed = s.num_tokens;
     s.num_tokens += 1;
     if (finished || s.num_tokens - s.prompt_len >= s.max_new) finish(id);
   }
 
-  // Batched on_token for a whole decode step (one call instead of one per sequence).
+  // Batched on_token for a whole step (one call instead of one per sequence).
   void on_tokens(const int64_t* ids, const bool* finished, int64_t n) {
     for (int64_t i = 0; i < n; ++i) on_token(ids[i], finished[i]);
   }
@@ -166,46 +186,19 @@ class Scheduler {
 
   StepBatch schedule() {
     StepBatch b;
-    // ---- admit prefills (FCFS, stop at the first one that does not fit)
-    int tokens = 0;
-    while (!waiting_.empty() && (int)running_.size() + (int)b.ids.size() < max_seqs_) {
-      auto& s = get(waiting_.front());
-      const int n = s.num_tokens;  // full recompute after preemption
-      const int need = blocks_for(n);
-      if (!b.ids.empty() && tokens + n > max_tokens_) break;
-      if (!alloc_.can_allocate(need)) break;
-      s.blocks = alloc_.allocate_n(need);
-      s.status = 1;
-      waiting_.pop_front();
-      b.ids.push_back(s.id);
-      b.query_lens.push_back(n);
-      b.ctx_lens.push_back(n);
-      for (int p = 0; p < n; ++p) {
-        b.positions.push_back(p);
-        b.slots.push_back(slot(s, p));
-      }
-      tokens += n;
-    }
-    if (!b.ids.empty()) {
-      for (auto id : b.ids) running_.push_back(id);
-      b.kind = 1;
-      fill_tables(b);
-      return b;
-    }
-    // ---- decode: one token per running sequence, preempting the newest on exhaustion
+    int budget = max_tokens_;
     std::vector<int64_t> order(running_.begin(), running_.end());
     std::sort(order.begin(), order.end(), [&](int64_t a, int64_t c) { return get(a).order < get(c).order; });
-    std::vector<int64_t> batch;
-    for (size_t i = 0; i < order.size(); ++i) {
+    // ---- 1. decodes
+    for (size_t i = 0; i < order.size() && budget > 0; ++i) {
       auto& s = get(order[i]);
-      if (s.status != 1) continue;
+      if (s.status != 1 || s.num_tokens - s.num_computed != 1) continue;
       while ((int)s.blocks.size() * bs_ < s.num_tokens) {
         if (alloc_.can_allocate(1)) {
           s.blocks.push_back(alloc_.allocate());
           continue;
         }
-        // preempt the newest running sequence that is not s (or s itself if it is the newest)
-        int64_t victim = -1;
+        int64_t victim = -1;  // the newest running sequence (possibly s itself)
         for (size_t j = order.size(); j-- > i;) {
           if (get(order[j]).status == 1) {
             victim = order[j];
@@ -216,28 +209,54 @@ class Scheduler {
         b.preempted.push_back(victim);
         if (victim == s.id) break;
       }
-      if (s.status == 1) batch.push_back(s.id);
+      if (s.status == 1) {
+        emit(b, s, 1);
+        budget -= 1;
+      }
     }
-    if (batch.empty()) return b;
-    b.kind = 2;
-    for (auto id : batch) {
-      auto& s = get(id);
-      b.ids.push_back(id);
-      b.query_lens.push_back(1);
-      b.ctx_lens.push_back(s.num_tokens);
-      b.positions.push_back(s.num_tokens - 1);
-      b.slots.push_back(slot(s, s.num_tokens - 1));
+    b.num_decode = (int)b.ids.size();
+    // ---- 2. continuing prompt chunks
+    for (size_t i = 0; i < order.size() && budget > 0; ++i) {
+      auto& s = get(order[i]);
+      if (s.status != 1 || s.num_tokens - s.num_computed <= 1) continue;
+      const int q = chunk_len(s, budget);
+      if (q <= 0 || !grow(s, s.num_computed + q)) break;
+      emit(b, s, q);
+      budget -= q;
     }
+    // ---- 3. admission (FCFS, stop at the first prompt that does not fit)
+    while (!waiting_.empty() && budget > 0 && (int)running_.size() < max_seqs_) {
+      auto& s = get(waiting_.front());
+      const int q = chunk_len(s, budget);  // after preemption the whole known sequence is recomputed
+      if (q <= 0 || !grow(s, q)) break;
+      s.status = 1;
+      waiting_.pop_front();
+      running_.push_back(s.id);
+      emit(b, s, q);
+      budget -= q;
+    }
+    if (b.ids.empty()) return b;
+    b.kind = (b.num_decode == (int)b.ids.size()) ? 2 : 1;
     fill_tables(b);
     return b;
   }
 
   int num_waiting() const { return (int)waiting_.size(); }
   int num_running() const { return (int)running_.size(); }
+  // running sequences with prompt tokens still to compute (the next step is not a pure decode)
+  int num_prefilling() const {
+    int n = 0;
+    for (auto id : running_) {
+      const auto& s = seqs_.at(id);
+      n += (s.num_tokens - s.num_computed) > 1;
+    }
+    return n;
+  }
   int num_free_blocks() const { return alloc_.num_free(); }
   int max_blocks_per_seq() const { return max_blocks_per_seq_; }
   bool has_work() const { return !waiting_.empty() || !running_.empty(); }
   int num_tokens(int64_t id) { return get(id).num_tokens; }
+  int num_computed(int64_t id) { return get(id).num_computed; }
   std::vector<int> blocks(int64_t id) { return get(id).blocks; }
   bool contains(int64_t id) const { return seqs_.count(id) > 0; }
 
@@ -249,10 +268,37 @@ class Scheduler {
   }
   int blocks_for(int n) const { return (n + bs_ - 1) / bs_; }
   int64_t slot(const SeqState& s, int p) const { return (int64_t)s.blocks[p / bs_] * bs_ + p % bs_; }
+  int chunk_len(const SeqState& s, int budget) const {
+    const int rem = s.num_tokens - s.num_computed;
+    if (chunk_ < 0) return rem <= budget ? rem : 0;  // whole prompts only
+    int q = std::min(rem, budget);
+    if (chunk_ > 0) q = std::min(q, chunk_);
+    return q;
+  }
+  bool grow(SeqState& s, int n_tokens) {  // blocks for n_tokens cached tokens, no preemption
+    const int need = blocks_for(n_tokens) - (int)s.blocks.size();
+    if (need <= 0) return true;
+    if (!alloc_.can_allocate(need)) return false;
+    for (int i = 0; i < need; ++i) s.blocks.push_back(alloc_.allocate());
+    return true;
+  }
+  void emit(StepBatch& b, SeqState& s, int q) {
+    const int p0 = s.num_computed;
+    b.ids.push_back(s.id);
+    b.query_lens.push_back(q);
+    b.ctx_lens.push_back(p0 + q);
+    for (int p = p0; p < p0 + q; ++p) {
+      b.positions.push_back(p);
+      b.slots.push_back(slot(s, p));
+    }
+    s.num_computed = p0 + q;
+    b.sample.push_back(s.num_computed == s.num_tokens ? 1 : 0);
+  }
   void preempt(int64_t id) {
     auto& s = get(id);
     alloc_.free_all(s.blocks);
     s.blocks.clear();
+    s.num_computed = 0;
     s.status = 0;
     s.preemptions++;
     running_.erase(std::remove(running_.begin(), running_.end(), id), running_.end());
@@ -269,7 +315,7 @@ class Scheduler {
   }
 
   BlockAllocator alloc_;
-  int bs_, max_seqs_, max_tokens_, max_len_, max_blocks_per_seq_;
+  int bs_, max_seqs_, max_tokens_, max_len_, max_blocks_per_seq_, chunk_;
   std::unordered_map<int64_t, SeqState> seqs_;
   std::deque<int64_t> waiting_;
   std::vector<int64_t> running_;
@@ -597,7 +643,13 @@ void register_runtime(py::module_& m) {
 
   py::class_<StepBatch>(m, "StepBatch")
       .def_readonly("kind", &StepBatch::kind)
+      .def_readonly("num_decode", &StepBatch::num_decode)
       .def_readonly("max_blocks", &StepBatch::max_blocks)
+      .def_property_readonly("sample", [](const StepBatch& b) {
+        py::array_t<bool> a((ssize_t)b.sample.size());
+        for (size_t i = 0; i < b.sample.size(); ++i) a.mutable_data()[i] = b.sample[i] != 0;
+        return a;
+      })
       .def_property_readonly("ids", [](const StepBatch& b) { return to_np(b.ids); })
       .def_property_readonly("query_lens", [](const StepBatch& b) { return to_np(b.query_lens); })
       .def_property_readonly("ctx_lens", [](const StepBatch& b) { return to_np(b.ctx_lens); })
@@ -613,8 +665,9 @@ void register_runtime(py::module_& m) {
       .def_property_readonly("preempted", [](const StepBatch& b) { return to_np(b.preempted); });
 
   py::class_<Scheduler>(m, "Scheduler")
-      .def(py::init<int, int, int, int, int>(), py::arg("num_blocks"), py::arg("block_size"), py::arg("max_num_seqs"),
-           py::arg("max_batched_tokens"), py::arg("max_model_len"))
+      .def(py::init<int, int, int, int, int, int>(), py::arg("num_blocks"), py::arg("block_size"),
+           py::arg("max_num_seqs"), py::arg("max_batched_tokens"), py::arg("max_model_len"),
+           py::arg("prefill_chunk") = 0)
       .def("add", &Scheduler::add)
       .def("on_token", &Scheduler::on_token)
       .def("on_tokens",
@@ -628,6 +681,8 @@ void register_runtime(py::module_& m) {
       .def("schedule", &Scheduler::schedule)
       .def("num_waiting", &Scheduler::num_waiting)
       .def("num_running", &Scheduler::num_running)
+      .def("num_prefilling", &Scheduler::num_prefilling)
+      .def("num_computed", &Scheduler::num_computed)
       .def("num_free_blocks", &Scheduler::num_free_blocks)
       .def("max_blocks_per_seq", &Scheduler::max_blocks_per_seq)
       .def("has_work", &Scheduler::has_work)

@@ -6,8 +6,10 @@ sampling on rank 0 followed by a ``dist.broadcast`` of the token every step, a h
 token and (no-cache mode) ``torch.cuda.empty_cache()`` per token.
 
 Here:
-* the C++ :class:`Scheduler` admits prompts FCFS under token/sequence/KV-block budgets and
-  batches every running sequence's next token (continuous batching, preemption by recompute);
+* the C++ :class:`Scheduler` spends a per-step token budget on every running sequence's next
+  token, then on prompt chunks (chunked prefill: a long prompt is split over steps and mixed with
+  the running decodes, its chunks attending their cached prefix through the paged cache), then on
+  FCFS admission (continuous batching, preemption by recompute);
 * the KV cache is a preallocated paged pool sized from free HBM (288 GB per MI355X);
 * decode steps replay a HIP graph captured per batch-size bucket (embedding -> all layers incl.
   RCCL all-reduces -> LM head -> all-gather -> sampler), so a step is one graph launch;
@@ -134,7 +136,7 @@ class LLMEngine:
                  block_size: int = 16, num_blocks: Optional[int] = None, max_model_len: Optional[int] = None,
                  kv_fraction: float = 0.9, use_graphs: Optional[bool] = None, eos_token_id: Optional[int] = None,
                  graph_buckets: Optional[Sequence[int]] = None, check_tokens: Optional[bool] = None,
-                 autotune: Optional[bool] = None):
+                 autotune: Optional[bool] = None, prefill_chunk: Optional[int] = None):
         self.model = model
         self.cfg = model.cfg
         self.tp = model.tp
@@ -143,7 +145,7 @@ class LLMEngine:
         self.block_size = block_size
         self.max_model_len = min(max_model_len or self.cfg.max_position_embeddings, self.cfg.max_position_embeddings)
         self.max_num_seqs = max_num_seqs
-        self.max_batched_tokens = max(max_batched_tokens, self.max_model_len)
+        self.max_batched_tokens = max_batched_tokens
         self.eos = eos_token_id if eos_token_id is not None else self.cfg.eos_token_id
         self.max_blocks = math.ceil(self.max_model_len / block_size)
         # every rank runs its own scheduler on the same request stream, so the KV pool (admission,
@@ -151,8 +153,12 @@ class LLMEngine:
         # take the minimum
         self.num_blocks = self.tp.all_reduce_int(num_blocks or self._auto_blocks(kv_fraction), "min")
         self.kv = model.allocate_kv_cache(self.num_blocks, block_size)
+        # chunked prefill: prompts are cut to fit the per-step token budget and ride along with the
+        # running decodes (prefill_chunk > 0 caps a chunk further; < 0 keeps prompts whole)
+        self.prefill_chunk = int(prefill_chunk if prefill_chunk is not None else
+                                 os.environ.get("LLMSS_PREFILL_CHUNK", "0"))
         self.sched = _native().Scheduler(self.num_blocks, block_size, max_num_seqs, self.max_batched_tokens,
-                                         self.max_model_len)
+                                         self.max_model_len, self.prefill_chunk)
         self.requests: Dict[int, Request] = {}
         self._next_id = 0
         self._pending = collections.deque()  # launched GPU decode steps whose tokens are not yet processed
@@ -208,7 +214,7 @@ class LLMEngine:
                 "num_blocks": self.num_blocks, "max_model_len": self.max_model_len,
                 "max_num_seqs": self.max_num_seqs, "max_batched_tokens": self.max_batched_tokens,
                 "buckets": list(self.buckets), "graphs": bool(self.use_graphs),
-                "async_decode": self.async_decode, "eos": self.eos,
+                "async_decode": self.async_decode, "eos": self.eos, "prefill_chunk": self.prefill_chunk,
                 "overlap_rows": self.model.overlap_rows, "tbo_min": self.model.tbo_min,
                 "fp8": any(L.qkv.w_scale is not None for L in self.model.w.layers[:1])}
 
@@ -302,7 +308,7 @@ class LLMEngine:
         t_a = time.perf_counter() if hp else 0.0
         done = None
         if self._pending:
-            if self.async_decode and self.sched.num_waiting() == 0:
+            if self.async_decode and self.sched.num_waiting() == 0 and self.sched.num_prefilling() == 0:
                 self._speculate(self._pending[-1])
             done = self._collect_decode()
             if self._pending:  # the next step is already in flight
@@ -322,14 +328,16 @@ class LLMEngine:
             self.stats["preemptions"] += len(batch.preempted)
             ids = batch.ids
             reqs = [self.requests[i] for i in ids.tolist()]
-            if batch.kind == 1:
+            if batch.kind == 1:  # prompt chunks (possibly with decode tokens riding along)
                 t0 = time.perf_counter()
                 with self.timer.phase("prefill"):
-                    tokens = self._prefill(batch, reqs)
+                    tokens = self._extend(batch, reqs)
                 self.stats["prefill_steps"] += 1
-                self.stats["prefill_tokens"] += int(batch.query_lens.sum())
+                self.stats["prefill_tokens"] += int(batch.query_lens[batch.num_decode:].sum())
+                self.stats["mixed_decode_tokens"] = self.stats.get("mixed_decode_tokens", 0) + batch.num_decode
                 self.stats["prefill_time_s"] += time.perf_counter() - t0
-                new_events = self._emit(*self._apply(ids, reqs, tokens))
+                smp = batch.sample
+                new_events = self._emit(*self._apply(ids[smp], [r for r, f in zip(reqs, smp) if f], tokens))
             elif self.is_gpu:
                 self._launch_decode(self._record_from_batch(batch, ids, reqs))
             else:
@@ -386,22 +394,35 @@ class LLMEngine:
         self.stats["tokens"] += len(events)
         return events
 
-    def _prefill(self, batch, reqs: List[Request]) -> List[int]:
+    def _extend(self, batch, reqs: List[Request]) -> List[int]:
+        """A step with prompt chunks: rows [0, num_decode) are decode tokens, then one chunk per
+        prompting sequence (positions ctx - q .. ctx - 1). Returns the tokens sampled for the
+        sequences whose known tokens the step completes (batch.sample)."""
         dev = self.device
         qlens = batch.query_lens.astype(np.int64)
-        ids = np.concatenate([np.asarray(r.all_ids[:q], dtype=np.int64) for r, q in zip(reqs, qlens)])
-        cu = np.zeros(len(reqs) + 1, dtype=np.int32)
-        cu[1:] = np.cumsum(qlens)
+        ctx = batch.ctx_lens.astype(np.int64)
+        nd = int(batch.num_decode)
+        ids = np.concatenate([np.asarray(r.all_ids[c - q:c], dtype=np.int64) for r, q, c in zip(reqs, qlens, ctx)])
+        ends = np.cumsum(qlens)
+        cu = np.zeros(len(reqs) - nd + 1, dtype=np.int32)
+        cu[1:] = ends[nd:] - (ends[nd - 1] if nd else 0)
+        smp = batch.sample
+        has_prefix = bool((ctx[nd:] > qlens[nd:]).any())
+        kind = "prefill" if nd == 0 and not has_prefix else "extend"
+
+        def d(a):
+            return torch.from_numpy(np.ascontiguousarray(a)).to(dev, non_blocking=True)
+
         inp = StepInput(
-            kind="prefill",
-            input_ids=torch.from_numpy(ids).to(dev, non_blocking=True),
-            positions=torch.from_numpy(batch.positions).to(dev, non_blocking=True),
-            slots=torch.from_numpy(batch.slots).to(dev, non_blocking=True),
-            cu_seqlens=torch.from_numpy(cu).to(dev, non_blocking=True),
-            max_seqlen=int(qlens.max()),
-            last_idx=torch.from_numpy(cu[1:].astype(np.int64) - 1).to(dev, non_blocking=True),
-        )
+            kind=kind, input_ids=d(ids), positions=d(batch.positions), slots=d(batch.slots), cu_seqlens=d(cu),
+            max_seqlen=int(qlens[nd:].max()), last_idx=d((ends - 1)[smp]),
+            block_tables=d(batch.block_table.astype(np.int32)) if kind == "extend" else None,
+            ctx_lens=d(ctx.astype(np.int32)) if kind == "extend" else None, max_ctx=self.max_model_len,
+            num_decode=nd, has_prefix=has_prefix)
         logits = self.model(inp, self.kv)
+        reqs = [r for r, f in zip(reqs, smp) if f]
+        if not reqs:
+            return []
         temp, topk, topp, seeds = self._sampling_arrays(reqs)
         tok = ops.sample(logits, torch.from_numpy(temp).to(dev), torch.from_numpy(topk).to(dev),
                          torch.from_numpy(topp).to(dev), torch.from_numpy(seeds).to(dev),

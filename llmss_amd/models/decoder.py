@@ -41,7 +41,16 @@ def _hip_ops():
 
 @dataclass
 class StepInput:
-    kind: str  # "prefill" | "decode"
+    """One forward step over T flattened tokens.
+
+    kind "prefill": every sequence starts at position 0 (cu_seqlens over its tokens);
+    kind "decode": one token per sequence attending its paged context (block_tables, ctx_lens);
+    kind "extend": rows [0, num_decode) are single-token decodes (as "decode"), the remaining rows
+    are prompt chunks (cu_seqlens relative to row num_decode) that may continue a cached prefix
+    (has_prefix: some chunk starts past position 0, so its attention reads the paged cache).
+    block_tables / ctx_lens cover every sequence of the step, decodes first.
+    """
+    kind: str  # "prefill" | "decode" | "extend"
     input_ids: torch.Tensor  # [T] int64
     positions: torch.Tensor  # [T] int64
     slots: torch.Tensor  # [T] int64 physical KV slots (-1 = do not cache)
@@ -52,6 +61,8 @@ class StepInput:
     max_ctx: int = 0
     decode_splits: Optional[Tuple[int, int]] = None
     last_idx: Optional[torch.Tensor] = None  # rows feeding the LM head ([B] int64); None = all rows
+    num_decode: int = 0  # extend: leading single-token decode rows
+    has_prefix: bool = False  # extend: a prompt chunk continues a cached prefix
 
 
 class DecoderLM:
@@ -113,8 +124,28 @@ class DecoderLM:
                              cfg.rotary_dim, cfg.rope_style, do_rope=cfg.position == "rope")
         if inp.kind == "prefill":
             return ops.attn_prefill(qkv, inp.cu_seqlens, inp.max_seqlen, p.nh_l, p.nkv_l, D, self.scale)
+        if inp.kind == "extend":
+            return self._attention_extend(qkv, inp, kc, vc)
         return ops.attn_decode(qkv, kc, vc, inp.block_tables, inp.ctx_lens, p.nh_l, p.nkv_l, D, self.scale,
                                inp.max_ctx, splits=inp.decode_splits)
+
+    def _attention_extend(self, qkv, inp: StepInput, kc, vc):
+        """Mixed step: decode rows through the split-K decode kernel, prompt-chunk rows through the
+        flash prefill kernel (no cached prefix) or the paged extend kernel, into one output."""
+        p, D = self.plan, self.cfg.head_dim
+        T, nd = qkv.shape[0], inp.num_decode
+        out = torch.empty(T, p.nh_l * D, dtype=qkv.dtype, device=qkv.device)
+        if nd:
+            ops.attn_decode(qkv[:nd], kc, vc, inp.block_tables[:nd], inp.ctx_lens[:nd], p.nh_l, p.nkv_l, D,
+                            self.scale, inp.max_ctx, out=out[:nd])
+        if T > nd:
+            if inp.has_prefix:
+                ops.attn_extend(qkv[nd:], kc, vc, inp.block_tables[nd:], inp.cu_seqlens, inp.ctx_lens[nd:],
+                                inp.max_seqlen, p.nh_l, p.nkv_l, D, self.scale, out=out[nd:])
+            else:
+                ops.attn_prefill(qkv[nd:], inp.cu_seqlens, inp.max_seqlen, p.nh_l, p.nkv_l, D, self.scale,
+                                 out=out[nd:])
+        return out
 
     def _comm(self, device):
         if self._comm_stream is None:

@@ -12,7 +12,7 @@ import torch
 
 from . import reference as ref
 
-__all__ = ["add_norm", "embed", "rope_cache", "attn_prefill", "attn_decode", "linear", "sample", "quant_fp8_rows",
+__all__ = ["add_norm", "embed", "rope_cache", "attn_prefill", "attn_decode", "attn_extend", "linear", "sample", "quant_fp8_rows",
            "rope_tables", "glu_interleave", "glu_split"]
 
 rope_tables = ref.rope_tables
@@ -49,17 +49,32 @@ def rope_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, ro
     return qkv
 
 
-def attn_prefill(qkv, cu_seqlens, max_seqlen, nh, nkv, D, scale):
+def _into(y, out):
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def attn_prefill(qkv, cu_seqlens, max_seqlen, nh, nkv, D, scale, out=None):
     if qkv.is_cuda:
-        return _hip().attn_prefill(qkv, cu_seqlens, max_seqlen, nh, nkv, D, scale)
-    return ref.attn_prefill(qkv, cu_seqlens, nh, nkv, D, scale)
+        return _hip().attn_prefill(qkv, cu_seqlens, max_seqlen, nh, nkv, D, scale, out=out)
+    return _into(ref.attn_prefill(qkv, cu_seqlens, nh, nkv, D, scale), out)
 
 
-def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale, max_ctx, splits=None):
+def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale, max_ctx, splits=None, out=None):
     if q.is_cuda:
         return _hip().attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale, max_ctx,
-                                  splits=splits)
-    return ref.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale)
+                                  splits=splits, out=out)
+    return _into(ref.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale), out)
+
+
+def attn_extend(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_qlen, nh, nkv, D, scale, out=None):
+    """Chunked-prefill attention over the paged cache (the chunk's K/V already written)."""
+    if q.is_cuda:
+        return _hip().attn_extend(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_qlen, nh, nkv, D, scale,
+                                  out=out)
+    return _into(ref.attn_extend(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, nh, nkv, D, scale), out)
 
 
 def linear(x, w, bias=None, act="none", glu=False, w_scale: Optional[torch.Tensor] = None, partial_ok=False):

@@ -148,6 +148,33 @@ def attn_prefill(qkv, cu_seqlens, max_seqlen, nh, nkv, D, scale, out=None):
     return y
 
 
+def attn_extend(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_qlen, nh, nkv, D, scale, out=None):
+    """Chunked-prefill attention: q rows [T, >= nh*D] (query heads first, as in the QKV output) of B
+    sequences (``cu_q`` [B+1] int32), each attending its whole paged context ``ctx_lens`` [B] int32 (the
+    chunk's own K/V already written to the cache) causally."""
+    T = q.shape[0]
+    _bf16_rows(q, "q")
+    _check(q.shape[1] >= nh * D, "q too narrow")
+    _check(D in (64, 128, 256), "extend attention supports head_dim 64/128/256")
+    _check(k_cache.dtype == torch.bfloat16 and k_cache.is_contiguous() and k_cache.dim() == 4, "k_cache")
+    _check(k_cache.shape[1] == nkv and k_cache.shape[3] == D, "k_cache shape [nb, nkv, bs, D]")
+    _check(v_cache.shape == k_cache.shape and v_cache.is_contiguous(), "v_cache")
+    _check(nh % nkv == 0, "nh % nkv")
+    B = cu_q.numel() - 1
+    for t, nm in ((cu_q, "cu_q"), (ctx_lens, "ctx_lens"), (block_tables, "block_tables")):
+        _check(t.dtype == torch.int32 and t.is_contiguous() and t.is_cuda, f"{nm} must be contiguous int32 cuda")
+    _check(ctx_lens.numel() == B and block_tables.dim() == 2 and block_tables.shape[0] >= B, "batch sizes")
+    bs = k_cache.shape[2]
+    _check(block_tables.shape[1] * bs >= 1, "block table width")
+    y = out if out is not None else torch.empty(T, nh * D, dtype=q.dtype, device=q.device)
+    _bf16_rows(y, "out")
+    _check(y.shape[0] >= T and y.shape[1] >= nh * D, "out shape")
+    lib().attn_extend(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
+                      block_tables.shape[1], cu_q.data_ptr(), ctx_lens.data_ptr(), y.data_ptr(), y.stride(0), B,
+                      int(max_qlen), nh, nkv, D, bs, float(scale), _stream())
+    return y
+
+
 class DecodeWorkspace:
     """Split-K partial buffers for decode attention (allocated once; graph-capture safe)."""
 

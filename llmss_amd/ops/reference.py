@@ -153,6 +153,30 @@ def attn_decode(q: torch.Tensor, k_cache, v_cache, block_tables, ctx_lens, nh: i
     return out
 
 
+def attn_extend(q: torch.Tensor, k_cache, v_cache, block_tables, cu_q, ctx_lens, nh: int, nkv: int, D: int,
+                scale: float) -> torch.Tensor:
+    """Chunked prefill over the paged cache: sequence b's rows cu_q[b]:cu_q[b+1] sit at positions
+    ctx_lens[b] - qlen ... ctx_lens[b] - 1 and attend every cached key up to their own position."""
+    T = q.shape[0]
+    g = nh // nkv
+    out = torch.zeros(T, nh * D, dtype=q.dtype, device=q.device)
+    cu = [int(c) for c in cu_q.tolist()]
+    for b in range(len(cu) - 1):
+        a, e = cu[b], cu[b + 1]
+        if e == a:
+            continue
+        ctx = int(ctx_lens[b])
+        p0 = ctx - (e - a)
+        qq = q[a:e, : nh * D].view(e - a, nh, D).float().transpose(0, 1)  # [nh, q, D]
+        k = gather_kv(k_cache, block_tables[b], ctx).float().repeat_interleave(g, 0)  # [nh, ctx, D]
+        v = gather_kv(v_cache, block_tables[b], ctx).float().repeat_interleave(g, 0)
+        s = torch.matmul(qq, k.transpose(1, 2)) * scale
+        qpos = torch.arange(p0, ctx, device=q.device)[:, None]
+        s = s.masked_fill(torch.arange(ctx, device=q.device)[None, :] > qpos, float("-inf"))
+        out[a:e] = torch.matmul(torch.softmax(s, -1), v).transpose(0, 1).reshape(e - a, nh * D).to(q.dtype)
+    return out
+
+
 def glu_split(w_or_y: torch.Tensor, dim: int = -1):
     """Split a 16-row/column interleaved gate|up tensor into (gate, up)."""
     n = w_or_y.shape[dim]

@@ -145,7 +145,7 @@ class TPGroup:
     def all_gather_object(self, obj) -> List:
         if not self.is_real:
             return [obj]
-        out = [None] * self.size
+        out = [None] * dist.get_world_size(self.group)
         dist.all_gather_object(out, obj, group=self.group)
         return out
 

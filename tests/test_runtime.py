@@ -49,17 +49,60 @@ def test_scheduler_budget_and_preemption(native):
     s.add(2, 8, 16)
     s.add(3, 8, 16)
     b = s.schedule()
-    assert b.ids.tolist() == [1, 2]  # token budget 16
+    assert b.kind == 1 and b.ids.tolist() == [1, 2]  # token budget 16
+    assert b.sample.tolist() == [True, True] and b.num_decode == 0
     for i in b.ids.tolist():
         s.on_token(i, False)
-    b = s.schedule()  # 3 waits: only 2 free blocks, needs 2 -> admitted
-    assert b.kind == 1 and b.ids.tolist() == [3]
-    s.on_token(3, False)
-    # all 6 blocks used; each needs a new block at token 9 -> preemption of the newest
+    b = s.schedule()  # decodes first: 1 and 2 take the last 2 blocks, 3 cannot be admitted
+    assert b.kind == 2 and b.ids.tolist() == [1, 2] and s.num_waiting() == 1
+    preempted = []
+    for _ in range(8):
+        for i in b.ids.tolist():
+            s.on_token(i, False)
+        b = s.schedule()
+        preempted += b.preempted.tolist()
+        if preempted:
+            break
+    assert preempted == [2]  # the newest running sequence is recomputed later
+    assert b.ids.tolist() == [1]
+    assert s.num_waiting() == 2
+
+
+def test_scheduler_chunked_prefill_and_mixed_steps(native):
+    s = native.Scheduler(num_blocks=64, block_size=4, max_num_seqs=4, max_batched_tokens=10, max_model_len=64)
+    s.add(1, 25, 4)
+    chunks = []
+    while True:
+        b = s.schedule()
+        assert b.kind == 1 and b.ids.tolist() == [1]
+        chunks.append((b.query_lens.tolist(), b.positions.tolist()[0], b.ctx_lens.tolist(), b.sample.tolist()))
+        if b.sample[0]:
+            break
+        assert s.num_prefilling() == 1
+    assert chunks == [([10], 0, [10], [False]), ([10], 10, [20], [False]), ([5], 20, [25], [True])]
+    s.on_token(1, False)
+    assert s.num_prefilling() == 0
+    s.add(2, 12, 4)
+    b = s.schedule()  # the decode of 1 rides along with the first chunk of 2
+    assert b.kind == 1 and b.num_decode == 1 and b.ids.tolist() == [1, 2]
+    assert b.query_lens.tolist() == [1, 9] and b.sample.tolist() == [True, False]
+    assert b.positions.tolist()[:2] == [25, 0] and b.ctx_lens.tolist() == [26, 9]
+    s.on_token(1, False)
     b = s.schedule()
-    assert b.kind == 2
-    assert 3 in b.preempted.tolist()
-    assert sorted(b.ids.tolist()) == [1, 2]
+    assert b.ids.tolist() == [1, 2] and b.query_lens.tolist() == [1, 3] and b.sample.tolist() == [True, True]
+    # slots of a chunk continue the sequence's blocks
+    bt = b.block_table[1]
+    assert b.slots.tolist()[1:] == [int(bt[p // 4]) * 4 + p % 4 for p in range(9, 12)]
+
+
+def test_scheduler_whole_prompt_mode(native):
+    s = native.Scheduler(64, 4, 4, 10, 64, -1)
+    with pytest.raises(ValueError):
+        s.add(1, 25, 4)  # longer than the per-step budget
+    s.add(2, 8, 4)
+    s.add(3, 8, 4)
+    b = s.schedule()
+    assert b.ids.tolist() == [2] and b.query_lens.tolist() == [8]  # 3 does not fit whole
 
 
 def test_scheduler_rejects_too_long(native):
