@@ -25,6 +25,8 @@ void launch_attn_decode(const void* q, int64_t q_stride, const void* kc, const v
 void launch_attn_prefill(const void* qkv, int64_t row_stride, const void* cu_seqlens, void* out, int64_t out_stride,
                          int B, int max_seqlen, int nh, int nkv, int D, int k_off, int v_off, float scale,
                          hipStream_t st);
+void launch_ce_loss(const void* logits, int64_t ld, bool fp32, const void* labels, int T, int V, void* loss,
+                    hipStream_t st);
 void launch_attn_extend(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
                         const void* block_tables, int max_blocks, const void* cu_q, const void* ctx_lens, void* out,
                         int64_t out_stride, int B, int max_qlen, int nh, int nkv, int D, int bs, float scale,
@@ -96,6 +98,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_prefill", [](uintptr_t qkv, int64_t rs, uintptr_t cu, uintptr_t out, int64_t os, int B, int maxlen,
                            int nh, int nkv, int D, int k_off, int v_off, float scale, uintptr_t st) {
     launch_attn_prefill(CP(qkv), rs, CP(cu), P(out), os, B, maxlen, nh, nkv, D, k_off, v_off, scale, S(st));
+  });
+  m.def("ce_loss", [](uintptr_t lg, int64_t ld, bool fp32, uintptr_t lab, int T, int V, uintptr_t loss, uintptr_t st) {
+    launch_ce_loss(CP(lg), ld, fp32, CP(lab), T, V, P(loss), S(st));
   });
   m.def("attn_extend", [](uintptr_t q, int64_t qs, uintptr_t kc, uintptr_t vc, uintptr_t bt, int maxb, uintptr_t cu,
                           uintptr_t cl, uintptr_t out, int64_t os, int B, int maxq, int nh, int nkv, int D, int bs,

@@ -108,11 +108,13 @@ class ModelWeights:
     extra: dict = field(default_factory=dict)
 
     def nbytes(self) -> int:
+        """Device bytes held (views sharing one allocation, like a tied embedding / head, count once)."""
         seen, tot = set(), 0
         for t in _tensors(self):
-            if t.data_ptr() not in seen:
-                seen.add(t.data_ptr())
-                tot += t.numel() * t.element_size()
+            st = t.untyped_storage()
+            if st.data_ptr() not in seen:
+                seen.add(st.data_ptr())
+                tot += st.nbytes()
         return tot
 
 
@@ -165,17 +167,25 @@ def _finish(cfg: ModelConfig, plan: ShardPlan, wte, wpe, layers_raw, lnf_w, lnf_
     # vocab-parallel head with padding
     vl = plan.v_l
     lo = plan.rank * vl
-    hw = torch.zeros(vl, cfg.hidden_size, dtype=head_w.dtype, device=head_w.device)
     n = max(0, min(cfg.vocab_size, lo + vl) - lo)
-    if n:
-        hw[:n] = head_w[lo:lo + n]
     hb = None
     if head_b is not None:
         hb = torch.zeros(vl, dtype=head_b.dtype, device=head_b.device)
         if n:
             hb[:n] = head_b[lo:lo + n]
-    mw = ModelWeights(wte=dev(wte), wpe=dev(wpe), layers=layers, lnf_w=dev(lnf_w), lnf_b=dev(lnf_b),
-                      head=lin(hw, hb))
+    if head_w is wte:
+        # tied embedding / head (GPT-2, BigCode): ONE device table [Vpadded, H]; the embedding is its
+        # first V rows and this rank's head shard is rows [lo, lo + vl) of it - no second copy in HBM
+        # (the reference loads the tied table twice, gpt_bigcode_modeling.py:564,793-797)
+        table = torch.zeros(plan.vocab_padded, cfg.hidden_size, dtype=dtype, device=device)
+        table[:cfg.vocab_size].copy_(wte.to(device=device, dtype=dtype))
+        wte_d, head = table[:cfg.vocab_size], Linear(table[lo:lo + vl], dev(hb))
+    else:
+        hw = torch.zeros(vl, cfg.hidden_size, dtype=head_w.dtype, device=head_w.device)
+        if n:
+            hw[:n] = head_w[lo:lo + n]
+        wte_d, head = dev(wte), lin(hw, hb)
+    mw = ModelWeights(wte=wte_d, wpe=dev(wpe), layers=layers, lnf_w=dev(lnf_w), lnf_b=dev(lnf_b), head=head)
     if cfg.position == "rope":
         cos, sin = ref.rope_tables(cfg.max_position_embeddings, cfg.rotary_dim, cfg.rope_theta, device)
         mw.cos, mw.sin = cos, sin
@@ -417,11 +427,17 @@ def _flat(mw: ModelWeights) -> Dict[str, torch.Tensor]:
 def save_shard(mw: ModelWeights, path: str) -> None:
     from safetensors.torch import save_file
 
-    tensors = {k: v.detach().contiguous().cpu() for k, v in _flat(mw).items()}
+    # clone: a tied head is a view of the embedding table (safetensors refuses shared storage)
+    tensors = {k: v.detach().cpu().contiguous().clone() for k, v in _flat(mw).items()}
+    meta = {"format": "llmss_amd-shard-v1", "layers": str(len(mw.layers)),
+            "glu": str(int(mw.layers[0].up.glu)) if mw.layers else "0"}
+    if mw.head.w.untyped_storage().data_ptr() == mw.wte.untyped_storage().data_ptr():
+        es = mw.wte.element_size()
+        meta["tied_head_row"] = str((mw.head.w.data_ptr() - mw.wte.data_ptr()) // (es * mw.wte.shape[1]))
+        meta["tied_table_rows"] = str(mw.wte.untyped_storage().nbytes() // (es * mw.wte.shape[1]))
     os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
     tmp = path + f".tmp{os.getpid()}"
-    save_file(tensors, tmp, metadata={"format": "llmss_amd-shard-v1", "layers": str(len(mw.layers)),
-                                      "glu": str(int(mw.layers[0].up.glu)) if mw.layers else "0"})
+    save_file(tensors, tmp, metadata=meta)
     os.replace(tmp, path)  # atomic: a concurrent reader never sees a partial file
 
 
@@ -449,8 +465,14 @@ def load_shard(cfg: ModelConfig, path: str, device, dtype) -> ModelWeights:
         layers.append(LayerWeights(get(f"l{i}.ln1_w"), get(f"l{i}.ln1_b"), get(f"l{i}.ln2_w"), get(f"l{i}.ln2_b"),
                                    lin(f"l{i}.qkv"), lin(f"l{i}.o"), lin(f"l{i}.up", glu=cfg.gated_mlp),
                                    lin(f"l{i}.down")))
-    mw = ModelWeights(wte=get("wte"), wpe=get("wpe"), layers=layers, lnf_w=get("lnf_w"), lnf_b=get("lnf_b"),
-                      head=lin("head"))
+    head, wte = lin("head"), get("wte")
+    meta = rd.metadata()
+    if "tied_head_row" in meta:  # re-tie: one [Vpadded, H] table, embedding and head shard are views of it
+        lo, rows = int(meta["tied_head_row"]), int(meta["tied_table_rows"])
+        table = torch.zeros(rows, wte.shape[1], dtype=wte.dtype, device=wte.device)
+        table[:wte.shape[0]] = wte
+        wte, head = table[:wte.shape[0]], Linear(table[lo:lo + head.w.shape[0]], head.b, head.w_scale, head.glu)
+    mw = ModelWeights(wte=wte, wpe=get("wpe"), layers=layers, lnf_w=get("lnf_w"), lnf_b=get("lnf_b"), head=head)
     if cfg.position == "rope":
         mw.cos, mw.sin = ref.rope_tables(cfg.max_position_embeddings, cfg.rotary_dim, cfg.rope_theta, device)
     return mw

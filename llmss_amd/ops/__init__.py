@@ -13,7 +13,7 @@ import torch
 from . import reference as ref
 
 __all__ = ["add_norm", "embed", "rope_cache", "attn_prefill", "attn_decode", "attn_extend", "linear", "sample", "quant_fp8_rows",
-           "rope_tables", "glu_interleave", "glu_split"]
+           "rope_tables", "glu_interleave", "glu_split", "cross_entropy"]
 
 rope_tables = ref.rope_tables
 glu_interleave = ref.glu_interleave
@@ -89,6 +89,27 @@ def sample(logits, temperature, top_k, top_p, seeds, vocab=None):
         return _hip().sample(logits, temperature, top_k, top_p, seeds, vocab)
     lg = logits if vocab is None else logits[:, :vocab]
     return ref.sample(lg, temperature, top_k, top_p, seeds)
+
+
+def cross_entropy(logits, labels, ignore_index: int = -100):
+    """Shifted LM loss (position t predicts label t+1), mean over non-ignored labels (reference
+    gptj_modeling.py:612-622). GPU: the one-pass logsumexp kernel (csrc/loss.hip)."""
+    if not logits.is_cuda:
+        return ref.cross_entropy(logits, labels)
+    V = logits.shape[-1]
+    lab = torch.full(labels.shape, -1, dtype=torch.int64, device=logits.device)
+    lab[..., :-1] = labels[..., 1:].to(logits.device)
+    lab[lab == ignore_index] = -1
+    # rows keep their (possibly vocab-padded) stride when the leading dims are uniformly strided
+    lead = logits.shape[:-1]
+    uniform = all(logits.stride(i) == logits.stride(i + 1) * logits.shape[i + 1] for i in range(logits.dim() - 2))
+    rows = torch.as_strided(logits, (lead.numel(), V), (logits.stride(-2), 1)) if uniform and logits.stride(-1) == 1 \
+        else logits.reshape(-1, V).contiguous()
+    if rows.stride(0) % 8 or rows.data_ptr() % 16:  # the kernel's 16-B row loads: pad the row stride
+        rows = torch.nn.functional.pad(rows, (0, (-V) % 8))
+    loss = _hip().ce_loss_rows(rows, lab.reshape(-1), V)
+    valid = (lab.reshape(-1) >= 0)
+    return loss.sum() / valid.sum().clamp(min=1)
 
 
 def quant_fp8_rows(w):

@@ -175,6 +175,24 @@ def attn_extend(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_qlen, nh,
     return y
 
 
+def ce_loss_rows(logits, labels, vocab=None):
+    """Per-row cross-entropy ``logsumexp(logits[t, :V]) - logits[t, label[t]]`` (0 where label < 0);
+    ``logits`` [T, >= V] bf16 or fp32 rows, ``labels`` [T] int64."""
+    T = logits.shape[0]
+    V = int(vocab or logits.shape[1])
+    _check(logits.is_cuda and logits.dim() == 2 and logits.stride(1) == 1, "logits [T, V] rows on the GPU")
+    _check(logits.device.index == torch.cuda.current_device(), "logits on the current device")
+    _check(logits.dtype in (torch.bfloat16, torch.float32), "logits must be bf16 or fp32")
+    _check(logits.stride(0) % 8 == 0 and logits.data_ptr() % 16 == 0, "logits rows 16-B aligned")
+    _check(V <= logits.shape[1], "vocab exceeds the row width")
+    _check(labels.dtype == torch.int64 and labels.is_cuda and labels.numel() == T and labels.is_contiguous(),
+           "labels [T] int64")
+    loss = torch.empty(T, dtype=torch.float32, device=logits.device)
+    lib().ce_loss(logits.data_ptr(), logits.stride(0), logits.dtype == torch.float32, labels.data_ptr(), T, V,
+                  loss.data_ptr(), _stream())
+    return loss
+
+
 class DecodeWorkspace:
     """Split-K partial buffers for decode attention (allocated once; graph-capture safe)."""
 

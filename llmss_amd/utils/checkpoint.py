@@ -79,6 +79,13 @@ class CheckpointReader:
                     raise RuntimeError(f"tensor {k} found in multiple files: {f} and {self.routing[k]}")
                 self.routing[k] = f
 
+    def metadata(self) -> Dict[str, str]:
+        """Merged ``__metadata__`` of the safetensors files."""
+        out: Dict[str, str] = {}
+        for h in self._st.values():
+            out.update(h.metadata())
+        return out
+
     # ------------------------------------------------------------------ lookup
     def resolve(self, name: str) -> str:
         if name in self.routing:

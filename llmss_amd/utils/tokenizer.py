@@ -25,15 +25,26 @@ class ByteTokenizer:
         return [self.decode(s) for s in seqs]
 
 
+_TOKENIZER_FILES = ("tokenizer.json", "tokenizer_config.json", "vocab.json", "merges.txt", "tokenizer.model",
+                    "spiece.model", "vocab.txt")
+
+
 def load_tokenizer(path: str, vocab_size: int = 256):
+    """HF tokenizer of a checkpoint directory; the byte tokenizer ONLY for synthetic presets and
+    checkpoint directories that ship no tokenizer files (logged). A directory whose tokenizer files
+    exist but fail to load raises: silently decoding garbage through the byte fallback would hide it."""
+    from .logging import get_logger
+
     if os.path.isdir(path):
-        try:
+        present = [f for f in _TOKENIZER_FILES if os.path.exists(os.path.join(path, f))]
+        if present:
             from transformers import AutoTokenizer
 
-            tok = AutoTokenizer.from_pretrained(path, padding_side="left", truncation_side="left")
-            return tok
-        except Exception:  # no tokenizer files in the checkpoint dir
-            pass
+            try:
+                return AutoTokenizer.from_pretrained(path, padding_side="left", truncation_side="left")
+            except Exception as e:
+                raise RuntimeError(f"tokenizer files {present} in {path} could not be loaded: {e}") from e
+        get_logger(__name__).warning("%s has no tokenizer files: using the byte-level tokenizer", path)
     return ByteTokenizer(vocab_size)
 
 

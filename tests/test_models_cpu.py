@@ -122,3 +122,18 @@ def test_shard_cache_roundtrip(tmp_path, name):
                     last_idx=torch.tensor([4]))
     kv1, kv2 = m1.allocate_kv_cache(4, 4), m2.allocate_kv_cache(4, 4)
     assert torch.equal(m1(inp, kv1), m2(inp, kv2))
+
+
+@pytest.mark.parametrize("tp,rank", [(1, 0), (2, 1)])
+def test_tied_head_shares_the_embedding_table(tp, rank):
+    cfg = get_preset("gpt2", num_layers=1)
+    assert cfg.tie_word_embeddings
+    w = random_weights(cfg, tp=tp, rank=rank, dtype=torch.float32)
+    plan = shard_plan(cfg, tp, rank)
+    assert w.head.w.untyped_storage().data_ptr() == w.wte.untyped_storage().data_ptr()
+    lo = rank * plan.v_l
+    n = min(cfg.vocab_size, lo + plan.v_l) - lo
+    assert torch.equal(w.head.w[:n], w.wte[lo:lo + n]) and w.head.w[n:].abs().sum() == 0
+    table = plan.vocab_padded * cfg.hidden_size * 4
+    assert w.nbytes() < table + sum(t.numel() * 4 for L in w.layers for t in (L.qkv.w, L.o.w, L.up.w, L.down.w)) * 1.01 \
+        + (w.wpe.numel() * 4) + 10 * cfg.hidden_size * 4 * 8

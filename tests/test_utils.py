@@ -64,3 +64,19 @@ def test_phase_timer_cpu_noop():
         with trace_range("inner"):
             pass
     assert t.summary() == {}
+
+
+def test_tokenizer_fallback_is_explicit(tmp_path):
+    import pytest
+
+    from llmss_amd.utils.tokenizer import ByteTokenizer, load_tokenizer
+
+    assert isinstance(load_tokenizer("llama2-7b"), ByteTokenizer)  # preset name: synthetic model
+    empty = tmp_path / "no_tok"
+    empty.mkdir()
+    assert isinstance(load_tokenizer(str(empty)), ByteTokenizer)  # checkpoint without tokenizer files
+    broken = tmp_path / "broken"
+    broken.mkdir()
+    (broken / "tokenizer.json").write_text("{not json")
+    with pytest.raises(RuntimeError):
+        load_tokenizer(str(broken))
