@@ -113,7 +113,7 @@ def run_config(args, model_name, tp, batch, progress, dp=False):
             torch.distributed.barrier()
 
     progress(f"engine ready: {model.cfg.model_type} {'dp' if dp else 'tp'}={world} batch={batch} "
-             f"kv_blocks={eng.num_blocks} graphs={sorted(eng.graphs)}")
+             f"kv_blocks={eng.num_blocks} graphs={sorted({b for b, _ in eng.graphs})}")
     if eng.tuned:
         mx = max(m for _, m in eng.tuned)
         progress("autotuned GEMMs at M=%d: " % mx + ", ".join(

@@ -25,6 +25,10 @@ void launch_attn_decode(const void* q, int64_t q_stride, const void* kc, const v
 void launch_attn_prefill(const void* qkv, int64_t row_stride, const void* cu_seqlens, void* out, int64_t out_stride,
                          int B, int max_seqlen, int nh, int nkv, int D, int k_off, int v_off, float scale,
                          hipStream_t st);
+void launch_cand_topk(const void* logits, int64_t ld, int B, int vl, int lo, int V, const void* temperature,
+                      const void* top_k, int K, int KC, void* pack, int64_t ldp, hipStream_t st);
+void launch_sample_cand(const void* pack, int64_t ldp, int B, int groups, int KC, const void* temperature,
+                        const void* top_k, const void* top_p, const void* seeds, void* out, void* out2, hipStream_t st);
 void launch_ce_loss(const void* logits, int64_t ld, bool fp32, const void* labels, int T, int V, void* loss,
                     hipStream_t st);
 void launch_attn_extend(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
@@ -98,6 +102,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_prefill", [](uintptr_t qkv, int64_t rs, uintptr_t cu, uintptr_t out, int64_t os, int B, int maxlen,
                            int nh, int nkv, int D, int k_off, int v_off, float scale, uintptr_t st) {
     launch_attn_prefill(CP(qkv), rs, CP(cu), P(out), os, B, maxlen, nh, nkv, D, k_off, v_off, scale, S(st));
+  });
+  m.def("cand_topk", [](uintptr_t lg, int64_t ld, int B, int vl, int lo, int V, uintptr_t temp, uintptr_t topk, int K,
+                        int KC, uintptr_t pack, int64_t ldp, uintptr_t st) {
+    launch_cand_topk(CP(lg), ld, B, vl, lo, V, CP(temp), CP(topk), K, KC, P(pack), ldp, S(st));
+  });
+  m.def("sample_cand", [](uintptr_t pack, int64_t ldp, int B, int groups, int KC, uintptr_t temp, uintptr_t topk,
+                          uintptr_t topp, uintptr_t seeds, uintptr_t out, uintptr_t out2, uintptr_t st) {
+    launch_sample_cand(CP(pack), ldp, B, groups, KC, CP(temp), CP(topk), CP(topp), CP(seeds), P(out), P(out2), S(st));
   });
   m.def("ce_loss", [](uintptr_t lg, int64_t ld, bool fp32, uintptr_t lab, int T, int V, uintptr_t loss, uintptr_t st) {
     launch_ce_loss(CP(lg), ld, fp32, CP(lab), T, V, P(loss), S(st));

@@ -438,3 +438,254 @@ void launch_sample(const void* logits, int64_t ld, bool fp32_logits, int B, int 
                                               (int64_t*)out, (int64_t*)out2);
   HIP_CHECK_LAUNCH();
 }
+
+// ---------------------------------------------------------------------------------------------
+// Distributed (vocab-parallel) sampling for tensor parallelism. Reference: the LM head output is
+// all-gathered as full [B, V] logits and rank 0 samples (layers.py:106-135, generate.py:109-144);
+// the v3 path above still needs the gathered row. Here each rank reduces its [B, V/tp] shard to
+// at most KC candidates per row (every element whose scaled logit is >= the shard's K-th largest,
+// ties included), the ranks all-gather those [B, tp, KC] (value, global index) pairs - KBs instead
+// of the full logits - and every rank runs the v3 selection (top-k boundary, fixed-point top-p
+// mass, Philox Gumbel-max keyed by the GLOBAL token index) on the union. For greedy rows and rows
+// with 1 <= top_k <= K the global kept set is inside that union, so the token equals the v3
+// sampler's on the gathered row bit for bit (same mx, same masses, same noise).
+// ---------------------------------------------------------------------------------------------
+constexpr int CAND_THREADS = 1024;
+
+// parallel "first digit from the top whose inclusive count reaches target" over 256 bins held in
+// LDS (cnt), by the first 256 threads; writes the digit and the count strictly above it
+__device__ void cand_find_digit(const unsigned* cnt, unsigned target, int* out_digit, unsigned* out_above,
+                                unsigned* wsum) {
+  const int t = threadIdx.x;
+  unsigned v = 0, inc = 0;
+  if (t < 256) {
+    v = cnt[255 - t];  // descending digits
+    inc = v;
+    const int lane = t & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) wsum[t >> 6] = inc;
+  }
+  __syncthreads();
+  if (t < 256) {
+    unsigned off = 0;
+    for (int w = 0; w < (t >> 6); ++w) off += wsum[w];
+    const unsigned excl = off + inc - v;
+    if (excl < target && excl + v >= target) {
+      *out_digit = 255 - t;
+      *out_above = excl;
+    }
+  }
+  __syncthreads();
+}
+
+template <int EPT>
+__global__ __launch_bounds__(CAND_THREADS) void cand_topk_kernel(const bf16_t* __restrict__ logits, int64_t ld,
+                                                                 int vl, int lo, int V,
+                                                                 const float* __restrict__ temperature,
+                                                                 const int* __restrict__ top_k, int K, int KC,
+                                                                 float* __restrict__ pack, int64_t ldp) {
+  __shared__ unsigned hist[256];
+  __shared__ unsigned wsum[4];
+  __shared__ int digit;
+  __shared__ unsigned above;
+  __shared__ int nout;
+  const int b = blockIdx.x, t = threadIdx.x;
+  const float temp = temperature ? temperature[b] : 0.f;
+  const int k = top_k ? top_k[b] : 0;
+  const bool greedy = !(temp > 0.f) || k == 1;
+  const float scale = greedy ? 1.f : 1.f / temp;
+  const bf16_t* row = logits + (int64_t)b * ld;
+  float x[EPT];
+  unsigned key[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int j = t + e * CAND_THREADS;
+    const bool ok = j < vl && lo + j < V;
+    x[e] = ok ? bf2f(row[j]) * scale : -INFINITY;
+    key[e] = ok ? fkey(x[e]) : 0u;  // 0 = below every real key
+  }
+  // K-th largest key by 4 passes of 8-bit radix select (counts are exact integers)
+  unsigned prefix = 0, mask = 0, target = (unsigned)K;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    if (t < 256) hist[t] = 0u;
+    if (t == 0) { digit = 0; above = 0u; }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < EPT; ++e)
+      if (key[e] != 0u && (key[e] & mask) == prefix) atomicAdd(&hist[(key[e] >> shift) & 255], 1u);
+    __syncthreads();
+    cand_find_digit(hist, target, &digit, &above, wsum);
+    const int d = digit;
+    const unsigned a = above;
+    __syncthreads();  // every thread has read digit / above before thread 0 resets them for the next pass
+    target -= a;
+    prefix |= (unsigned)d << shift;
+    mask |= 255u << shift;
+  }
+  // prefix = K-th largest key (or 0 when the shard has fewer than K elements: keep all)
+  if (t == 0) nout = 0;
+  __syncthreads();
+  const unsigned kth = prefix;
+  // packed row: KC values then KC global indices (one tensor, one all-gather)
+  float* ov = pack + (int64_t)b * ldp;
+  int* oi = reinterpret_cast<int*>(ov + KC);
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    if (key[e] != 0u && key[e] >= kth) {
+      const int s = atomicAdd(&nout, 1);
+      if (s < KC) {
+        ov[s] = x[e];
+        oi[s] = lo + t + e * CAND_THREADS;
+      }
+    }
+  }
+  __syncthreads();
+  for (int s = nout + t; s < KC; s += CAND_THREADS) {  // unused slots
+    ov[s] = -INFINITY;
+    oi[s] = 0x7fffffff;
+  }
+}
+
+constexpr int SCAND_MAX = 2048;  // gathered candidates per row (tp * KC)
+
+__global__ __launch_bounds__(256) void sample_cand_kernel(const float* __restrict__ pack, int64_t ldp, int groups,
+                                                          int KC, const float* __restrict__ temperature,
+                                                          const int* __restrict__ top_k,
+                                                          const float* __restrict__ top_p,
+                                                          const int64_t* __restrict__ seeds,
+                                                          int64_t* __restrict__ out, int64_t* __restrict__ out2) {
+  __shared__ float v[SCAND_MAX];
+  __shared__ int id[SCAND_MAX];
+  __shared__ float sv[SCAND_MAX];  // sorted (value desc, index asc)
+  __shared__ int sid[SCAND_MAX];
+  __shared__ float red[8];
+  __shared__ int redi[8];
+  __shared__ float thr_s;
+  __shared__ int nvalid;
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int N = groups * KC;
+  const float temp = temperature ? temperature[b] : 0.f;
+  const int k = top_k ? top_k[b] : 0;
+  const float p = top_p ? top_p[b] : 1.f;
+  const bool greedy = !(temp > 0.f) || k == 1;
+  if (t == 0) nvalid = 0;
+  __syncthreads();
+  const float* row = pack + (int64_t)b * ldp;  // [groups][KC values | KC indices]
+  for (int i = t; i < N; i += 256) {
+    const int g = i / KC, s = i - g * KC;
+    v[i] = row[(int64_t)g * 2 * KC + s];
+    id[i] = reinterpret_cast<const int*>(row)[(int64_t)g * 2 * KC + KC + s];
+    if (v[i] > -INFINITY) atomicAdd(&nvalid, 1);
+  }
+  __syncthreads();
+  float thr = -INFINITY;
+  if (!greedy) {
+    float mx = -INFINITY;
+    for (int i = t; i < N; i += 256) mx = fmaxf(mx, v[i]);
+    mx = block_max(mx, red);
+    // exact ranks (value desc, global index asc) -> sorted copy
+    for (int i = t; i < N; i += 256) {
+      const float a = v[i];
+      const int ai = id[i];
+      if (!(a > -INFINITY)) continue;
+      int r = 0;
+      for (int j = 0; j < N; ++j) {
+        const float c = v[j];
+        r += (c > a || (c == a && id[j] < ai)) ? 1 : 0;
+      }
+      sv[r] = a;
+      sid[r] = ai;
+    }
+    __syncthreads();
+    if (t == 0) {
+      const int n = nvalid;  // sv[0, n) holds every real candidate in order
+      float th = -INFINITY;
+      if (k > 0 && k <= n) th = sv[k - 1];  // top-k boundary value (ties at it are kept)
+      if (p < 1.f) {
+        unsigned long long z = 0;
+        int m = 0;
+        for (; m < n && sv[m] >= th; ++m) z += sv3_mass(sv[m], mx);
+        unsigned long long target = (unsigned long long)((double)p * (double)z);
+        if (target < 1ull) target = 1ull;
+        unsigned long long cum = 0;
+        float tp = sv[m > 0 ? m - 1 : 0];
+        for (int r = 0; r < m; ++r) {
+          const unsigned long long hi = cum + sv3_mass(sv[r], mx);
+          if (cum < target && hi >= target) {
+            tp = sv[r];
+            break;
+          }
+          cum = hi;
+        }
+        th = fmaxf(th, tp);
+      }
+      thr_s = th;
+    }
+    __syncthreads();
+    thr = thr_s;
+  }
+  const unsigned long long seed = seeds ? (unsigned long long)seeds[b] : 0ull;
+  const unsigned s0 = (unsigned)seed, s1 = (unsigned)(seed >> 32);
+  float best = -INFINITY;
+  int besti = 0x7fffffff;
+  for (int i = t; i < N; i += 256) {
+    float x = v[i];
+    const int idx = id[i];
+    if (!(x > -INFINITY)) continue;
+    if (!greedy) {
+      if (x < thr) continue;
+      const unsigned r = philox((unsigned)idx, 0u, s0, s1);
+      const float u = ((float)(r >> 8) + 0.5f) * (1.0f / 16777216.0f);
+      x = x - __logf(-__logf(u));
+    }
+    if (x > best || (x == best && idx < besti)) { best = x; besti = idx; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(besti, o, 64);
+    if (ob > best || (ob == best && oi < besti)) { best = ob; besti = oi; }
+  }
+  __syncthreads();
+  if ((t & 63) == 0) { red[t >> 6] = best; redi[t >> 6] = besti; }
+  __syncthreads();
+  if (t == 0) {
+    float bb = red[0];
+    int bi = redi[0];
+    for (int i = 1; i < 4; ++i)
+      if (red[i] > bb || (red[i] == bb && redi[i] < bi)) { bb = red[i]; bi = redi[i]; }
+    if (bi == 0x7fffffff) bi = 0;
+    out[b] = bi;
+    if (out2) out2[b] = bi;
+  }
+}
+
+void launch_cand_topk(const void* logits, int64_t ld, int B, int vl, int lo, int V, const void* temperature,
+                      const void* top_k, int K, int KC, void* pack, int64_t ldp, hipStream_t st) {
+  if (B == 0) return;
+  if (K < 1 || KC < K) throw std::runtime_error("cand_topk: need 1 <= K <= KC");
+  const int ept = (vl + CAND_THREADS - 1) / CAND_THREADS;
+#define CT(E_)                                                                                                    \
+  cand_topk_kernel<E_><<<B, CAND_THREADS, 0, st>>>((const bf16_t*)logits, ld, vl, lo, V, (const float*)temperature, \
+                                                   (const int*)top_k, K, KC, (float*)pack, ldp)
+  if (ept <= 4) CT(4);
+  else if (ept <= 8) CT(8);
+  else if (ept <= 16) CT(16);
+  else throw std::runtime_error("cand_topk: vocab shard wider than 16384 (use the gathered-logits sampler)");
+#undef CT
+  HIP_CHECK_LAUNCH();
+}
+
+void launch_sample_cand(const void* pack, int64_t ldp, int B, int groups, int KC, const void* temperature,
+                        const void* top_k, const void* top_p, const void* seeds, void* out, void* out2, hipStream_t st) {
+  if (B == 0) return;
+  if (groups * KC > SCAND_MAX) throw std::runtime_error("sample_cand: too many candidates per row");
+  sample_cand_kernel<<<B, 256, 0, st>>>((const float*)pack, ldp, groups, KC, (const float*)temperature,
+                                        (const int*)top_k, (const float*)top_p, (const int64_t*)seeds, (int64_t*)out,
+                                        (int64_t*)out2);
+  HIP_CHECK_LAUNCH();
+}

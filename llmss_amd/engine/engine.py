@@ -174,7 +174,13 @@ class LLMEngine:
         self.use_graphs = self.is_gpu if use_graphs is None else (use_graphs and self.is_gpu)
         if self.tp.is_real and self.tp.host_staged:  # gloo-staged device collectives cannot be captured
             self.use_graphs = False
-        self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}  # (batch bucket, candidate sampler) -> graph
+        # vocab-parallel sampling from per-rank candidates (SURVEY R11 "better"): greedy / top-k <= 64 rows
+        # gather [B, tp, 128] (value, id) pairs instead of [B, V] logits; LLMSS_DIST_SAMPLER=0 disables
+        from ..ops.hip import CAND_MAX_SHARD
+
+        self.dist_sampling = (self.tp.size > 1 and os.environ.get("LLMSS_DIST_SAMPLER", "1") != "0"
+                              and (not self.is_gpu or model.plan.v_l <= CAND_MAX_SHARD))
         self.buckets = sorted(set(graph_buckets or self._default_buckets()))
         self.buckets = [b for b in self.buckets if b <= max_num_seqs] or [max_num_seqs]
         if self.buckets[-1] < max_num_seqs:
@@ -215,6 +221,7 @@ class LLMEngine:
                 "max_num_seqs": self.max_num_seqs, "max_batched_tokens": self.max_batched_tokens,
                 "buckets": list(self.buckets), "graphs": bool(self.use_graphs),
                 "async_decode": self.async_decode, "eos": self.eos, "prefill_chunk": self.prefill_chunk,
+                "dist_sampling": self.dist_sampling,
                 "overlap_rows": self.model.overlap_rows, "tbo_min": self.model.tbo_min,
                 "fp8": any(L.qkv.w_scale is not None for L in self.model.w.layers[:1])}
 
@@ -419,23 +426,40 @@ class LLMEngine:
             block_tables=d(batch.block_table.astype(np.int32)) if kind == "extend" else None,
             ctx_lens=d(ctx.astype(np.int32)) if kind == "extend" else None, max_ctx=self.max_model_len,
             num_decode=nd, has_prefix=has_prefix)
-        logits = self.model(inp, self.kv)
         reqs = [r for r, f in zip(reqs, smp) if f]
         if not reqs:
+            self.model.hidden_states(inp, self.kv)  # prompt chunks only: fill the cache, nothing to sample
             return []
         temp, topk, topp, seeds = self._sampling_arrays(reqs)
-        tok = ops.sample(logits, torch.from_numpy(temp).to(dev), torch.from_numpy(topk).to(dev),
-                         torch.from_numpy(topp).to(dev), torch.from_numpy(seeds).to(dev),
-                         vocab=min(self.cfg.vocab_size, logits.shape[-1]))
+        tok = self._forward_sample(inp, *(torch.from_numpy(a).to(dev) for a in (temp, topk, topp, seeds)),
+                                   dist=self._dist_ok(temp, topk))
         return tok.cpu().tolist()
 
-    def _decode_forward(self, b: int, buf: _DecodeBuffers):
+    def _dist_ok(self, temp, topk) -> bool:
+        """Sample this step from vocab-parallel candidates (no [B, V] logits all-gather)?"""
+        return self.dist_sampling and ops.cand_ok(temp, topk)
+
+    def _forward_sample(self, inp: StepInput, temp, topk, topp, seeds, out=None, dist=False):
+        """Forward + LM head + sampler. ``dist``: each rank keeps its logit shard and only candidates
+        are gathered (ops.sample_distributed); otherwise the [B, V] logits are all-gathered."""
+        m = self.model
+        V = self.cfg.vocab_size
+        if dist:
+            h = m.hidden_states(inp, self.kv)
+            if inp.last_idx is not None:
+                h = h.index_select(0, inp.last_idx)
+            return ops.sample_distributed(m.local_logits(h), self.tp, m.vocab_lo, V, temp, topk, topp, seeds, out=out)
+        logits = m(inp, self.kv)
+        if logits.is_cuda:
+            return _hip_ops.sample(logits, temp, topk, topp, seeds, vocab=min(V, logits.shape[-1]), out=out)
+        return ops.sample(logits, temp, topk, topp, seeds, vocab=min(V, logits.shape[-1]))
+
+    def _decode_forward(self, b: int, buf: _DecodeBuffers, dist: bool = False):
         inp = StepInput(kind="decode", input_ids=buf.ids[:b], positions=buf.pos[:b], slots=buf.slots[:b],
                         block_tables=buf.bt[:b], ctx_lens=buf.ctx[:b], max_ctx=self.max_model_len,
                         decode_splits=self._splits(b))
-        logits = self.model(inp, self.kv)
-        _hip_ops.sample(logits, buf.temp[:b], buf.topk[:b], buf.topp[:b], buf.seeds[:b],
-                        vocab=min(self.cfg.vocab_size, logits.shape[-1]), out=buf.out[:b])
+        self._forward_sample(inp, buf.temp[:b], buf.topk[:b], buf.topp[:b], buf.seeds[:b], out=buf.out[:b],
+                             dist=dist)
 
     def _decode_cpu(self, batch, reqs: List[Request]) -> List[int]:
         ids = np.array([r.last_id for r in reqs], dtype=np.int64)
@@ -444,8 +468,7 @@ class LLMEngine:
                         slots=torch.from_numpy(batch.slots),
                         block_tables=torch.from_numpy(batch.block_table.astype(np.int32)),
                         ctx_lens=torch.from_numpy(batch.ctx_lens.astype(np.int32)), max_ctx=self.max_model_len)
-        logits = self.model(inp, self.kv)
-        return ops.sample(logits, temp, topk, topp, seeds, vocab=min(self.cfg.vocab_size, logits.shape[-1])).tolist()
+        return self._forward_sample(inp, temp, topk, topp, seeds, dist=self._dist_ok(temp, topk)).tolist()
 
     # ------------------------------------------------------------------ pipelined GPU decode
     def _record_from_batch(self, batch, ids: np.ndarray, reqs: List[Request]) -> dict:
@@ -467,6 +490,7 @@ class LLMEngine:
                  "last": np.array([r.last_id for r in reqs], dtype=np.int64)}
         c.update(ids=ids, reqs=reqs, n=len(reqs), pos=batch.positions, ctx=batch.ctx_lens.astype(np.int32),
                  slots=batch.slots, bt=batch.block_table, keep=np.ones(len(reqs), dtype=bool))
+        c["dist"] = self._dist_ok(c["temp"], c["topk"])
         return c
 
     def _launch_decode(self, rec: dict, device_ids: bool = False):
@@ -480,10 +504,11 @@ class LLMEngine:
             buf.fill(k, b, None if device_ids else rec.pop("last"), rec["pos"], rec["slots"],
                      step_seeds(rec["seed"], rec["nout"]), rec["ctx"], rec["topk"], rec["bt"], rec["temp"],
                      rec["topp"])
-            if self.use_graphs and b in self.graphs:
-                self.graphs[b].replay()
+            key = (b, bool(rec["dist"]))
+            if self.use_graphs and key in self.graphs:
+                self.graphs[key].replay()
             else:
-                self._decode_forward(b, buf)
+                self._decode_forward(b, buf, dist=key[1])
             buf.h_out[k][:n].copy_(buf.out[:n], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
@@ -499,7 +524,7 @@ class LLMEngine:
         if (nxt_pos[alive] % self.block_size == 0).any():  # a sequence enters a new KV block
             return
         dead = ~alive
-        rec = {k: cur[k] for k in ("ids", "reqs", "n", "temp", "topk", "topp", "seed", "maxnew", "bt")}
+        rec = {k: cur[k] for k in ("ids", "reqs", "n", "temp", "topk", "topp", "seed", "maxnew", "bt", "dist")}
         rec["pos"] = nxt_pos
         rec["ctx"] = np.where(alive, cur["ctx"] + 1, 0).astype(np.int32)
         rec["slots"] = np.where(alive, cur["slots"] + 1, -1)
@@ -558,21 +583,27 @@ class LLMEngine:
         buf.d_i32.zero_()
         buf.topk.fill_(1)
         buf.d_f32.zero_()
+        # vocab-parallel runs: graphs for both samplers (candidates when every row allows it, else the
+        # gathered-logits sampler), chosen per step
+        modes = (True, False) if self.dist_sampling else (False,)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for b in reversed(self.buckets):
-                for _ in range(2):
-                    self._decode_forward(b, buf)
+                for d in modes:
+                    for _ in range(2):
+                        self._decode_forward(b, buf, dist=d)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         for b in reversed(self.buckets):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
-                self._decode_forward(b, buf)
-            self.graphs[b] = g
+            for d in modes:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    self._decode_forward(b, buf, dist=d)
+                self.graphs[(b, d)] = g
         torch.cuda.synchronize()
-        log.info("captured %d decode graphs: %s", len(self.graphs), self.buckets)
+        log.info("captured %d decode graphs: buckets %s, samplers %s", len(self.graphs), self.buckets,
+                 ["candidates" if d else "gathered" for d in modes])
 
     # -------------------------------------------------------------------------- offline API
     def generate(self, prompts: Iterable[Sequence[int]], params=None) -> List[List[int]]:

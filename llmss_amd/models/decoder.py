@@ -297,6 +297,15 @@ class DecoderLM:
         h, _ = ops.add_norm(delta, w.lnf_w, w.lnf_b, eps, rms, residual)
         return h
 
+    @property
+    def vocab_lo(self) -> int:
+        """Global token id of this rank's first LM-head row (vocab-parallel shard)."""
+        return self.plan.rank * self.plan.v_l
+
+    def local_logits(self, h: torch.Tensor) -> torch.Tensor:
+        """[B, H] -> this rank's [B, Vpadded / tp] logit shard (no gather)."""
+        return self.w.head(h)
+
     def logits(self, h: torch.Tensor) -> torch.Tensor:
         """[B, H] -> full-vocab logits [B, Vpadded] (all-gathered across TP ranks)."""
         local = self.w.head(h)

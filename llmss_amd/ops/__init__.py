@@ -112,6 +112,33 @@ def cross_entropy(logits, labels, ignore_index: int = -100):
     return loss.sum() / valid.sum().clamp(min=1)
 
 
+CAND_K = 64
+CAND_KC = 128
+
+
+def cand_ok(temperature, top_k) -> bool:
+    """Rows the vocab-parallel candidate sampler reproduces exactly: greedy, or 1 <= top_k <= CAND_K."""
+    import numpy as np
+
+    t = np.asarray(temperature, dtype=np.float32)
+    k = np.asarray(top_k, dtype=np.int64)
+    return bool(np.all(~(t > 0) | (k == 1) | ((k >= 1) & (k <= CAND_K))))
+
+
+def sample_distributed(local, tp, lo, V, temperature, top_k, top_p, seeds, out=None):
+    """Vocab-parallel sampling without gathering logits: per-rank candidates -> all-gather -> select.
+    ``local`` = this rank's [B, V/tp] logit shard whose first column is global token ``lo``."""
+    if local.is_cuda:
+        h = _hip()
+        pack = h.cand_topk(local, lo, V, temperature, top_k)
+        allp = tp.all_gather_last_dim(pack)
+        return h.sample_cand(allp, h.CAND_KC, temperature, top_k, top_p, seeds, out=out)
+    pack = ref.cand_topk(local, lo, V, temperature, top_k, CAND_K, CAND_KC)
+    allp = tp.all_gather_last_dim(pack)
+    y = ref.sample_cand(allp, allp.shape[1] // (2 * CAND_KC), CAND_KC, temperature, top_k, top_p, seeds, V)
+    return _into(y, out)
+
+
 def quant_fp8_rows(w):
     if w.is_cuda:
         return _hip().quant_fp8_rows(w)

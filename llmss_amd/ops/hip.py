@@ -468,6 +468,41 @@ def quant_fp8_rows(w):
 
 
 # ---------------------------------------------------------------------------------- sampler
+CAND_K = 64  # rows with 1 <= top_k <= CAND_K (or greedy) can be sampled from gathered candidates
+CAND_KC = 128  # candidate slots per rank and row (>= CAND_K: ties at the K-th value ride along)
+CAND_MAX_SHARD = 16384  # widest vocab shard the candidate kernel takes
+
+
+def cand_topk(local, lo, V, temperature, top_k, K=CAND_K, KC=CAND_KC, out=None):
+    """Per-rank candidates of a vocab-parallel logit shard: [B, 2*KC] fp32 (KC scaled values, then KC
+    global token ids as int32 bits)."""
+    _bf16_rows(local, "local logits")
+    B, vl = local.shape
+    _check(vl <= CAND_MAX_SHARD, "vocab shard too wide for the candidate sampler")
+    for t, dt, nm in ((temperature, torch.float32, "temperature"), (top_k, torch.int32, "top_k")):
+        _check(t.dtype == dt and t.numel() >= B and t.is_contiguous() and t.is_cuda, f"{nm} must be {dt}")
+    pack = out if out is not None else torch.empty(B, 2 * KC, dtype=torch.float32, device=local.device)
+    _check(pack.shape == (B, 2 * KC) and pack.is_contiguous() and pack.dtype == torch.float32, "candidate pack")
+    lib().cand_topk(local.data_ptr(), local.stride(0), B, vl, int(lo), int(V), temperature.data_ptr(),
+                    top_k.data_ptr(), int(K), int(KC), pack.data_ptr(), pack.stride(0), _stream())
+    return pack
+
+
+def sample_cand(pack, KC, temperature, top_k, top_p, seeds, out=None, out2=None):
+    """Sample from gathered candidates ``pack`` [B, groups * 2*KC] (rank-major)."""
+    _check(pack.is_cuda and pack.dtype == torch.float32 and pack.dim() == 2 and pack.stride(1) == 1, "pack")
+    B = pack.shape[0]
+    _check(pack.shape[1] % (2 * KC) == 0, "pack width must be a multiple of 2*KC")
+    groups = pack.shape[1] // (2 * KC)
+    for t, dt, nm in ((temperature, torch.float32, "temperature"), (top_k, torch.int32, "top_k"),
+                      (top_p, torch.float32, "top_p"), (seeds, torch.int64, "seeds")):
+        _check(t.dtype == dt and t.numel() >= B and t.is_contiguous() and t.is_cuda, f"{nm} must be {dt}")
+    y = out if out is not None else torch.empty(B, dtype=torch.int64, device=pack.device)
+    lib().sample_cand(pack.data_ptr(), pack.stride(0), B, groups, int(KC), temperature.data_ptr(), top_k.data_ptr(),
+                      top_p.data_ptr(), seeds.data_ptr(), y.data_ptr(), _ptr(out2), _stream())
+    return y
+
+
 def sample(logits, temperature, top_k, top_p, seeds, vocab: Optional[int] = None, out=None, out2=None):
     _check(logits.is_cuda and logits.dim() == 2 and logits.stride(1) == 1, "logits [B, V]")
     _check(logits.dtype in (torch.bfloat16, torch.float32), "logits bf16/fp32")

@@ -10,6 +10,7 @@ from __future__ import annotations
 import math
 from typing import Optional, Tuple
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -226,39 +227,119 @@ def quant_fp8_rows(w: torch.Tensor):
     return q, scale
 
 
+# ---------------------------------------------------------------------------------------- sampling
+# CPU definition of the GPU sampler (csrc/sampling.hip sample_v3 / sample_cand): temperature ->
+# top-k -> top-p -> Gumbel-max with Philox-4x32-10 noise keyed by (row seed, global token index).
+# Top-p mass is summed as 2^-32 fixed-point integers, so the kept set does not depend on summation
+# order - which is what lets a vocab-parallel (candidate) evaluation reproduce the full-row result.
+def philox(idx: np.ndarray, seed: int) -> np.ndarray:
+    """Philox-4x32-10 first output word for counters (idx, 0, 0, 0) and key = 64-bit seed."""
+    m = np.uint64(0xFFFFFFFF)
+    c0 = idx.astype(np.uint64) & m
+    c1 = np.zeros_like(c0)
+    c2 = np.zeros_like(c0)
+    c3 = np.zeros_like(c0)
+    k0, k1 = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
+    for _ in range(10):
+        p0 = np.uint64(0xD2511F53) * c0
+        p1 = np.uint64(0xCD9E8D57) * c2
+        h0, l0, h1, l1 = p0 >> np.uint64(32), p0 & m, p1 >> np.uint64(32), p1 & m
+        c0, c1, c2, c3 = (h1 ^ c1 ^ k0) & m, l1, (h0 ^ c3 ^ k1) & m, l0
+        k0, k1 = (k0 + np.uint64(0x9E3779B9)) & m, (k1 + np.uint64(0xBB67AE85)) & m
+    return c0
+
+
+def _mass(x: np.ndarray, mx: np.float32) -> np.ndarray:
+    return (np.exp((x - mx).astype(np.float32)).astype(np.float32) * np.float32(4294967296.0)).astype(np.uint64)
+
+
+def _select(x: np.ndarray, idx: np.ndarray, t: float, k: int, p: float, seed: int, V: int) -> int:
+    """One row: x = scaled logits of the (candidate) elements, idx their global token ids."""
+    valid = np.isfinite(x) | (x > -np.inf)
+    x, idx = x[valid], idx[valid]
+    if x.size == 0:
+        return 0
+    greedy = not t > 0 or k == 1
+    thr = -np.inf
+    if not greedy:
+        order = np.lexsort((idx, -x))  # value desc, index asc
+        xs = x[order]
+        mx = np.float32(xs[0])
+        if 0 < k < V and k <= xs.size:
+            thr = xs[k - 1]
+        if p < 1.0:
+            kept = xs[xs >= thr]
+            m = _mass(kept, mx)
+            z = int(m.sum(dtype=np.uint64))
+            target = max(1, int(float(p) * float(z)))
+            cum = np.cumsum(m, dtype=np.uint64)
+            j = int(np.searchsorted(cum, np.uint64(target), side="left"))
+            tp = kept[min(j, kept.size - 1)]
+            thr = max(thr, tp)
+    v = x.astype(np.float32)
+    if not greedy:
+        keep = x >= thr
+        v, idx = v[keep], idx[keep]
+        r = philox(idx, seed)
+        u = ((r >> np.uint64(8)).astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 16777216.0)
+        v = (v - np.log(-np.log(u))).astype(np.float32)
+    best = v.max()
+    return int(idx[v == best].min())
+
+
 def sample(logits: torch.Tensor, temperature, top_k, top_p, seeds, generator=None) -> torch.Tensor:
-    """Reference sampler: temperature -> top-k -> top-p -> multinomial (argmax if temp <= 0)."""
+    """Full-row sampler (the GPU ``sample_v3`` definition): temperature -> top-k -> top-p -> Gumbel-max."""
     B, V = logits.shape
-    out = torch.empty(B, dtype=torch.long, device=logits.device)
+    lg = logits.detach().float().cpu().numpy()
+    out = torch.empty(B, dtype=torch.long)
     for b in range(B):
-        row = logits[b].float()
         t = float(temperature[b]) if temperature is not None else 0.0
         k = int(top_k[b]) if top_k is not None else 0
         p = float(top_p[b]) if top_p is not None else 1.0
-        if not t > 0 or k == 1:
-            out[b] = int(torch.argmax(row))
-            continue
-        x = row / t
-        if 0 < k < V:
-            kth = torch.topk(x, k).values[-1]
-            x = x.masked_fill(x < kth, float("-inf"))
-        if p < 1.0:
-            probs = torch.softmax(x, -1)
-            sp, si = probs.sort(descending=True)
-            cum = sp.cumsum(0)
-            keep = cum - sp < p  # keep tokens until mass >= p
-            keep[0] = True
-            thr = sp[keep].min()
-            x = x.masked_fill(probs < thr, float("-inf"))
-        probs = torch.softmax(x, -1)
-        g = None
-        if generator is not None:
-            g = generator
-        elif seeds is not None:
-            g = torch.Generator(device="cpu")
-            g.manual_seed(int(seeds[b]) & ((1 << 63) - 1))
-        out[b] = int(torch.multinomial(probs.cpu(), 1, generator=g))
-    return out
+        sc = np.float32(1.0) if (not t > 0 or k == 1) else np.float32(1.0) / np.float32(t)
+        x = lg[b].astype(np.float32) * sc
+        seed = int(seeds[b]) & ((1 << 64) - 1) if seeds is not None else 0
+        out[b] = _select(x, np.arange(V), t, k, p, seed, V)
+    return out.to(logits.device)
+
+
+def cand_topk(local: torch.Tensor, lo: int, V: int, temperature, top_k, K: int, KC: int) -> torch.Tensor:
+    """Per-rank candidates of a vocab shard (GPU ``cand_topk``): every element whose scaled logit is
+    >= the shard's K-th largest, packed per row as [KC values | KC global indices as int32 bits]."""
+    B, vl = local.shape
+    lg = local.detach().float().cpu().numpy()
+    pack = np.zeros((B, 2 * KC), dtype=np.float32)
+    for b in range(B):
+        t = float(temperature[b]) if temperature is not None else 0.0
+        k = int(top_k[b]) if top_k is not None else 0
+        sc = np.float32(1.0) if (not t > 0 or k == 1) else np.float32(1.0) / np.float32(t)
+        n = max(0, min(vl, V - lo))
+        x = lg[b, :n].astype(np.float32) * sc
+        kth = np.sort(x)[::-1][K - 1] if n >= K else -np.inf
+        sel = np.flatnonzero(x >= kth)[:KC]
+        vals = np.full(KC, -np.inf, dtype=np.float32)
+        ids = np.full(KC, 0x7FFFFFFF, dtype=np.int32)
+        vals[:sel.size] = x[sel]
+        ids[:sel.size] = lo + sel
+        pack[b, :KC] = vals
+        pack[b, KC:] = ids.view(np.float32)
+    return torch.from_numpy(pack).to(local.device)
+
+
+def sample_cand(pack: torch.Tensor, groups: int, KC: int, temperature, top_k, top_p, seeds, V: int) -> torch.Tensor:
+    """Sampling over gathered candidates [B, groups * 2KC] (GPU ``sample_cand``)."""
+    B = pack.shape[0]
+    a = pack.detach().cpu().numpy().reshape(B, groups, 2, KC)
+    out = torch.empty(B, dtype=torch.long)
+    for b in range(B):
+        x = a[b, :, 0, :].reshape(-1).astype(np.float32)
+        idx = a[b, :, 1, :].reshape(-1).view(np.int32).astype(np.int64)
+        t = float(temperature[b]) if temperature is not None else 0.0
+        k = int(top_k[b]) if top_k is not None else 0
+        p = float(top_p[b]) if top_p is not None else 1.0
+        seed = int(seeds[b]) & ((1 << 64) - 1) if seeds is not None else 0
+        out[b] = _select(x, idx, t, k, p, seed, V)
+    return out.to(pack.device)
 
 
 def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:

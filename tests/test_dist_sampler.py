@@ -1,0 +1,75 @@
+"""Vocab-parallel sampling from per-rank candidates (ops.sample_distributed): each TP rank keeps its
+[B, V/tp] logit shard, sends [B, 128] (value, token id) candidates, and every rank then draws the
+token the full-row sampler would draw from the all-gathered logits - greedy and seeded
+temperature / top-k / top-p alike (top-k <= 64). Checked against the full-row sampler on CPU (the
+oracle) and on the GPU (sample_v3 vs cand_topk + sample_cand), with bf16 ties at the boundary;
+the multi-process gloo TP=2/4 engine runs in test_tp_gloo.py sample through this path."""
+import numpy as np
+import pytest
+import torch
+
+
+def _rows(B, V, seed, ties=True):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, V, generator=g) * 3
+    if ties:  # bf16-rounded logits: many exact ties among the top values
+        x = x.to(torch.bfloat16).float()
+    return x
+
+
+def _params(B, seed):
+    rng = np.random.default_rng(seed)
+    temp = rng.choice([0.0, 0.7, 1.0], B).astype(np.float32)
+    topk = rng.choice([1, 5, 40, 50, 64], B).astype(np.int32)
+    topp = rng.choice([1.0, 0.95, 0.5, 0.9], B).astype(np.float32)
+    seeds = rng.integers(-2 ** 62, 2 ** 62, B).astype(np.int64)
+    return temp, topk, topp, seeds
+
+
+class _FakeGather:
+    """In-process stand-in for the TP group: all_gather_last_dim over precomputed per-rank packs."""
+
+    def __init__(self, packs):
+        self.packs = packs
+
+    def all_gather_last_dim(self, _):
+        return torch.cat(self.packs, -1)
+
+
+@pytest.mark.parametrize("tp", [2, 4, 8])
+def test_candidates_equal_full_row_sampler_cpu(tp):
+    from llmss_amd.ops import reference as R
+
+    B, V = 24, 1000
+    Vp = -(-V // (16 * tp)) * 16 * tp
+    x = torch.full((B, Vp), float("-inf"))
+    x[:, :V] = _rows(B, V, tp)
+    temp, topk, topp, seeds = _params(B, tp)
+    full = R.sample(x[:, :V], temp, topk, topp, seeds)
+    vl = Vp // tp
+    packs = [R.cand_topk(x[:, r * vl:(r + 1) * vl], r * vl, V, temp, topk, 64, 128) for r in range(tp)]
+    got = R.sample_cand(torch.cat(packs, -1), tp, 128, temp, topk, topp, seeds, V)
+    assert got.tolist() == full.tolist()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tp,V", [(2, 32000), (8, 32000), (4, 50257), (8, 1000)])
+def test_gpu_candidates_equal_v3_sampler(tp, V):
+    from llmss_amd import ops
+    from llmss_amd.ops import hip as H
+
+    dev = torch.device("cuda")
+    B = 64
+    Vp = -(-V // (16 * tp)) * 16 * tp
+    x = torch.zeros(B, Vp, dtype=torch.bfloat16, device=dev)
+    x[:, :V] = _rows(B, V, V + tp).to(torch.bfloat16).to(dev)
+    temp, topk, topp, seeds = (torch.from_numpy(a).to(dev) for a in _params(B, tp))
+    full = H.sample(x, temp, topk, topp, seeds, vocab=V)
+    vl = Vp // tp
+    packs = [H.cand_topk(x[:, r * vl:(r + 1) * vl].contiguous(), r * vl, V, temp, topk) for r in range(tp)]
+    got = ops.sample_distributed(x[:, :vl].contiguous(), _FakeGather(packs), 0, V, temp, topk, topp, seeds)
+    assert got.tolist() == full.tolist()
+    # candidate packs hold every shard element >= the shard's 64th largest scaled logit
+    p0 = packs[0].cpu()
+    ids = p0[:, 128:].view(torch.int32)
+    assert bool(((ids >= 0) & (ids < vl) | (ids == 0x7fffffff)).all())
