@@ -42,6 +42,8 @@ class TPGroup:
         # workgroup), so the comm/compute overlap of a TP=N schedule can be measured on one GPU.
         self.sim_comm = sim_comm if fake and size > 1 else None
         self._cycles_per_us = None
+        # data parallelism (initialize_distributed(dp=...)): this group is replica `replica` of `dp`
+        self.replica, self.dp, self.global_rank, self.ctrl_group = 0, 1, rank, None
 
     # reference-compatible accessors (FakeGroup.size()/rank())
     def world_size(self) -> int:
@@ -129,17 +131,22 @@ class TPGroup:
         if self.is_real and t.is_cuda and self.host_staged:
             self._no_capture()
             h = t.cpu()
-            dist.broadcast(h, src=src, group=self.group)
+            dist.broadcast(h, src=self._global(src), group=self.group)
             t.copy_(h)
         elif self.is_real:
-            dist.broadcast(t, src=src, group=self.group)
+            dist.broadcast(t, src=self._global(src), group=self.group)
         return t
+
+    def _global(self, r: int) -> int:
+        """Global rank of group rank ``r`` (torch.distributed's src/dst are global ranks)."""
+        return dist.get_global_rank(self.group, r) if self.group is not None and self.group != dist.group.WORLD \
+            else r
 
     def broadcast_object(self, obj, src: int = 0):
         if not self.is_real:
             return obj
         box = [obj]
-        dist.broadcast_object_list(box, src=src, group=self.group)
+        dist.broadcast_object_list(box, src=self._global(src), group=self.group)
         return box[0]
 
     def all_gather_object(self, obj) -> List:
@@ -192,11 +199,16 @@ def _env_int(name: str, default: int) -> int:
     return int(v) if v not in (None, "") else default
 
 
-def initialize_distributed(timeout_s: Optional[int] = None, backend: Optional[str] = None):
+def initialize_distributed(timeout_s: Optional[int] = None, backend: Optional[str] = None, dp: Optional[int] = None):
     """Initialise torch.distributed from torchrun env vars.
 
     Returns ``(tp_group, rank, world_size)`` like the reference
     (``dist.py:40``); ``tp_group`` is a :class:`TPGroup`.
+
+    ``dp`` (or ``LLMSS_DP``) > 1 splits the world into ``dp`` data-parallel replicas of
+    ``world / dp`` consecutive ranks each (one node: a replica's ranks share an xGMI island). Every
+    replica gets its own data-plane communicator (RCCL / gloo) and its own gloo control group;
+    the returned TPGroup is this rank's replica (``.replica``, ``.dp``, ``.global_rank``).
     """
     if timeout_s is None:  # engine start-up (weight load, per-rank GEMM autotuning) runs between collectives
         timeout_s = _env_int("LLMSS_DIST_TIMEOUT_S", 600)
@@ -211,6 +223,9 @@ def initialize_distributed(timeout_s: Optional[int] = None, backend: Optional[st
     if backend is None:
         backend = "nccl" if use_cuda else "gloo"
 
+    dp = int(dp if dp is not None else _env_int("LLMSS_DP", 1))
+    if dp < 1 or world_size % dp:
+        raise ValueError(f"data-parallel degree {dp} does not divide world size {world_size}")
     if world_size == 1:
         return TPGroup(0, 1), rank, world_size
     if os.environ.get("DEBUG") == "1":
@@ -225,7 +240,21 @@ def initialize_distributed(timeout_s: Optional[int] = None, backend: Optional[st
             kwargs["device_id"] = torch.device("cuda", torch.cuda.current_device())
         dist.init_process_group(**kwargs)
     log.info("rank %d/%d initialised backend=%s", rank, world_size, backend)
-    return TPGroup(rank, world_size, group=dist.group.WORLD), rank, world_size
+    if dp == 1:
+        return TPGroup(rank, world_size, group=dist.group.WORLD), rank, world_size
+    tp = world_size // dp
+    mine = None
+    for r in range(dp):  # new_group is collective over the world: every rank creates every group
+        ranks = list(range(r * tp, (r + 1) * tp))
+        data = dist.new_group(ranks, backend=backend) if tp > 1 else None
+        ctrl = dist.new_group(ranks, backend="gloo", timeout=timedelta(seconds=timeout_s)) if tp > 1 else None
+        if rank in ranks:
+            mine = (r, data, ctrl)
+    r, data, ctrl = mine
+    g = TPGroup(rank - r * tp, tp, group=data)
+    g.replica, g.dp, g.global_rank, g.ctrl_group = r, dp, rank, ctrl
+    log.info("rank %d: data-parallel replica %d/%d, tensor-parallel rank %d/%d", rank, r, dp, g.rank, tp)
+    return g, rank, world_size
 
 
 # Reference-compatible alias (dist.py:40).

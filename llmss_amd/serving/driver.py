@@ -91,7 +91,8 @@ class EngineDriver:
         self.heartbeat_s = heartbeat_s
         self.cg = control_group
         if self.tp.is_real and self.cg is None:
-            self.cg = dist.new_group(backend="gloo", timeout=timedelta(seconds=leader_timeout_s))
+            self.cg = getattr(self.tp, "ctrl_group", None) or \
+                dist.new_group(backend="gloo", timeout=timedelta(seconds=leader_timeout_s))
         self.inbox: "queue.Queue" = queue.Queue()
         self.handles: Dict[int, Handle] = {}
         self._next = 0
@@ -103,6 +104,13 @@ class EngineDriver:
         self.error: Optional[BaseException] = None
         self._last_bcast = time.perf_counter()
         self.stats = {"ctrl_bcasts": 0, "ctrl_payloads": 0}
+        self._rid_stride = 1
+        # global rank of this replica's leader (broadcast src is a global rank in torch.distributed)
+        self._src = dist.get_global_rank(self.cg, 0) if self.tp.is_real else 0
+
+    def set_rid_space(self, start: int, stride: int):
+        """Request ids start, start + stride, ... (a Router keeps ids unique across its replicas)."""
+        self._next, self._rid_stride = start, stride
 
     # --------------------------------------------------------------------- leader API
     def submit(self, prompt_ids: List[int], params: SamplingParams,
@@ -112,7 +120,7 @@ class EngineDriver:
         params.resolved_seed()  # fix the seed on the leader so every rank uses the same one
         with self._lock:
             rid = self._next
-            self._next += 1
+            self._next += self._rid_stride
         h = Handle(rid, list(prompt_ids), params, on_done=on_done)
         if deadline_s is not None:
             h.deadline = h.t_submit + deadline_s
@@ -158,14 +166,14 @@ class EngineDriver:
                 payload = pickle.dumps(msg, protocol=pickle.HIGHEST_PROTOCOL)
                 hdr[0] = len(payload)
             hdr[1] = 1 if msg.get("hb") else 0
-        dist.broadcast(hdr, src=0, group=self.cg)
+        dist.broadcast(hdr, src=self._src, group=self.cg)
         n = int(hdr[0])
         self.stats["ctrl_bcasts"] += 1
         if n == 0:
             return dict(self._EMPTY, hb=bool(hdr[1]))
         self.stats["ctrl_payloads"] += 1
         buf = torch.frombuffer(bytearray(payload), dtype=torch.uint8) if self.leader else torch.empty(n, dtype=torch.uint8)
-        dist.broadcast(buf, src=0, group=self.cg)
+        dist.broadcast(buf, src=self._src, group=self.cg)
         return msg if self.leader else pickle.loads(buf.numpy().tobytes())
 
     def _collect(self, block: bool):

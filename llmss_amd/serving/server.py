@@ -17,9 +17,13 @@ def main(argv=None):
     p.add_argument("--model", "--pretrained_model_path", dest="model", required=True)
     p.add_argument("--grpc_host", default="0.0.0.0")
     p.add_argument("--grpc_port", type=int, default=50051)
+    p.add_argument("--broker_port", type=int, default=20001,
+                   help="with torchrun --dp > 1: port of the in-process broker on rank 0 that the replicas pull from")
     add_engine_args(p)
     args = p.parse_args(argv)
     driver, tok, _ = build_driver(args.model, args)
+    if getattr(driver.tp, "dp", 1) > 1:  # multi-process data parallelism: replicas pull from one broker
+        return _serve_replicas(driver, tok, args)
     if driver.leader:
         driver.start()
         server = serve(EngineServicer(driver, tok), args.grpc_port, args.grpc_host)
@@ -34,6 +38,30 @@ def main(argv=None):
         driver.stop()
     else:
         driver.run()
+
+
+def _serve_replicas(driver, tok, args):
+    """torchrun world = dp x tp: global rank 0 hosts a broker and the gRPC front-end (BrokerServicer);
+    every replica leader runs a Consumer on that broker (BRPOP = load balancing, replies correlated
+    by request id); followers run their replica's driver loop."""
+    import torch.distributed as dist
+
+    from .broker import MiniRedisServer, RedisBroker
+    from .consumer import Consumer
+    from .grpc_api import BrokerServicer
+
+    g = driver.tp
+    broker_srv = None
+    if g.global_rank == 0:
+        broker_srv = MiniRedisServer("127.0.0.1", args.broker_port)
+        broker_srv._thread.start()
+    dist.barrier()  # the broker is listening before replicas connect
+    if driver.leader:
+        Consumer(driver, tok, RedisBroker("127.0.0.1", args.broker_port)).start()
+    if g.global_rank == 0:
+        server = serve(BrokerServicer(RedisBroker("127.0.0.1", args.broker_port)), args.grpc_port, args.grpc_host)
+        print(f"llmss gRPC Generate on {args.grpc_host}:{server.bound_port}: {g.dp} replicas x tp={g.size}", flush=True)
+    driver.run()
 
 
 if __name__ == "__main__":

@@ -38,6 +38,7 @@ def main(argv=None):
     driver, tok, model = build_driver(args.pretrained_model_path, args)
     if args.model_type and args.model_type not in (model.cfg.model_type, "gpt_bigcode" if model.cfg.model_type == "gpt_bigcode" else None):
         raise SystemExit(f"--model_type {args.model_type} does not match checkpoint type {model.cfg.model_type}")
+    # --dp N with torchrun: world = N replicas x TP; every replica leader pulls from the same broker
     if driver.leader:
         print(f"{model.cfg.model_type} setup is done.", flush=True)
         Consumer(driver, tok, RedisBroker(args.redis_host, args.redis_port)).start()
