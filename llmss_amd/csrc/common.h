@@ -119,6 +119,100 @@ __device__ __forceinline__ TileWork tile_work(int ntm, int ntn, int bm, int bn) 
   return {(t - nt * ntm) * bm, nt * bn, z};
 }
 
+// Cooperative GEMM epilogue through LDS. A wave's accumulators (MT x NT mfma_f32_16x16x32 tiles in
+// the C layout: lane (li = lane & 15, g = lane >> 4) holds rows 4g..4g+3 of column li) are written
+// row-major into a padded fp32 image in LDS, then every thread stores 16 B row-contiguous pieces:
+// fp32 split-K slabs (part != nullptr, [M][N] of this slice) or bf16 Y with bias / activation /
+// SwiGLU (16-row interleaved gate|up) applied on the way. Replaces per-lane 2-/4-byte stores of
+// every accumulator element, whose issue cost dominated small tiles (an 8-k-step 128x128 tile spent
+// ~10 us in the store tail). The tile is processed in row chunks that fit LDSB bytes; the caller
+// must have drained every load into / read from that LDS region.
+template <int BM, int BN, int MT, int NT, int NTHR, int LDSB>
+__device__ __forceinline__ void tile_store_lds(const f32x4 (&acc)[MT][NT], char* lds, int wrow0, int wcol0, int m0,
+                                               int n0, int M, int N, float* __restrict__ part,
+                                               bf16_t* __restrict__ Y, int64_t ldy, const bf16_t* __restrict__ bias,
+                                               int act, int glu) {
+  constexpr int LDW = BN + 4;  // padded row: the 4 rows a wave-instruction writes hit different banks
+  constexpr int RMAX = LDSB / (LDW * 4);
+  constexpr int R = (RMAX >= BM ? BM : RMAX) / 16 * 16;
+  static_assert(R >= 16, "LDS too small for a 16-row epilogue chunk");
+  float* ct = reinterpret_cast<float*>(lds);
+  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every wave is done reading the operand stages
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  for (int r0 = 0; r0 < BM; r0 += R) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int rb = wrow0 + mt * 16;  // a 16-row block is entirely inside or outside the chunk
+      if (rb < r0 || rb >= r0 + R) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) ct[(rb - r0 + 4 * g + i) * LDW + wcol0 + nt * 16 + li] = acc[mt][nt][i];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int rows = BM - r0 < R ? BM - r0 : R;  // the last chunk may be shorter
+    if (part) {  // fp32 slab rows: 4 floats (16 B) per thread-step
+      constexpr int VPR = BN / 4;
+      for (int v = threadIdx.x; v < rows * VPR; v += NTHR) {
+        const int r = v / VPR, c = (v - r * VPR) * 4;
+        const int m = m0 + r0 + r, n = n0 + c;
+        if (m >= M || n >= N) continue;
+        const f32x4 val = *reinterpret_cast<const f32x4*>(&ct[r * LDW + c]);
+        float* dst = part + (int64_t)m * N + n;
+        if (n + 3 < N && (N & 3) == 0) *reinterpret_cast<f32x4*>(dst) = val;
+        else
+          for (int j = 0; j < 4 && n + j < N; ++j) dst[j] = val[j];
+      }
+    } else if (glu) {  // out col 16p + j = silu(gate col 32p + j) * up col 32p + 16 + j, 8 per thread-step
+      constexpr int VPR = BN / 16;
+      for (int v = threadIdx.x; v < rows * VPR; v += NTHR) {
+        const int r = v / VPR, oc = (v - r * VPR) * 8;
+        const int p = oc >> 4, j = oc & 15;
+        const int cg = 32 * p + j, m = m0 + r0 + r, ng = n0 + cg;
+        if (m >= M || ng >= N) continue;  // N % 32 == 0: the whole gate|up pair exists
+        u16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float gv = ct[r * LDW + cg + e], uv = ct[r * LDW + cg + 16 + e];
+          if (bias) { gv += bf2f(bias[ng + e]); uv += bf2f(bias[ng + 16 + e]); }
+          o[e] = f2bf(silu(gv) * uv);
+        }
+        bf16_t* dst = Y + (int64_t)m * ldy + n0 / 2 + oc;
+        if (ng + 16 + 7 < N && (ldy & 7) == 0) *reinterpret_cast<u16x8*>(dst) = o;
+        else
+          for (int e = 0; e < 8 && ng + 16 + e < N; ++e) dst[e] = o[e];
+      }
+    } else {  // bf16 rows: 8 values (16 B) per thread-step
+      constexpr int VPR = BN / 8;
+      for (int v = threadIdx.x; v < rows * VPR; v += NTHR) {
+        const int r = v / VPR, c = (v - r * VPR) * 8;
+        const int m = m0 + r0 + r, n = n0 + c;
+        if (m >= M || n >= N) continue;
+        u16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float x = ct[r * LDW + c + e];
+          if (bias && n + e < N) x += bf2f(bias[n + e]);
+          o[e] = f2bf(apply_act(x, act));
+        }
+        bf16_t* dst = Y + (int64_t)m * ldy + n;
+        if (n + 7 < N && (ldy & 7) == 0) *reinterpret_cast<u16x8*>(dst) = o;
+        else
+          for (int e = 0; e < 8 && n + e < N; ++e) dst[e] = o[e];
+      }
+    }
+    if (r0 + R < BM) {  // the next chunk overwrites the image
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+}
+
 #define HIP_CHECK_LAUNCH()                                                               \
   do {                                                                                   \
     hipError_t e__ = hipGetLastError();                                                  \

@@ -1386,7 +1386,15 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_f
 static int tiles_of(int M, int N, int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); }
 // tsel: 1 = 128x128, 2 = 64x128, 3 = 64x64 (4 waves); 5 = 256x128, 6 = 256x64 (8 waves, 1 WG/CU);
 // 4 = the big-tile kernel
+bool gemm_mid_dims(int tsel, int* bm, int* bn, int* threads);
+void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
+                     const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
+                     int split, hipStream_t st);
+
+// tsel 8-12: gemm_mid (gemm_mid.hip: buffer-descriptor staging, 128x128 / 256x128 / 64x256 / 64x128 / 128x256)
 static int tile_dims(int tsel, int* bm, int* bn) {
+  int thr;
+  if (gemm_mid_dims(tsel, bm, bn, &thr)) return 0;
   *bm = tsel >= 5 ? 256 : (tsel == 1 ? 128 : 64);
   *bn = (tsel == 3 || tsel == 6) ? 64 : 128;
   return 0;
@@ -1506,7 +1514,7 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   const int tsel_raw = tsel;
   int s = split_hint;
   const bool f8 = wscale != nullptr;  // fp8-e4m3 weights (W8A16): half the weight bytes of a decode step
-  if (f8 && (tsel & 15) >= 5) tsel = (tsel & ~15) | 1;  // 8-wave tiles are bf16-only
+  if (f8 && (tsel & 15) >= 5) tsel = (tsel & ~15) | 1;  // 8-wave and mid tiles are bf16-only
   gemm_tiled_plan(M, N, K, &tsel, &s, g != 0);
   static constexpr int kDepth[4] = {2, 3, 4, 6};
   int ns = kDepth[(tsel >> 4) & 3];  // LDS ring depth (hint bits 4-5); bit 6: default-policy weights
@@ -1533,6 +1541,18 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   float* part = s > 1 ? (float*)workspace : nullptr;
   const int act_k = s > 1 ? 0 : act, glu_k = s > 1 ? 0 : g;
   dim3 grid(nt, s);
+  if (tsel >= 8 && tsel <= 12) {
+    launch_gemm_mid(tsel, ns, wnt_ok(tsel_raw, M, tsel), X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, part, M, N, K,
+                    act_k, glu_k, s, st);
+    if (s > 1 && partial_out && !g && act == 0) return s;
+    if (s > 1) {
+      const int nout = g ? N / 2 : N;
+      dim3 rgrid(std::min((nout + 255) / 256, 64), M);
+      splitk_reduce_kernel<<<rgrid, 256, 0, st>>>(part, s, M, N, B, Y, ldy, act, g);
+      HIP_CHECK_LAUNCH();
+    }
+    return 0;
+  }
   // non-temporal weight staging when every weight tile is read by exactly one workgroup row
   const bool wnt = wnt_ok(tsel_raw, M, tsel);
   if (tsel >= 5) {  // 8-wave tiles (bf16 weights)

@@ -1,0 +1,217 @@
+// Mid-M MFMA GEMM (tensor-parallel decode at M = 64-512 rows, mid-size prefill chunks):
+//   Y[M, N] = epilogue(X[M, K] . W[N, K]^T), bf16 in, fp32 accumulate; split-K over grid.y into fp32
+//   slabs that the next kernel (rope / add_norm / splitk_reduce) sums.
+//
+// Why a separate kernel from gemm_tiled (gemm.hip): rocprofv3 on the TP=8 QKV shape (M=512, N=1536,
+// K=4096; profiles/r2_gemm_pmc) showed the tiled kernels issue 7-8 VALU instructions per MFMA -
+// per-k-step 64-bit address math for every global_load_lds (row clamp, swizzle, K clamp) and
+// per-fragment LDS addresses - and spend 38-48 % of wave cycles waiting: ~10 % MFMA utilisation.
+// Here every operand load is a buffer_load ... lds through a wave-uniform buffer descriptor:
+//   * the per-lane part (row * ld + swizzled 16-B chunk) is a 32-bit voffset computed ONCE;
+//   * the k position is the scalar soffset (+128 B per k-step: SALU, not VALU);
+//   * rows past M / N and the K tail of the last row fall outside the descriptor's num_records and
+//     read as zero (hardware bounds check) - no clamps in the loop;
+// and each wave's LDS fragment addresses are one base register per k-half plus immediate offsets
+// (the XOR swizzle term depends only on lane & 7 because fragment rows step by 16).
+// Tiles are larger per wave (32-64 MFMAs per k-step) so the fixed per-step cost (barrier, counted
+// vmcnt wait, staging issue) is amortised. Ring of NS stages, stage t+NS-1 issued while t computes.
+#include "common.h"
+
+// The buffer descriptor is built and used only inside the kernel body, and every offset argument of
+// the buffer builtins is cast to uint32_t explicitly: otherwise the host compilation pass of this
+// template fails overload resolution quietly and hipcc drops the kernel's launch stub (undefined
+// __device_stub__ at link time, no diagnostic).
+template <int BM, int BN, int WM, int WN, int NS, bool WNT>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                              const bf16_t* __restrict__ B, int64_t ldb,
+                                                              const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
+                                                              int64_t ldy, float* __restrict__ part, int M, int N, int K,
+                                                              int act, int glu) {
+  constexpr int NW = WM * WN;
+  constexpr int MT = BM / WM / 16, NT = BN / WN / 16;  // 16x16 accumulator tiles per wave
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  constexpr int AL = BM / (8 * NW), BL = BN / (8 * NW);  // 1-KiB buffer_load_lds per wave per stage
+  constexpr int LOADS = AL + BL;
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows must split evenly over the waves");
+  static_assert(MT >= 1 && NT >= 1, "per-wave tile");
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  const int wm = w / WN, wn = w % WN;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
+  const TileWork tw = tile_work(ntm, ntn, BM, BN);
+  const int m0 = tw.m0, n0 = tw.n0, zk = tw.z;
+
+  const int nk_all = (K + 63) / 64;
+  const int per = (nk_all + gridDim.y - 1) / gridDim.y;
+  const int t0 = zk * per, t1 = min(nk_all, t0 + per);
+
+  // descriptors start at this tile's first row; everything past the matrix end reads as zero
+  const uint64_t abytes = (uint64_t)(M - m0) * (uint64_t)lda * 2, bbytes = (uint64_t)(N - n0) * (uint64_t)ldb * 2;
+  const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(A + (int64_t)m0 * lda), (short)0,
+                                                    (int)(abytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)abytes),
+                                                    0x00020000);
+  const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(B + (int64_t)n0 * ldb), (short)0,
+                                                    (int)(bbytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)bbytes),
+                                                    0x00020000);
+  uint32_t va[AL], vb[BL];  // per-lane byte offsets (row, source-swizzled chunk), fixed over k
+#pragma unroll
+  for (int i = 0; i < AL; ++i) {
+    const int row = (i * NW + w) * 8 + (lane >> 3);
+    va[i] = (uint32_t)(row * lda * 2 + (((lane & 7) ^ (row & 7)) << 4));
+  }
+#pragma unroll
+  for (int i = 0; i < BL; ++i) {
+    const int row = (i * NW + w) * 8 + (lane >> 3);
+    vb[i] = (uint32_t)(row * ldb * 2 + (((lane & 7) ^ (row & 7)) << 4));
+  }
+  // one ring stage (k-step T_) into LDS slot SA_: AL + BL wave-instructions of 1 KiB (8 rows x 128 B);
+  // the k position is the scalar soffset, the per-lane voffsets never change
+#define MID_STAGE(T_, SA_)                                                                                         \
+  do {                                                                                                           \
+    char* sA_ = (SA_);                                                                                           \
+    const int soff_ = (T_) * 128;                                                                                \
+    _Pragma("unroll") for (int i_ = 0; i_ < AL; ++i_)                                                             \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)(sA_ + (i_ * NW + w) * 1024), 16, (uint32_t)va[i_], (uint32_t)soff_, 0, 0); \
+    _Pragma("unroll") for (int i_ = 0; i_ < BL; ++i_)                                                             \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (LDS_AS void*)(sA_ + A_BYTES + (i_ * NW + w) * 1024), 16, (uint32_t)vb[i_], \
+                                               (uint32_t)soff_, 0, WNT ? 2 : 0); /* weights: read once per step, nt */  \
+  } while (0)
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment addresses: row r = base + 16 t (t = tile), chunk c = 4 s + g -> (c ^ (li & 7)) << 4
+  const int arow = wm * (MT * 16) + li, brow = wn * (NT * 16) + li;
+  const int x0 = ((g) ^ (li & 7)) << 4, x1 = ((4 + g) ^ (li & 7)) << 4;
+  const int aoff0 = arow * 128 + x0, aoff1 = arow * 128 + x1;
+  const int boff0 = A_BYTES + brow * 128 + x0, boff1 = A_BYTES + brow * 128 + x1;
+
+  // ONE copy of the MFMA body (a second, masked copy made hipcc shuffle every accumulator between
+  // AGPRs and VGPRs each k-step); the K tail is zeroed in LDS instead (below)
+  auto compute = [&](const char* st) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ao = s ? aoff1 : aoff0, bo = s ? boff1 : boff0;
+      s16x8 a[MT], b[NT];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) a[t] = *reinterpret_cast<const s16x8*>(st + ao + t * 2048);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) b[t] = *reinterpret_cast<const s16x8*>(st + bo + t * 2048);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+    }
+  };
+
+#pragma unroll
+  for (int j = 0; j < NS - 1; ++j)
+    if (t0 + j < t1) MID_STAGE(t0 + j, smem + j * STAGE);
+  int cur = 0;
+  const bool ktail = (K & 63) != 0;
+  for (int t = t0; t < t1; ++t) {
+    // stage t landed for this wave (younger stages stay in flight), then for every wave
+    const int younger = t1 - 1 - t;
+    if constexpr (NS >= 4) {
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (NS == 3) {
+      if (younger >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // raw barrier: in-flight loads survive it
+    asm volatile("" ::: "memory");
+    const int nxt = cur == 0 ? NS - 1 : cur - 1;  // (cur + NS - 1) % NS: freed by compute(t - 1)
+    if (t + NS - 1 < t1) MID_STAGE(t + NS - 1, smem + nxt * STAGE);
+    char* st = smem + cur * STAGE;
+    if (ktail && t == nk_all - 1) {
+      // last, partial k-step (wave-uniform branch, once per kernel): the A chunks past K hold the next
+      // row's values - zero them so the B side's next-row bytes multiply by 0; nothing is in flight now
+      const int kv = K - t * 64;  // valid k of this step, a multiple of 16
+      for (int idx = threadIdx.x; idx < BM * 8; idx += 64 * NW) {
+        const int row = idx >> 3, c = idx & 7;
+        if (c * 8 >= kv) *reinterpret_cast<u32x4*>(st + row * 128 + ((c ^ (row & 7)) << 4)) = u32x4{0u, 0u, 0u, 0u};
+      }
+      __syncthreads();
+    }
+    compute(st);
+    cur = cur == NS - 1 ? 0 : cur + 1;
+  }
+
+#undef MID_STAGE
+  // epilogue through LDS (row-contiguous 16-B stores); every stage has landed (vmcnt(0) in the last
+  // step) and tile_store_lds waits for this wave's last fragment reads before its first barrier
+  tile_store_lds<BM, BN, MT, NT, 64 * NW, NS * STAGE>(acc, smem, wm * (MT * 16), wn * (NT * 16), m0, n0, M, N,
+                                                        part ? part + (int64_t)zk * M * N : nullptr, Y, ldy, bias,
+                                                        act, glu);
+}
+
+// tsel 8: 128x128 (2x2 waves), 9: 256x128 (4x2), 10: 64x256 (1x4), 11: 64x128 (1x4), 12: 128x256 (2x4)
+bool gemm_mid_dims(int tsel, int* bm, int* bn, int* threads) {
+  switch (tsel) {
+    case 8: *bm = 128; *bn = 128; *threads = 256; return true;
+    case 9: *bm = 256; *bn = 128; *threads = 512; return true;
+    case 10: *bm = 64; *bn = 256; *threads = 256; return true;
+    case 11: *bm = 64; *bn = 128; *threads = 256; return true;
+    case 12: *bm = 128; *bn = 256; *threads = 512; return true;
+    default: return false;
+  }
+}
+
+// largest ring depth <= want that fits the 160 KiB LDS
+static int mid_depth(int bm, int bn, int want) {
+  const int stage = (bm + bn) * 128;
+  int ns = std::max(2, std::min(want, 6));
+  while (ns > 2 && ns * stage > 160 * 1024) --ns;
+  return ns;
+}
+
+void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
+                     const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
+                     int split, hipStream_t st) {
+  int bm, bn, thr;
+  if (!gemm_mid_dims(tsel, &bm, &bn, &thr)) throw std::runtime_error("gemm_mid: bad tile code");
+  if (glu && (bn / (thr / 64 / (bm == 256 ? 4 : (bm == 128 ? 2 : 1))) / 16) % 2)
+    throw std::runtime_error("gemm_mid: SwiGLU needs an even number of 16-column tiles per wave");
+  if ((uint64_t)bm * ldx * 2 >= (1ull << 31) || (uint64_t)bn * ldw * 2 >= (1ull << 31))
+    throw std::runtime_error("gemm_mid: row stride too large for 32-bit buffer offsets");
+  const int ns = mid_depth(bm, bn, depth);
+  const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  dim3 grid(tiles, split);
+#define MID(BM_, BN_, WM_, WN_, NS_)                                                                             \
+  do {                                                                                                         \
+    if (wnt)                                                                                                   \
+      gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, true><<<grid, 64 * WM_ * WN_, 0, st>>>(X, ldx, W, ldw, bias, Y, ldy, \
+                                                                                    part, M, N, K, act, glu);  \
+    else                                                                                                       \
+      gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, false><<<grid, 64 * WM_ * WN_, 0, st>>>(X, ldx, W, ldw, bias, Y,  \
+                                                                                     ldy, part, M, N, K, act, glu); \
+  } while (0)
+#define MID_NS(BM_, BN_, WM_, WN_)                                               \
+  do {                                                                         \
+    if (ns >= 4) MID(BM_, BN_, WM_, WN_, 4);                                   \
+    else if (ns == 3) MID(BM_, BN_, WM_, WN_, 3);                              \
+    else MID(BM_, BN_, WM_, WN_, 2);                                           \
+  } while (0)
+  switch (tsel) {
+    case 8: MID_NS(128, 128, 2, 2); break;
+    case 9: if (ns >= 3) MID(256, 128, 4, 2, 3); else MID(256, 128, 4, 2, 2); break;
+    case 10: if (ns >= 3) MID(64, 256, 1, 4, 3); else MID(64, 256, 1, 4, 2); break;
+    case 11: MID_NS(64, 128, 1, 4); break;
+    case 12: if (ns >= 3) MID(128, 256, 2, 4, 3); else MID(128, 256, 2, 4, 2); break;
+  }
+#undef MID_NS
+#undef MID
+  HIP_CHECK_LAUNCH();
+}

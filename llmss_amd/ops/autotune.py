@@ -62,6 +62,14 @@ def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, 
         out.append((4 << 8, 1))
     if M >= 128:  # 8-wave 256x128 (5) / 256x64 (6) tiles: one workgroup per CU, deep split-K
         out += [((t | d) << 8, s) for t, d in ((5, 16), (6, 16), (6, 32)) for s in (2, 4, 8, 12, 16)]
+    # gemm_mid (buffer-descriptor staging, csrc/gemm_mid.hip): 8 = 128x128, 9 = 256x128, 10 = 64x256,
+    # 11 = 64x128, 12 = 128x256; depth code 16 / 32 = 3 / 4 stages (clamped to the LDS)
+    mids = [(10, 16), (11, 16), (11, 32)]
+    if M > 64:
+        mids += [(8, 16), (8, 32), (12, 16)]
+    if M >= 256:
+        mids += [(9, 16)]
+    out += [((t | d) << 8, s) for t, d in mids for s in (1, 2, 4, 8)]
     return out
 
 
