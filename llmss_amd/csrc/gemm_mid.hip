@@ -9,8 +9,9 @@
 // Here every operand load is a buffer_load ... lds through a wave-uniform buffer descriptor:
 //   * the per-lane part (row * ld + swizzled 16-B chunk) is a 32-bit voffset computed ONCE;
 //   * the k position is the scalar soffset (+128 B per k-step: SALU, not VALU);
-//   * rows past M / N and the K tail of the last row fall outside the descriptor's num_records and
-//     read as zero (hardware bounds check) - no clamps in the loop;
+//   * rows past M / N fall outside the descriptor's num_records and read as zero (hardware bounds
+//     check) - no clamps in the loop; the partial last k-step (K % 64 != 0) moves k into the voffset
+//     so the last row's tail is range checked too (the check covers voffset, not soffset);
 // and each wave's LDS fragment addresses are one base register per k-half plus immediate offsets
 // (the XOR swizzle term depends only on lane & 7 because fragment rows step by 16).
 // Tiles are larger per wave (32-64 MFMAs per k-step) so the fixed per-step cost (barrier, counted
@@ -73,11 +74,19 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
   do {                                                                                                           \
     char* sA_ = (SA_);                                                                                           \
     const int soff_ = (T_) * 128;                                                                                \
-    _Pragma("unroll") for (int i_ = 0; i_ < AL; ++i_)                                                             \
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)(sA_ + (i_ * NW + w) * 1024), 16, (uint32_t)va[i_], (uint32_t)soff_, 0, 0); \
-    _Pragma("unroll") for (int i_ = 0; i_ < BL; ++i_)                                                             \
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (LDS_AS void*)(sA_ + A_BYTES + (i_ * NW + w) * 1024), 16, (uint32_t)vb[i_], \
-                                               (uint32_t)soff_, 0, WNT ? 2 : 0); /* weights: read once per step, nt */  \
+    if (!ktail || (T_) != nk_all - 1) {                                                                          \
+      _Pragma("unroll") for (int i_ = 0; i_ < AL; ++i_)                                                           \
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)(sA_ + (i_ * NW + w) * 1024), 16, (uint32_t)va[i_], (uint32_t)soff_, 0, 0); \
+      _Pragma("unroll") for (int i_ = 0; i_ < BL; ++i_)                                                           \
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (LDS_AS void*)(sA_ + A_BYTES + (i_ * NW + w) * 1024), 16, (uint32_t)vb[i_], \
+                                                 (uint32_t)soff_, 0, WNT ? 2 : 0); /* weights: read once per step, nt */ \
+    } else { /* partial last k-step: k folded into the voffset, so the range check covers the row tail */     \
+      _Pragma("unroll") for (int i_ = 0; i_ < AL; ++i_)                                                           \
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)(sA_ + (i_ * NW + w) * 1024), 16, (uint32_t)(va[i_] + soff_), (uint32_t)0, 0, 0); \
+      _Pragma("unroll") for (int i_ = 0; i_ < BL; ++i_)                                                           \
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (LDS_AS void*)(sA_ + A_BYTES + (i_ * NW + w) * 1024), 16, (uint32_t)(vb[i_] + soff_), \
+                                                 (uint32_t)0, 0, WNT ? 2 : 0);                                  \
+    }                                                                                                            \
   } while (0)
 
   f32x4 acc[MT][NT];
@@ -111,11 +120,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
     }
   };
 
+  const bool ktail = (K & 63) != 0;
 #pragma unroll
   for (int j = 0; j < NS - 1; ++j)
     if (t0 + j < t1) MID_STAGE(t0 + j, smem + j * STAGE);
   int cur = 0;
-  const bool ktail = (K & 63) != 0;
   for (int t = t0; t < t1; ++t) {
     // stage t landed for this wave (younger stages stay in flight), then for every wave
     const int younger = t1 - 1 - t;

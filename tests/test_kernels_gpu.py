@@ -178,6 +178,22 @@ def test_gemm_tiled_variants(tile, stages, split, M, N, K):
           R.linear(x.float(), w.float(), None, glu=True), 2e-2)
 
 
+@pytest.mark.parametrize("tile", [8, 11, 12])
+def test_gemm_mid_k_tail_reads_nothing_past_the_operands(tile):
+    """Operands as views at the front of NaN-filled buffers: the partial last k-step of the last rows
+    must not pick up the NaNs that follow (0 * NaN would poison the row)."""
+    torch.manual_seed(0)
+    M, N, K = 130, 384, 64 * 3 + 16
+    xb = torch.full((M * K + 4096,), float("nan"), dtype=torch.bfloat16, device=dev)
+    wb = torch.full((N * K + 4096,), float("nan"), dtype=torch.bfloat16, device=dev)
+    x, w = xb[: M * K].view(M, K), wb[: N * K].view(N, K)
+    x.copy_(rnd(M, K))
+    w.copy_(rnd(N, K, scale=K ** -0.5))
+    for split in (1, 2):
+        y = H.linear(x, w, None, nt_hint=(tile | 16) << 8, split_hint=split)
+        close(y, R.linear(x.float(), w.float(), None), 2e-2)
+
+
 @pytest.mark.parametrize("M", [1, 8, 64, 100])
 def test_gemm_fp8(M):
     torch.manual_seed(0)
