@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--secondary", default="gpt2-xl",
                     help="second headline model timed after the first (TP=1 per GPU, data-parallel over N GPUs); "
-                         "'' to skip")
+                         "'' or 'none' to skip")
     ap.add_argument("--simulate-tp", type=int, default=0,
                     help="dev tool: one process computes rank 0 of a TP=N shard plan with no communication "
                          "(per-rank compute time at TP=N shapes; not a headline number)")
@@ -66,7 +66,7 @@ def main():
             print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
     res = run_config(args, args.model, tp, args.batch_per_gpu * max(world, args.simulate_tp), progress)
-    if args.secondary and args.simulate_tp <= 1 and args.secondary != args.model:
+    if args.secondary not in ("", "none") and args.simulate_tp <= 1 and args.secondary != args.model:
         # second BASELINE headline config (GPT-2-XL TP=1, 25 heads: no TP split), driver-timed in the same run;
         # with N GPUs every rank serves its own TP=1 replica (data parallel) and the node total is reported
         torch.cuda.empty_cache()

@@ -1303,22 +1303,24 @@ void gemm_stream_plan(int M, int N, int K, int* nt_out, int* splitk_out);
 namespace {
 std::mutex g_tuned_mu;
 std::unordered_map<uint64_t, std::pair<int, int>> g_tuned;
-uint64_t tune_key(int M, int N, int K, bool glu, bool fp8) {
-  return ((uint64_t)M << 43) | ((uint64_t)N << 22) | ((uint64_t)K << 2) | (glu ? 2u : 0u) | (fp8 ? 1u : 0u);
+// kind: 0 = bf16 [N, K] weights, 1 = fp8 weights, 2 = packed bf16 weights (launch_gemm_packed)
+uint64_t tune_key(int M, int N, int K, bool glu, int kind) {
+  return ((uint64_t)(kind & 3) << 62) | ((uint64_t)M << 42) | ((uint64_t)N << 22) | ((uint64_t)K << 2) |
+         (glu ? 2u : 0u) | (kind == 1 ? 1u : 0u);
 }
 }  // namespace
 
-void gemm_tuned_set(int M, int N, int K, bool glu, bool fp8, int nt_hint, int split) {
+void gemm_tuned_set(int M, int N, int K, bool glu, int kind, int nt_hint, int split) {
   std::lock_guard<std::mutex> lk(g_tuned_mu);
-  g_tuned[tune_key(M, N, K, glu, fp8)] = {nt_hint, split};
+  g_tuned[tune_key(M, N, K, glu, kind)] = {nt_hint, split};
 }
 void gemm_tuned_clear() {
   std::lock_guard<std::mutex> lk(g_tuned_mu);
   g_tuned.clear();
 }
-bool gemm_tuned_get(int M, int N, int K, bool glu, bool fp8, int* nt_hint, int* split) {
+bool gemm_tuned_get(int M, int N, int K, bool glu, int kind, int* nt_hint, int* split) {
   std::lock_guard<std::mutex> lk(g_tuned_mu);
-  auto it = g_tuned.find(tune_key(M, N, K, glu, fp8));
+  auto it = g_tuned.find(tune_key(M, N, K, glu, kind));
   if (it == g_tuned.end()) return false;
   *nt_hint = it->second.first;
   *split = it->second.second;
@@ -1329,7 +1331,7 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_f
                 const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace,
                 int64_t ws_bytes, int nt_hint, int split_hint, bool partial_out, hipStream_t st) {
   if (M == 0 || N == 0) return 0;
-  if (nt_hint == 0 && split_hint == 0) gemm_tuned_get(M, N, K, glu, w_fp8, &nt_hint, &split_hint);
+  if (nt_hint == 0 && split_hint == 0) gemm_tuned_get(M, N, K, glu, w_fp8 ? 1 : 0, &nt_hint, &split_hint);
   if (!y && (!partial_out || gemm_partial_slabs(M, N, K, w_fp8, glu, act, nt_hint, split_hint, ws_bytes) == 0))
     throw std::runtime_error("gemm: this configuration writes the output, but no output buffer was given");
   if (K % 16) throw std::runtime_error("gemm: K must be a multiple of 16");
@@ -1389,7 +1391,7 @@ static int tiles_of(int M, int N, int bm, int bn) { return ((M + bm - 1) / bm) *
 bool gemm_mid_dims(int tsel, int* bm, int* bn, int* threads);
 void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
-                     int split, hipStream_t st);
+                     int split, hipStream_t st, bool packed = false);
 
 // tsel 8-12: gemm_mid (gemm_mid.hip: buffer-descriptor staging, 128x128 / 256x128 / 64x256 / 64x128 / 128x256)
 static int tile_dims(int tsel, int* bm, int* bn) {
@@ -1612,7 +1614,7 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
 int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int nt_hint, int split_hint,
                        int64_t ws_bytes) {
   if (M == 0 || N == 0 || glu || act != 0) return 0;
-  if (nt_hint == 0 && split_hint == 0) gemm_tuned_get(M, N, K, glu, w_fp8, &nt_hint, &split_hint);
+  if (nt_hint == 0 && split_hint == 0) gemm_tuned_get(M, N, K, glu, w_fp8 ? 1 : 0, &nt_hint, &split_hint);
   const int tiled_hint = nt_hint >> 8;
   const bool stream = (nt_hint & 0xff) || (!tiled_hint && (M <= 16 || (w_fp8 && M > 128)));
   int s;
@@ -1634,7 +1636,7 @@ int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int n
 }
 
 void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk) {
-  if (gemm_tuned_get(M, N, K, false, w_fp8, nt, splitk)) {
+  if (gemm_tuned_get(M, N, K, false, w_fp8 ? 1 : 0, nt, splitk)) {
     if ((*nt >> 8) & 128) {
       *splitk = 1;  // stream-K finishes its tiles in-kernel: no partial slabs for the consumer
     } else if (*nt >> 8) {  // tiled hint: the split the kernel will really use
@@ -1651,4 +1653,66 @@ void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk) {
     *nt = tsel << 8;
     *splitk = s;
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Packed bf16 weights ([N/16][ceil(K/64)][16][64], ops/hip.py pack_weight): every shape runs the
+// gemm_mid kernels (tiles 8-12), whose weight stages are then contiguous 2-KiB panel blocks.
+// Plan: tile by M (64x128 up to 64 rows, 128x128 up to 128, then 256x128 / 128x256), K split until
+// the grid holds ~200 workgroups (>= 4 k-steps per slice); tuned plans (kind 2) override.
+static void packed_plan(int M, int N, int K, bool glu, int nt_hint, int split_hint, int* tsel_out, int* ns_out,
+                        int* split_out) {
+  if (nt_hint == 0 && split_hint == 0) gemm_tuned_get(M, N, K, glu, 2, &nt_hint, &split_hint);
+  int tsel = (nt_hint >> 8) & 15;
+  static constexpr int kDepth[4] = {2, 3, 4, 6};
+  int ns = (nt_hint >> 8) ? kDepth[(nt_hint >> 12) & 3] : 4;
+  if (tsel < 8 || tsel > 12) tsel = M <= 64 ? 11 : (M <= 128 ? 8 : (N >= 4 * M ? 12 : 9));
+  int bm, bn;
+  tile_dims(tsel, &bm, &bn);
+  const int nt = tiles_of(M, N, bm, bn), nk = (K + 63) / 64;
+  int s = split_hint;
+  if (s <= 0) {
+    s = 1;
+    while (nt * s < 200 && s < 8 && nk / (2 * s) >= 4) s *= 2;
+  }
+  *tsel_out = tsel;
+  *ns_out = ns;
+  *split_out = std::max(1, std::min(s, nk));
+}
+
+int gemm_packed_partial_slabs(int M, int N, int K, bool glu, int act, int nt_hint, int split_hint, int64_t ws_bytes) {
+  if (M == 0 || N == 0 || glu || act != 0) return 0;
+  int tsel, ns, s;
+  packed_plan(M, N, K, glu, nt_hint, split_hint, &tsel, &ns, &s);
+  if ((int64_t)s * M * N * 4 > ws_bytes) s = 1;
+  return s > 1 ? s : 0;
+}
+
+int launch_gemm_packed(const void* x, int64_t ldx, const void* w, int64_t k64, const void* bias, void* y, int64_t ldy,
+                       int M, int N, int K, int act, bool glu, void* workspace, int64_t ws_bytes, int nt_hint,
+                       int split_hint, bool partial_out, hipStream_t st) {
+  if (M == 0 || N == 0) return 0;
+  if (K % 16) throw std::runtime_error("gemm_packed: K must be a multiple of 16");
+  if (glu && (N % 32)) throw std::runtime_error("gemm_packed: glu needs N % 32 == 0");
+  int tsel, ns, s;
+  packed_plan(M, N, K, glu, nt_hint, split_hint, &tsel, &ns, &s);
+  if ((int64_t)s * M * N * 4 > ws_bytes) s = 1;
+  const int g = glu ? 1 : 0;
+  const bool keep = s > 1 && partial_out && !g && act == 0;
+  if (!y && !keep) throw std::runtime_error("gemm_packed: this configuration writes the output, but no output buffer");
+  auto Y = (bf16_t*)y;
+  auto B = (const bf16_t*)bias;
+  float* part = s > 1 ? (float*)workspace : nullptr;
+  int bm, bn;
+  tile_dims(tsel, &bm, &bn);
+  launch_gemm_mid(tsel, ns, M <= bm, (const bf16_t*)x, ldx, (const bf16_t*)w, k64, B, Y, ldy, part, M, N, K,
+                  s > 1 ? 0 : act, s > 1 ? 0 : g, s, st, true);
+  if (keep) return s;
+  if (s > 1) {
+    const int nout = g ? N / 2 : N;
+    dim3 rgrid(std::min((nout + 255) / 256, 64), M);
+    splitk_reduce_kernel<<<rgrid, 256, 0, st>>>(part, s, M, N, B, Y, ldy, act, g);
+    HIP_CHECK_LAUNCH();
+  }
+  return 0;
 }

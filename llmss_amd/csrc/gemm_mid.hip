@@ -22,7 +22,7 @@
 // the buffer builtins is cast to uint32_t explicitly: otherwise the host compilation pass of this
 // template fails overload resolution quietly and hipcc drops the kernel's launch stub (undefined
 // __device_stub__ at link time, no diagnostic).
-template <int BM, int BN, int WM, int WN, int NS, bool WNT>
+template <int BM, int BN, int WM, int WN, int NS, bool WNT, bool PK>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                               const bf16_t* __restrict__ B, int64_t ldb,
                                                               const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
@@ -50,11 +50,16 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
   const int t0 = zk * per, t1 = min(nk_all, t0 + per);
 
   // descriptors start at this tile's first row; everything past the matrix end reads as zero
-  const uint64_t abytes = (uint64_t)(M - m0) * (uint64_t)lda * 2, bbytes = (uint64_t)(N - n0) * (uint64_t)ldb * 2;
+  // PK: weights packed [N/16][K64][16][64] (ldb = K64, the 64-wide k blocks per row): a k-step of a
+  // 16-row panel is one contiguous 2-KiB block, so a stage streams BN/16 such blocks instead of BN
+  // strided 128-B row pieces (+18 % HBM read rate, bench/stream_ceiling.hip)
+  const uint64_t abytes = (uint64_t)(M - m0) * (uint64_t)lda * 2;
+  const uint64_t bbytes = PK ? (uint64_t)((N - n0) / 16) * (uint64_t)ldb * 2048 : (uint64_t)(N - n0) * (uint64_t)ldb * 2;
+  const int64_t boff = PK ? (int64_t)(n0 / 16) * ldb * 1024 : (int64_t)n0 * ldb;
   const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(A + (int64_t)m0 * lda), (short)0,
                                                     (int)(abytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)abytes),
                                                     0x00020000);
-  const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(B + (int64_t)n0 * ldb), (short)0,
+  const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(B + boff), (short)0,
                                                     (int)(bbytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)bbytes),
                                                     0x00020000);
   uint32_t va[AL], vb[BL];  // per-lane byte offsets (row, source-swizzled chunk), fixed over k
@@ -66,25 +71,26 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
     const int row = (i * NW + w) * 8 + (lane >> 3);
-    vb[i] = (uint32_t)(row * ldb * 2 + (((lane & 7) ^ (row & 7)) << 4));
+    vb[i] = PK ? (uint32_t)((row >> 4) * ldb * 2048 + (row & 15) * 128 + (((lane & 7) ^ (row & 7)) << 4))
+               : (uint32_t)(row * ldb * 2 + (((lane & 7) ^ (row & 7)) << 4));
   }
   // one ring stage (k-step T_) into LDS slot SA_: AL + BL wave-instructions of 1 KiB (8 rows x 128 B);
   // the k position is the scalar soffset, the per-lane voffsets never change
 #define MID_STAGE(T_, SA_)                                                                                         \
   do {                                                                                                           \
     char* sA_ = (SA_);                                                                                           \
-    const int soff_ = (T_) * 128;                                                                                \
+    const int soff_ = (T_) * 128, sofb_ = (T_) * (PK ? 2048 : 128);                                             \
     if (!ktail || (T_) != nk_all - 1) {                                                                          \
       _Pragma("unroll") for (int i_ = 0; i_ < AL; ++i_)                                                           \
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)(sA_ + (i_ * NW + w) * 1024), 16, (uint32_t)va[i_], (uint32_t)soff_, 0, 0); \
       _Pragma("unroll") for (int i_ = 0; i_ < BL; ++i_)                                                           \
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (LDS_AS void*)(sA_ + A_BYTES + (i_ * NW + w) * 1024), 16, (uint32_t)vb[i_], \
-                                                 (uint32_t)soff_, 0, WNT ? 2 : 0); /* weights: read once per step, nt */ \
+                                                 (uint32_t)sofb_, 0, WNT ? 2 : 0); /* weights: read once per step, nt */ \
     } else { /* partial last k-step: k folded into the voffset, so the range check covers the row tail */     \
       _Pragma("unroll") for (int i_ = 0; i_ < AL; ++i_)                                                           \
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)(sA_ + (i_ * NW + w) * 1024), 16, (uint32_t)(va[i_] + soff_), (uint32_t)0, 0, 0); \
       _Pragma("unroll") for (int i_ = 0; i_ < BL; ++i_)                                                           \
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (LDS_AS void*)(sA_ + A_BYTES + (i_ * NW + w) * 1024), 16, (uint32_t)(vb[i_] + soff_), \
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (LDS_AS void*)(sA_ + A_BYTES + (i_ * NW + w) * 1024), 16, (uint32_t)(vb[i_] + sofb_), \
                                                  (uint32_t)0, 0, WNT ? 2 : 0);                                  \
     }                                                                                                            \
   } while (0)
@@ -127,17 +133,14 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
   int cur = 0;
   for (int t = t0; t < t1; ++t) {
     // stage t landed for this wave (younger stages stay in flight), then for every wave
-    const int younger = t1 - 1 - t;
-    if constexpr (NS >= 4) {
-      if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
-      else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if constexpr (NS == 3) {
-      if (younger >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // stages t+1 .. t+NS-2 may still be in flight: LOADS wave-instructions each
+    const int younger = min(t1 - 1 - t, NS - 2);
+    static_assert((NS - 2) * LOADS <= 63, "vmcnt immediate");
+    if (NS >= 6 && younger >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * LOADS) : "memory");
+    else if (NS >= 5 && younger == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * LOADS) : "memory");
+    else if (NS >= 4 && younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
+    else if (NS >= 3 && younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // raw barrier: in-flight loads survive it
     asm volatile("" ::: "memory");
@@ -181,46 +184,55 @@ bool gemm_mid_dims(int tsel, int* bm, int* bn, int* threads) {
 // largest ring depth <= want that fits the 160 KiB LDS
 static int mid_depth(int bm, int bn, int want) {
   const int stage = (bm + bn) * 128;
-  int ns = std::max(2, std::min(want, 6));
+  int ns = std::max(2, std::min(want, 6));  // 6: the deepest ring (64x128 at 144 KiB)
   while (ns > 2 && ns * stage > 160 * 1024) --ns;
   return ns;
 }
 
 void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
-                     int split, hipStream_t st) {
+                     int split, hipStream_t st, bool packed) {
   int bm, bn, thr;
   if (!gemm_mid_dims(tsel, &bm, &bn, &thr)) throw std::runtime_error("gemm_mid: bad tile code");
   if (glu && (bn / (thr / 64 / (bm == 256 ? 4 : (bm == 128 ? 2 : 1))) / 16) % 2)
     throw std::runtime_error("gemm_mid: SwiGLU needs an even number of 16-column tiles per wave");
-  if ((uint64_t)bm * ldx * 2 >= (1ull << 31) || (uint64_t)bn * ldw * 2 >= (1ull << 31))
+  if ((uint64_t)bm * ldx * 2 >= (1ull << 31) || (uint64_t)bn * ldw * (packed ? 128 : 2) >= (1ull << 31))
     throw std::runtime_error("gemm_mid: row stride too large for 32-bit buffer offsets");
+  if (packed && (N % 16 || (int64_t)ldw * 64 < K || (int64_t)ldw * 64 >= K + 64))
+    throw std::runtime_error("gemm_mid: packed weights need N % 16 == 0 and ldw = ceil(K / 64)");
   const int ns = mid_depth(bm, bn, depth);
   const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   dim3 grid(tiles, split);
+#define MID1(BM_, BN_, WM_, WN_, NS_, WNT_, PK_)                                                                   \
+  gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, WNT_, PK_><<<grid, 64 * WM_ * WN_, 0, st>>>(X, ldx, W, ldw, bias, Y, ldy, \
+                                                                                      part, M, N, K, act, glu)
 #define MID(BM_, BN_, WM_, WN_, NS_)                                                                             \
   do {                                                                                                         \
-    if (wnt)                                                                                                   \
-      gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, true><<<grid, 64 * WM_ * WN_, 0, st>>>(X, ldx, W, ldw, bias, Y, ldy, \
-                                                                                    part, M, N, K, act, glu);  \
-    else                                                                                                       \
-      gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, false><<<grid, 64 * WM_ * WN_, 0, st>>>(X, ldx, W, ldw, bias, Y,  \
-                                                                                     ldy, part, M, N, K, act, glu); \
+    if (packed) {                                                                                              \
+      if (wnt) MID1(BM_, BN_, WM_, WN_, NS_, true, true); else MID1(BM_, BN_, WM_, WN_, NS_, false, true);     \
+    } else {                                                                                                   \
+      if (wnt) MID1(BM_, BN_, WM_, WN_, NS_, true, false); else MID1(BM_, BN_, WM_, WN_, NS_, false, false);   \
+    }                                                                                                          \
   } while (0)
 #define MID_NS(BM_, BN_, WM_, WN_)                                               \
   do {                                                                         \
-    if (ns >= 4) MID(BM_, BN_, WM_, WN_, 4);                                   \
+    if (ns >= 6) MID(BM_, BN_, WM_, WN_, 6);                                   \
+    else if (ns == 5) MID(BM_, BN_, WM_, WN_, 5);                              \
+    else if (ns == 4) MID(BM_, BN_, WM_, WN_, 4);                              \
     else if (ns == 3) MID(BM_, BN_, WM_, WN_, 3);                              \
     else MID(BM_, BN_, WM_, WN_, 2);                                           \
   } while (0)
   switch (tsel) {
-    case 8: MID_NS(128, 128, 2, 2); break;
+    case 8: if (ns >= 5) MID(128, 128, 2, 2, 5); else if (ns == 4) MID(128, 128, 2, 2, 4);
+            else if (ns == 3) MID(128, 128, 2, 2, 3); else MID(128, 128, 2, 2, 2); break;
     case 9: if (ns >= 3) MID(256, 128, 4, 2, 3); else MID(256, 128, 4, 2, 2); break;
-    case 10: if (ns >= 3) MID(64, 256, 1, 4, 3); else MID(64, 256, 1, 4, 2); break;
+    case 10: if (ns >= 4) MID(64, 256, 1, 4, 4); else if (ns == 3) MID(64, 256, 1, 4, 3);
+             else MID(64, 256, 1, 4, 2); break;
     case 11: MID_NS(64, 128, 1, 4); break;
     case 12: if (ns >= 3) MID(128, 256, 2, 4, 3); else MID(128, 256, 2, 4, 2); break;
   }
 #undef MID_NS
 #undef MID
+#undef MID1
   HIP_CHECK_LAUNCH();
 }

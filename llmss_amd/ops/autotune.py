@@ -36,6 +36,20 @@ class GemmShape:
     fp8: bool = False
     partial: bool = False  # consumer sums split-K slabs itself
     act: str = "none"
+    packed: bool = False  # panel-packed bf16 weights (gemm_mid kernels only)
+
+
+def packed_candidates(M: int, N: int, K: int, glu: bool) -> List[Tuple[int, int]]:
+    """(nt_hint, split) pairs for panel-packed weights: gemm_mid tiles x ring depth x split-K (odd
+    splits too: with one workgroup per CU a grid just over 256 workgroups runs a nearly empty second
+    wave, so the best split is the one whose grid lands just under a multiple of the CU count)."""
+    mids = [(11, 16), (11, 32), (10, 16), (10, 32)]
+    if M > 64:
+        mids += [(8, 16), (8, 32), (12, 16)]
+    if M >= 256:
+        mids += [(9, 16)]
+    nk = -(-K // 64)
+    return [((t | d) << 8, s) for t, d in mids for s in (1, 2, 3, 4, 5, 6, 8) if nk // s >= 2]
 
 
 def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, int]]:
@@ -110,6 +124,8 @@ def tune_shape(M: int, shape: GemmShape, device, weight_budget: int = 600 << 20,
         sc = torch.full((N,), 1e-2, device=device)
     else:
         base = (torch.randn(N, K, device=device, generator=g) * K ** -0.5).to(torch.bfloat16)
+        if shape.packed:
+            base = H.pack_weight(base)
         ws = [base.clone() for _ in range(ncopy)]
         sc = None
     nout = N // 2 if shape.glu else N
@@ -135,7 +151,9 @@ def tune_shape(M: int, shape: GemmShape, device, weight_budget: int = 600 << 20,
 
     default = cost(0, 0)
     best = (0, 0, default)
-    for nt, s in (cands if cands is not None else candidates(M, N, K, shape.glu, shape.fp8)):
+    if cands is None:
+        cands = packed_candidates(M, N, K, shape.glu) if shape.packed else candidates(M, N, K, shape.glu, shape.fp8)
+    for nt, s in cands:
         try:
             t = cost(nt, s)
         except (ValueError, RuntimeError):  # config rejected by host-side validation
@@ -151,14 +169,11 @@ def model_shapes(model) -> Dict[str, GemmShape]:
     L = model.w.layers[0]
     fuse = model.tp.size == 1 and not model.cfg.parallel_block
     act = model.act if not L.up.glu else "none"
-    out = {
-        "qkv": GemmShape(L.qkv.w.shape[0], L.qkv.w.shape[1], False, L.qkv.w_scale is not None, True),
-        "o": GemmShape(L.o.w.shape[0], L.o.w.shape[1], False, L.o.w_scale is not None, fuse),
-        "up": GemmShape(L.up.w.shape[0], L.up.w.shape[1], L.up.glu, L.up.w_scale is not None, False, act),
-        "down": GemmShape(L.down.w.shape[0], L.down.w.shape[1], False, L.down.w_scale is not None, fuse),
-    }
-    head = model.w.head
-    out["head"] = GemmShape(head.w.shape[0], head.w.shape[1], False, head.w_scale is not None, False)
+    def shp(lin, partial, act_="none"):
+        return GemmShape(lin.N, lin.K, lin.glu, lin.w_scale is not None, partial, act_, lin.packed)
+
+    out = {"qkv": shp(L.qkv, True), "o": shp(L.o, fuse), "up": shp(L.up, False, act), "down": shp(L.down, fuse)}
+    out["head"] = shp(model.w.head, False)
     return out
 
 
@@ -183,7 +198,7 @@ def tune_model(model, ms: Sequence[int], native=None) -> Dict[Tuple[str, int], T
                 done[key] = tune_shape(M, shp, dev)
             nt, s, t, t0_us = done[key]
             if nt:
-                lib.gemm_tuned_set(M, shp.N, shp.K, shp.glu, shp.fp8, nt, s)
+                lib.gemm_tuned_set(M, shp.N, shp.K, shp.glu, 2 if shp.packed else int(shp.fp8), nt, s)
             res[(name, M)] = done[key]
     torch.cuda.synchronize(dev)
     gain = sum(v[3] - v[2] for v in res.values())
