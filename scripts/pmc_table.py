@@ -5,6 +5,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 
@@ -19,11 +20,11 @@ def main():
         for run in glob.glob(os.path.join(d, f"{c}_p*")):
             for f in glob.glob(os.path.join(run, "**", "*counter_collection.csv"), recursive=True):
                 for r in csv.DictReader(open(f)):
-                    if match in r["Kernel_Name"]:
+                    if re.search(match, r["Kernel_Name"]):
                         agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
             for f in glob.glob(os.path.join(run, "**", "*kernel_trace.csv"), recursive=True):
                 durs += [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(f))
-                         if match in r["Kernel_Name"]]
+                         if re.search(match, r["Kernel_Name"])]
         row = {k: sum(v) / len(v) for k, v in agg.items()}
         if durs:
             durs.sort()
