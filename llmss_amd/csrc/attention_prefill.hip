@@ -141,16 +141,219 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const bf16_t* __restr
   }
 }
 
-void launch_attn_prefill(const void* qkv, int64_t row_stride, const void* cu_seqlens, void* out, int64_t out_stride,
-                         int B, int max_seqlen, int nh, int nkv, int D, int k_off, int v_off, float scale,
-                         hipStream_t st) {
+// ------------------------------------------------------------------------------------------------
+// v2: K/V tiles staged by LDS-DMA (buffer_load ... lds) into a two-slot ring, so tile j+1 streams in
+// while tile j is computed (v1 above waits for register-staged loads before every tile); each wave
+// owns QB 16-row query blocks, so every K / V fragment read from LDS feeds QB MFMAs; a workgroup
+// serves GH query heads of one kv head (GQA: the K/V tile is loaded once for all of them); query
+// blocks are dispatched last-first so the long causal rows start early.
+// LDS rows are unpadded (DMA writes 1 KiB per wave-instruction linearly) with the 16-B chunk index
+// XOR-swizzled by the row: chunk' = chunk ^ (row & (SW-1)), applied on the source side of the DMA.
+template <int D, int QB>
+__global__ __launch_bounds__(256, 2) void attn_prefill_v2_kernel(const bf16_t* __restrict__ qkv, int64_t row_stride,
+                                                                 int T, const int* __restrict__ cu_seqlens,
+                                                                 bf16_t* __restrict__ out, int64_t out_stride, int nh,
+                                                                 int nkv, int GH, int k_off, int v_off,
+                                                                 float scale_log2) {
+  constexpr int BKV = 64;
+  constexpr int CH = D / 8;                    // 16-B chunks per row
+  constexpr int SW = CH < 16 ? CH : 16;        // swizzle span (conflict-free b128 reads of 16 rows)
+  constexpr int TILE = BKV * D * 2;            // bytes of one K (or V) tile
+  constexpr int RPI = 64 / CH;                 // rows per 1-KiB DMA wave-instruction
+  constexpr int LPW = BKV / RPI / 4;           // DMA instructions per wave per tile (K and V each)
+  static_assert(LPW >= 1, "tile / wave split");
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];  // [slot][K, V]
+
+  const int G = nh / nkv;
+  const int WPH = 4 / GH;                      // waves per query head
+  const int BQ = WPH * 16 * QB;
+  const int nqb = gridDim.x;
+  const int qb = nqb - 1 - (int)blockIdx.x;    // heavy (late) query blocks first
+  const int b = blockIdx.z;
+  const int ngrp = G / GH;
+  const int kvh = blockIdx.y / ngrp, grp = blockIdx.y % ngrp;
+  const int tok0 = cu_seqlens[b];
+  const int len = cu_seqlens[b + 1] - tok0;
+  const int q0 = qb * BQ;
+  if (q0 >= len) return;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  const int h = kvh * G + grp * GH + w / WPH;
+  const int wrow = q0 + (w % WPH) * 16 * QB;   // first query row of this wave
+
+  // K / V descriptors from this sequence's first row; rows past the qkv tensor read as zero
+  const uint64_t bytes = (uint64_t)(T - tok0) * (uint64_t)row_stride * 2;
+  const uint32_t nrec = bytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)bytes;
+  const bf16_t* base = qkv + (int64_t)tok0 * row_stride + (int64_t)kvh * D;
+  const auto rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base + k_off), (short)0, (int)nrec, 0x00020000);
+  const auto rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(base + v_off), (short)0, (int)nrec, 0x00020000);
+  uint32_t voff[LPW];                          // per-lane (row, source-swizzled chunk) of each instruction
+#pragma unroll
+  for (int i = 0; i < LPW; ++i) {
+    const int r = (i * 4 + w) * RPI + lane / CH, c = lane % CH;
+    voff[i] = (uint32_t)(r * row_stride * 2 + ((c ^ (r & (SW - 1))) << 4));
+  }
+  // k position folded into the voffset (the range check covers voffset), soffset 0
+#define PF_STAGE(J_)                                                                                           \
+  do {                                                                                                         \
+    char* sk_ = smem + ((J_) & 1) * 2 * TILE;                                                                  \
+    const uint32_t kb_ = (uint32_t)((J_) * BKV) * (uint32_t)row_stride * 2u;                                   \
+    _Pragma("unroll") for (int i_ = 0; i_ < LPW; ++i_) {                                                       \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (LDS_AS void*)(sk_ + (i_ * 4 + w) * 1024), 16,              \
+                                               (uint32_t)(voff[i_] + kb_), (uint32_t)0, 0, 0);                 \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (LDS_AS void*)(sk_ + TILE + (i_ * 4 + w) * 1024), 16,       \
+                                               (uint32_t)(voff[i_] + kb_), (uint32_t)0, 0, 0);                 \
+    }                                                                                                          \
+  } while (0)
+
+  // Q^T fragments (B operand) of the wave's QB row blocks: lane holds Q[row][32ks + 8g .. +7]
+  s16x8 qf[QB][D / 32];
+#pragma unroll
+  for (int qi = 0; qi < QB; ++qi) {
+    const int r = min(wrow + qi * 16 + li, len - 1);
+    const bf16_t* qp = qkv + (int64_t)(tok0 + r) * row_stride + (int64_t)h * D + 8 * g;
+#pragma unroll
+    for (int ks = 0; ks < D / 32; ++ks) qf[qi][ks] = *reinterpret_cast<const s16x8*>(qp + 32 * ks);
+  }
+  f32x4 o[QB][D / 16];
+  float m[QB], lsum[QB];
+#pragma unroll
+  for (int qi = 0; qi < QB; ++qi) {
+    m[qi] = -1.0e30f;
+    lsum[qi] = 0.f;
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) o[qi][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  const int kv_end = min(len, q0 + BQ);        // causal: no key past the block's last query row
+  const int ntiles = (kv_end + BKV - 1) / BKV;
+  const int w_hi = wrow + 16 * QB - 1;         // this wave's last query row
+  const int tq = li >> 2, tp = li & 3;         // transpose-read lane roles (row q, 4 columns 4p..4p+3)
+  PF_STAGE(0);
+  for (int j = 0; j < ntiles; ++j) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();              // tile j landed for every wave; slot (j+1)&1 is free
+    asm volatile("" ::: "memory");
+    if (j + 1 < ntiles) PF_STAGE(j + 1);
+    const int kv0 = j * BKV;
+    if (kv0 > w_hi) continue;                  // the whole tile is in this wave's causal future
+    const char* Ks = smem + (j & 1) * 2 * TILE;
+    const char* Vs = Ks + TILE;
+
+    // ---- S^T = K Q^T: 4 key tiles of 16, each K fragment feeds QB MFMAs -------------------------
+    f32x4 s[QB][4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+      for (int qi = 0; qi < QB; ++qi) s[qi][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int r = kt * 16 + li;
+#pragma unroll
+      for (int ks = 0; ks < D / 32; ++ks) {
+        const s16x8 kf = *reinterpret_cast<const s16x8*>(Ks + r * D * 2 + (((4 * ks + g) ^ (r & (SW - 1))) << 4));
+#pragma unroll
+        for (int qi = 0; qi < QB; ++qi) s[qi][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qi][ks], s[qi][kt], 0, 0, 0);
+      }
+    }
+    // ---- mask + online softmax per row block (lane owns query row wrow + 16 qi + li) -------------
+    s16x8 pf[QB][2];
+#pragma unroll
+    for (int qi = 0; qi < QB; ++qi) {
+      const int qrow = wrow + qi * 16 + li;
+      float mx = m[qi];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = kv0 + kt * 16 + 4 * g + i;
+          float v = s[qi][kt][i] * scale_log2;
+          v = (key <= qrow && key < len) ? v : -1.0e30f;
+          s[qi][kt][i] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = xor32_max(xor16_max(mx));
+      const float alpha = exp2f(m[qi] - mx);
+      m[qi] = mx;
+      float ps = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bf16_t pb = f2bf(exp2f(s[qi][kt][i] - mx));
+          ps += bf2f(pb);
+          pf[qi][kt >> 1][(kt & 1) * 4 + i] = (short)pb;
+        }
+      ps = xor32_sum(xor16_sum(ps));
+      lsum[qi] = lsum[qi] * alpha + ps;
+#pragma unroll
+      for (int i = 0; i < D / 16; ++i) o[qi][i] *= alpha;
+    }
+    // ---- O^T += V^T P^T (V^T by transpose reads of the swizzled V tile), each V fragment feeds QB MFMAs
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int r0 = 32 * ks + 4 * g + tq, r1 = r0 + 16;
+#pragma unroll
+      for (int dt = 0; dt < D / 16; ++dt) {
+        const int c = 2 * dt + (tp >> 1);
+        const char* a0 = Vs + r0 * D * 2 + ((c ^ (r0 & (SW - 1))) << 4) + (tp & 1) * 8;
+        const char* a1 = Vs + r1 * D * 2 + ((c ^ (r1 & (SW - 1))) << 4) + (tp & 1) * 8;
+        const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a0));
+        const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(a1));
+        const s16x8 vf = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+        for (int qi = 0; qi < QB; ++qi) o[qi][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qi][ks], o[qi][dt], 0, 0, 0);
+      }
+    }
+  }
+#undef PF_STAGE
+#pragma unroll
+  for (int qi = 0; qi < QB; ++qi) {
+    const int qrow = wrow + qi * 16 + li;
+    if (qrow >= len) continue;
+    const float inv = lsum[qi] > 0.f ? 1.f / lsum[qi] : 0.f;
+    bf16_t* op = out + (int64_t)(tok0 + qrow) * out_stride + (int64_t)h * D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      u16x4 r;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = f2bf(o[qi][dt][i] * inv);
+      *reinterpret_cast<u16x4*>(op + dt * 16) = r;
+    }
+  }
+}
+
+static int g_prefill_version = 2;
+void attn_prefill_set_version(int v) { g_prefill_version = v == 1 ? 1 : 2; }
+
+void launch_attn_prefill(const void* qkv, int64_t row_stride, int T, const void* cu_seqlens, void* out,
+                         int64_t out_stride, int B, int max_seqlen, int nh, int nkv, int D, int k_off, int v_off,
+                         float scale, hipStream_t st) {
   if (nh % nkv) throw std::runtime_error("attn_prefill: nh must be a multiple of nkv");
   if (B == 0 || max_seqlen == 0) return;
-  dim3 grid((max_seqlen + 63) / 64, nh, B);
   auto Q = (const bf16_t*)qkv;
   auto CU = (const int*)cu_seqlens;
   auto O = (bf16_t*)out;
   const float sl = scale * kLog2eP;
+  // v2 except where v1 measured faster (bench/attn_prefill_bench.py, profiles/r2_prefill_attn): D = 256
+  // (GPT-J: one row block per wave fits the registers) and D = 64 beyond 2K-token sequences
+  if (g_prefill_version == 2 && D != 256 && !(D == 64 && max_seqlen > 2048)) {
+    if (row_stride % 8 || k_off % 8 || v_off % 8)
+      throw std::runtime_error("attn_prefill: 16-B aligned rows and k/v offsets required");
+    if ((uint64_t)64 * row_stride * 2 >= (1ull << 31)) throw std::runtime_error("attn_prefill: row stride too large");
+    const int G = nh / nkv;
+    const int GH = G % 4 == 0 ? 4 : (G % 2 == 0 ? 2 : 1);
+    const int QB = 2;
+    const int BQ = (4 / GH) * 16 * QB;
+    dim3 grid((max_seqlen + BQ - 1) / BQ, nkv * (G / GH), B);
+    switch (D) {
+      case 64: attn_prefill_v2_kernel<64, 2><<<grid, 256, 0, st>>>(Q, row_stride, T, CU, O, out_stride, nh, nkv, GH, k_off, v_off, sl); break;
+      case 128: attn_prefill_v2_kernel<128, 2><<<grid, 256, 0, st>>>(Q, row_stride, T, CU, O, out_stride, nh, nkv, GH, k_off, v_off, sl); break;
+      default: throw std::runtime_error("attn_prefill: head_dim must be 64, 128 or 256");
+    }
+    HIP_CHECK_LAUNCH();
+    return;
+  }
+  dim3 grid((max_seqlen + 63) / 64, nh, B);
   switch (D) {
     case 64: attn_prefill_kernel<64><<<grid, 256, 0, st>>>(Q, row_stride, CU, O, out_stride, nh, nkv, k_off, v_off, sl); break;
     case 128: attn_prefill_kernel<128><<<grid, 256, 0, st>>>(Q, row_stride, CU, O, out_stride, nh, nkv, k_off, v_off, sl); break;

@@ -22,9 +22,10 @@ void launch_attn_decode(const void* q, int64_t q_stride, const void* kc, const v
                         int bt_stride, const void* ctx_lens, void* out, int64_t out_stride, void* part_o,
                         void* part_ml, int B, int nh, int nkv, int D, int block_size, int nsplit, int part_size,
                         float scale, hipStream_t st);
-void launch_attn_prefill(const void* qkv, int64_t row_stride, const void* cu_seqlens, void* out, int64_t out_stride,
-                         int B, int max_seqlen, int nh, int nkv, int D, int k_off, int v_off, float scale,
-                         hipStream_t st);
+void launch_attn_prefill(const void* qkv, int64_t row_stride, int T, const void* cu_seqlens, void* out,
+                         int64_t out_stride, int B, int max_seqlen, int nh, int nkv, int D, int k_off, int v_off,
+                         float scale, hipStream_t st);
+void attn_prefill_set_version(int v);
 void launch_cand_topk(const void* logits, int64_t ld, int B, int vl, int lo, int V, const void* temperature,
                       const void* top_k, int K, int KC, void* pack, int64_t ldp, hipStream_t st);
 void launch_sample_cand(const void* pack, int64_t ldp, int B, int groups, int KC, const void* temperature,
@@ -103,10 +104,11 @@ PYBIND11_MODULE(_C, m) {
                              style, k_off, v_off, P(kc), P(vc), CP(bt), bts, CP(cl), P(out), os, P(po), P(pml), B, nh,
                              nkv, D, bs, nsplit, psize, scale, S(st));
   });
-  m.def("attn_prefill", [](uintptr_t qkv, int64_t rs, uintptr_t cu, uintptr_t out, int64_t os, int B, int maxlen,
-                           int nh, int nkv, int D, int k_off, int v_off, float scale, uintptr_t st) {
-    launch_attn_prefill(CP(qkv), rs, CP(cu), P(out), os, B, maxlen, nh, nkv, D, k_off, v_off, scale, S(st));
+  m.def("attn_prefill", [](uintptr_t qkv, int64_t rs, int T, uintptr_t cu, uintptr_t out, int64_t os, int B,
+                           int maxlen, int nh, int nkv, int D, int k_off, int v_off, float scale, uintptr_t st) {
+    launch_attn_prefill(CP(qkv), rs, T, CP(cu), P(out), os, B, maxlen, nh, nkv, D, k_off, v_off, scale, S(st));
   });
+  m.def("attn_prefill_set_version", &attn_prefill_set_version);
   m.def("cand_topk", [](uintptr_t lg, int64_t ld, int B, int vl, int lo, int V, uintptr_t temp, uintptr_t topk, int K,
                         int KC, uintptr_t pack, int64_t ldp, uintptr_t st) {
     launch_cand_topk(CP(lg), ld, B, vl, lo, V, CP(temp), CP(topk), K, KC, P(pack), ldp, S(st));

@@ -107,6 +107,23 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // one K-slice: its L2 fetches each weight tile once for every M-tile and only its K-slice of the
 // activations. Measured on the TP=8 QKV shape (M=512, N=1536, K=4096): the M-major order fetched
 // 59 MB from the fabric for 16.6 MB of unique operands.
+// Reductions over lane pairs (lane, lane ^ 16) / (lane, lane ^ 32) by the gfx950 permlane swaps (VALU,
+// no LDS round trip like ds_bpermute-based __shfl_xor): swapping two copies of x leaves x and its
+// partner's x in the two registers, in some order - symmetric ops need no fix-up. Inline asm (with the
+// 2 wait states the swap needs after a VALU write of its operands): through the builtins hipcc treats
+// the two results as one value and drops the partner.
+template <bool P32>
+__device__ __forceinline__ f32x2 swap_pair(float x) {
+  unsigned a = __builtin_bit_cast(unsigned, x), b = a;
+  if constexpr (P32) asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  else asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  return f32x2{__builtin_bit_cast(float, a), __builtin_bit_cast(float, b)};
+}
+__device__ __forceinline__ float xor16_max(float x) { const f32x2 r = swap_pair<false>(x); return fmaxf(r[0], r[1]); }
+__device__ __forceinline__ float xor32_max(float x) { const f32x2 r = swap_pair<true>(x); return fmaxf(r[0], r[1]); }
+__device__ __forceinline__ float xor16_sum(float x) { const f32x2 r = swap_pair<false>(x); return r[0] + r[1]; }
+__device__ __forceinline__ float xor32_sum(float x) { const f32x2 r = swap_pair<true>(x); return r[0] + r[1]; }
+
 struct TileWork {
   int m0, n0, z;
 };

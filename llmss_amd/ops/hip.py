@@ -145,7 +145,8 @@ def attn_prefill(qkv, cu_seqlens, max_seqlen, nh, nkv, D, scale, out=None):
     B = cu_seqlens.numel() - 1
     y = out if out is not None else torch.empty(T, nh * D, dtype=qkv.dtype, device=qkv.device)
     _bf16_rows(y, "out")
-    lib().attn_prefill(qkv.data_ptr(), qkv.stride(0), cu_seqlens.data_ptr(), y.data_ptr(), y.stride(0), B,
+    _check(qkv.stride(0) % 8 == 0 and qkv.data_ptr() % 16 == 0, "qkv rows 16-B aligned")
+    lib().attn_prefill(qkv.data_ptr(), qkv.stride(0), T, cu_seqlens.data_ptr(), y.data_ptr(), y.stride(0), B,
                        int(max_seqlen), nh, nkv, D, nh * D, (nh + nkv) * D, float(scale), _stream())
     return y
 

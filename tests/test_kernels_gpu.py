@@ -101,15 +101,25 @@ def test_rope_cache_from_split_k_partials(style, T):
     close(vc1, vc2, 2e-2)
 
 
-@pytest.mark.parametrize("D,nh,nkv", [(64, 4, 4), (128, 8, 2), (128, 16, 1), (256, 4, 4)])
-def test_attn_prefill(D, nh, nkv):
+@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("D,nh,nkv", [(64, 4, 4), (128, 8, 2), (128, 16, 1), (256, 4, 4), (128, 12, 4), (128, 16, 2),
+                                      (64, 6, 3), (256, 8, 2)])
+def test_attn_prefill(D, nh, nkv, version):
+    """v1 (register-staged tiles) and v2 (LDS-DMA two-slot ring, 2 row blocks per wave, GQA heads
+    sharing a K/V tile) against the fp32 oracle; qkv as a row-strided view, NaN-filled output."""
     torch.manual_seed(0)
-    lens = [1, 70, 129, 5]
+    lens = [1, 70, 129, 5, 300]
     T = sum(lens)
-    qkv = rnd(T, (nh + 2 * nkv) * D)
+    W = (nh + 2 * nkv) * D
+    qkv = rnd(T, W + 64)[:, :W]  # row stride > width (as a fused-QKV view would have)
     cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=dev)
     sc = 1 / math.sqrt(D)
-    out = H.attn_prefill(qkv, cu, max(lens), nh, nkv, D, sc)
+    H.lib().attn_prefill_set_version(version)
+    try:
+        out = torch.full((T, nh * D), float("nan"), dtype=torch.bfloat16, device=dev)
+        H.attn_prefill(qkv, cu, max(lens), nh, nkv, D, sc, out=out)
+    finally:
+        H.lib().attn_prefill_set_version(2)
     ref = R.attn_prefill(qkv.float(), cu.cpu(), nh, nkv, D, sc)
     close(out, ref, 2e-2)
 
