@@ -222,7 +222,8 @@ class LLMEngine:
                 "buckets": list(self.buckets), "graphs": bool(self.use_graphs),
                 "async_decode": self.async_decode, "eos": self.eos, "prefill_chunk": self.prefill_chunk,
                 "dist_sampling": self.dist_sampling,
-                "overlap_rows": self.model.overlap_rows, "tbo_min": self.model.tbo_min,
+                "overlap_rows": self.model.overlap_rows, "bucket_bytes": self.model.bucket_bytes,
+                "tbo_min": self.model.tbo_min,
                 "fp8": any(L.qkv.w_scale is not None for L in self.model.w.layers[:1])}
 
     def _default_buckets(self):

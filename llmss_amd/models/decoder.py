@@ -74,8 +74,14 @@ class DecoderLM:
         self.scale = cfg.head_dim ** -0.5
         self.rms = cfg.norm == "rmsnorm"
         self.act = "none" if cfg.gated_mlp else cfg.activation
-        # TP all-reduce / GEMM overlap for large steps (prefill): row chunks of this many tokens
-        self.overlap_rows = int(os.environ.get("LLMSS_TP_OVERLAP_ROWS", "4096"))
+        # TP all-reduce / GEMM overlap: the row-parallel output is cut into row buckets of about
+        # `bucket_bytes` (LLMSS_TP_BUCKET_BYTES, default 32 MiB: a prefill chunk's all-reduce is then
+        # long enough to hide the next chunk's GEMM behind it, while each RCCL call stays in its
+        # bandwidth regime on xGMI); a decode step's few-MiB all-reduce stays one bucket unless the
+        # knob is lowered. LLMSS_TP_OVERLAP_ROWS / `overlap_rows` fixes the bucket in rows instead.
+        rows = os.environ.get("LLMSS_TP_OVERLAP_ROWS")
+        self.overlap_rows = int(rows) if rows else None
+        self.bucket_bytes = int(os.environ.get("LLMSS_TP_BUCKET_BYTES", str(32 << 20)))
         # fused RoPE+KV-write+attention decode: correct, but measured slower (its prologue halves the
         # attention kernel's occupancy), so opt-in
         self.fused_decode = os.environ.get("LLMSS_FUSED_DECODE", "0") == "1"
@@ -147,6 +153,17 @@ class DecoderLM:
                                  out=out[nd:])
         return out
 
+    def bucket_rows(self, M: int) -> int:
+        """Rows per all-reduce bucket of an M-row row-parallel output (>= M: one all-reduce)."""
+        if self.overlap_rows is not None:
+            return self.overlap_rows
+        row_bytes = self.cfg.hidden_size * 2
+        rows = max(8, self.bucket_bytes // row_bytes // 8 * 8)
+        if rows >= M:
+            return M
+        nb = -(-M // rows)  # equal buckets (a short last one would pay a full RCCL latency)
+        return (-(-M // nb) + 7) // 8 * 8
+
     def _comm(self, device):
         if self._comm_stream is None:
             self._comm_stream = torch.cuda.Stream(device=device, priority=-1)
@@ -163,7 +180,7 @@ class DecoderLM:
         if not self.tp.comm_active:
             return fn(*inputs)
         M = inputs[0].shape[0]
-        step = self.overlap_rows
+        step = self.bucket_rows(M)
         if M <= step or step <= 0:
             return self.tp.all_reduce(fn(*inputs))
         if not inputs[0].is_cuda:  # gloo / CPU: same chunking (numerics), no streams

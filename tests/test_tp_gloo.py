@@ -55,7 +55,7 @@ def _run(world, ckpt, prompts, env=None):
     return res
 
 
-# LLMSS_TP_OVERLAP_ROWS: row-chunked prefill all-reduce / GEMM overlap;
+# LLMSS_TP_OVERLAP_ROWS / LLMSS_TP_BUCKET_BYTES: row-bucketed all-reduce / GEMM overlap (rows, or bytes per bucket);
 # LLMSS_TP_DECODE_OVERLAP_MIN: decode steps as two interleaved micro-batches (the 3-sequence batch splits 1 + 2)
 _ROWS = {"LLMSS_TP_OVERLAP_ROWS": "4"}
 _TBO = {"LLMSS_TP_DECODE_OVERLAP_MIN": "2"}
@@ -64,6 +64,7 @@ _TBO = {"LLMSS_TP_DECODE_OVERLAP_MIN": "2"}
 @pytest.mark.parametrize("name,world,overlap", [("llama", 2, None), ("gptj", 2, None), ("bigcode", 4, None),
                                                 ("gpt2", 2, None), ("bigcode_mha", 2, None), ("llama", 2, _ROWS),
                                                 ("gptj", 2, {"LLMSS_TP_OVERLAP_ROWS": "5"}), ("llama", 2, _TBO),
+                                                ("llama", 2, {"LLMSS_TP_BUCKET_BYTES": "64"}),
                                                 ("gptj", 2, _TBO), ("bigcode", 4, _TBO)])
 def test_tp_matches_single(tmp_path, name, world, overlap):
     d = str(tmp_path / name)
