@@ -1,5 +1,18 @@
 """Per-request sampling parameters (mirrors the reference CLI/HTTP fields, generate.py:21-40,
-producer_server.py:9-15) plus the deterministic per-step seed used identically on every rank."""
+producer_server.py:9-15) plus the deterministic per-step seed used identically on every rank.
+
+Filter order. The reference builds HF warpers in the order TopP -> TopK -> Temperature
+(generate.py:111-119) but then inverts its own test (``if not list_of_warpers``), so the warpers
+are never applied: its effective sampler is plain multinomial sampling from softmax(logits) at
+temperature 1 whatever the flags say. Here the flags are honoured in the order HF ``generate()``
+applies them - temperature, then top-k, then top-p on the temperature-scaled distribution
+(csrc/sampling.hip, ops/reference.sample) - because that is what a caller of these flags expects
+and it keeps top-p's nucleus consistent with the distribution actually sampled. The reference's
+*stated* order would compute the nucleus at temperature 1 and rescale afterwards; the two agree
+whenever temperature == 1 (the reference's default) or when top-p == 1. The reference's *effective*
+behaviour is ``temperature=1.0, top_k=0, top_p=1.0`` (unfiltered multinomial sampling), which these
+parameters reproduce exactly.
+"""
 from __future__ import annotations
 
 import itertools
