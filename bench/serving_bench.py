@@ -9,6 +9,8 @@ token per character). Prints one JSON line: output tokens/s over the timed reque
 latency and p50 server-side TTFT.
 
 usage: python bench/serving_bench.py [--model gpt2-xl] [--mode grpc|pubsub] [--clients 64] [--requests 4]
+       python bench/serving_bench.py --rate 20 --num-requests 256 --long-frac 0.1 --long-len 2048   (open loop)
+Open loop compares scheduling policies: LLMSS_PREFILL_CHUNK=-1 (whole prompts) vs the default chunked prefill.
 """
 import argparse
 import concurrent.futures as cf
@@ -61,6 +63,71 @@ def run_clients(a):
                       "wall_s": round(el, 3)}), flush=True)
 
 
+def run_open_loop(a):
+    """Open-loop arrivals: `num_requests` requests at Poisson times of mean rate `rate` req/s, each streamed
+    (GenerateStream) so every token's arrival is timed on the client. A `long_frac` share of the prompts is
+    `long_len` characters long (the prompts that stall running decodes unless prefill is chunked).
+    Reports p50 / p99 of TTFT, of each request's mean time per output token, and of the worst gap
+    between two consecutive tokens of a request."""
+    import threading
+
+    import grpc
+
+    from llmss_amd.serving.grpc_api import GenerateRequest, Stub
+
+    rng = random.Random(0)
+    alphabet = string.ascii_letters + string.digits + " "
+    plan, t = [], 0.0
+    for i in range(a.num_requests):
+        t += rng.expovariate(a.rate)
+        n = a.long_len if rng.random() < a.long_frac else a.prompt_len
+        plan.append((t, "".join(rng.choice(alphabet) for _ in range(n))))
+    res = [None] * len(plan)
+    ch = grpc.insecure_channel(f"127.0.0.1:{a.client_port}")
+    stub = Stub(ch)
+    # warmup (not timed): one short and one long request
+    for n in (a.prompt_len, a.long_len):
+        stub.Generate(GenerateRequest(prompt="w" * n, max_new_tokens=4, is_greedy=True), timeout=600)
+
+    def one(i, prompt, t_arr):
+        times = []
+        for tok in stub.GenerateStream(GenerateRequest(prompt=prompt, max_new_tokens=a.gen_len, temperature=1.0,
+                                                       top_p=0.95, top_k=50, request_id=f"o{i}"), timeout=1200):
+            if tok.finished:
+                break
+            times.append(time.perf_counter())
+        res[i] = (t_arr, times, len(prompt))
+
+    t0 = time.perf_counter()
+    threads = []
+    for i, (ta, prompt) in enumerate(plan):
+        dt = t0 + ta - time.perf_counter()
+        if dt > 0:
+            time.sleep(dt)
+        th = threading.Thread(target=one, args=(i, prompt, time.perf_counter()))
+        th.start()
+        threads.append(th)
+    for th in threads:
+        th.join()
+    el = time.perf_counter() - t0
+    ch.close()
+    ttft = [r[1][0] - r[0] for r in res if r[1]]
+    tpot = [(r[1][-1] - r[1][0]) / (len(r[1]) - 1) for r in res if len(r[1]) > 1]
+    gap = [max(b - c for b, c in zip(r[1][1:], r[1][:-1])) for r in res if len(r[1]) > 1]
+    toks = sum(len(r[1]) for r in res)
+
+    def pct(v, q):
+        return round(float(np.percentile(v, q)) * 1e3, 2) if v else None
+
+    print(json.dumps({"metric": "serving_open_loop", "value": round(toks / el, 2), "unit": "tokens/s",
+                      "rate_rps": a.rate, "requests": len(res), "prompt_len": a.prompt_len, "long_len": a.long_len,
+                      "long_frac": a.long_frac, "gen_len": a.gen_len,
+                      "p50_ttft_ms": pct(ttft, 50), "p99_ttft_ms": pct(ttft, 99),
+                      "p50_tpot_ms": pct(tpot, 50), "p99_tpot_ms": pct(tpot, 99),
+                      "p50_max_token_gap_ms": pct(gap, 50), "p99_max_token_gap_ms": pct(gap, 99),
+                      "wall_s": round(el, 3)}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="gpt2-xl")
@@ -70,18 +137,23 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--gen-len", type=int, default=128)
     ap.add_argument("--fp8", action="store_true")
+    ap.add_argument("--rate", type=float, default=0.0, help="open loop: Poisson arrivals at this many requests/s")
+    ap.add_argument("--num-requests", type=int, default=256, help="open loop: requests in total")
+    ap.add_argument("--long-len", type=int, default=2048, help="open loop: length of the long prompts")
+    ap.add_argument("--long-frac", type=float, default=0.1, help="open loop: share of long prompts")
     ap.add_argument("--client-port", type=int, default=0, help=argparse.SUPPRESS)
     a = ap.parse_args()
 
     if a.client_port:
         if a.client_port < 0:  # spawned before the parent touched the GPU; the port comes on stdin
             a.client_port = int(sys.stdin.readline())
-        return run_clients(a)
+        return run_open_loop(a) if a.rate > 0 else run_clients(a)
 
     # the clients run in their own process (no GPU, no shared GIL with the engine loop); it is started
     # before this process initialises the GPU and learns the server port on stdin
     cmd = [sys.executable, os.path.abspath(__file__), "--client-port=-1"] + [
-        f"--{k.replace('_', '-')}={v}" for k, v in vars(a).items() if k in ("clients", "requests", "prompt_len", "gen_len")]
+        f"--{k.replace('_', '-')}={v}" for k, v in vars(a).items()
+        if k in ("clients", "requests", "prompt_len", "gen_len", "rate", "num_requests", "long_len", "long_frac")]
     child = subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
 
     import torch
@@ -96,8 +168,9 @@ def main():
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
     model = build_model(a.model, None, "bf16" if dev.type == "cuda" else "fp32", dev, fp8=a.fp8, random_init=True)
     tok = load_tokenizer(a.model, model.cfg.vocab_size)
+    longest = max(a.prompt_len, a.long_len if a.rate > 0 else 0)
     eng = LLMEngine(model, max_num_seqs=a.clients, max_batched_tokens=max(8192, a.clients * a.prompt_len),
-                    max_model_len=min(model.cfg.max_position_embeddings, a.prompt_len + a.gen_len + 8))
+                    max_model_len=min(model.cfg.max_position_embeddings, longest + a.gen_len + 8))
     drv = EngineDriver(eng).start()
     servers, consumer, mini = [], None, None
     if a.mode == "grpc":
@@ -111,7 +184,8 @@ def main():
     if child.returncode:
         raise RuntimeError(f"client process failed with exit code {child.returncode}")
     res = json.loads(out.strip().splitlines()[-1])
-    res.update(mode=a.mode, model=a.model, fp8=a.fp8, data="synthetic prompts, random-init weights")
+    res.update(mode=a.mode, model=a.model, fp8=a.fp8, data="synthetic prompts, random-init weights",
+               prefill_chunk=eng.prefill_chunk, engine_stats=eng.stats)
     print(json.dumps(res), flush=True)
     # orderly shutdown: front-ends first, then the engine thread, then device state
     for s in servers:
