@@ -101,12 +101,6 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
-// Split-K tiled GEMMs: linear block id -> (m0, n0, split z). Items are ordered z-major, then
-// N-tile, with the M-tiles of one N-tile adjacent, and each XCD receives a contiguous item range
-// (dispatch is round-robin over the linear id). An XCD therefore works on whole weight columns and
-// one K-slice: its L2 fetches each weight tile once for every M-tile and only its K-slice of the
-// activations. Measured on the TP=8 QKV shape (M=512, N=1536, K=4096): the M-major order fetched
-// 59 MB from the fabric for 16.6 MB of unique operands.
 // Reductions over lane pairs (lane, lane ^ 16) / (lane, lane ^ 32) by the gfx950 permlane swaps (VALU,
 // no LDS round trip like ds_bpermute-based __shfl_xor): swapping two copies of x leaves x and its
 // partner's x in the two registers, in some order - symmetric ops need no fix-up. Inline asm (with the
@@ -124,6 +118,12 @@ __device__ __forceinline__ float xor32_max(float x) { const f32x2 r = swap_pair<
 __device__ __forceinline__ float xor16_sum(float x) { const f32x2 r = swap_pair<false>(x); return r[0] + r[1]; }
 __device__ __forceinline__ float xor32_sum(float x) { const f32x2 r = swap_pair<true>(x); return r[0] + r[1]; }
 
+// Split-K tiled GEMMs: linear block id -> (m0, n0, split z). Items are ordered z-major, then
+// N-tile, with the M-tiles of one N-tile adjacent, and each XCD receives a contiguous item range
+// (dispatch is round-robin over the linear id). An XCD therefore works on whole weight columns and
+// one K-slice: its L2 fetches each weight tile once for every M-tile and only its K-slice of the
+// activations. Measured on the TP=8 QKV shape (M=512, N=1536, K=4096): the M-major order fetched
+// 59 MB from the fabric for 16.6 MB of unique operands.
 struct TileWork {
   int m0, n0, z;
 };

@@ -665,6 +665,10 @@ __global__ __launch_bounds__(64 * NW) void gemm_tiled_kernel(const bf16_t* __res
 // "Pipelining across barriers", 3-buffer-equivalent depth in 2 buffers).
 // Requires K % 64 == 0; rows beyond M / N are clamped on load and masked on store.
 // -------------------------------------------------------------------------------------------
+// M-tiles per tile group of the big-tile kernel's launch order (gemm_big_set_group; measured 4)
+static int g_big_group_m = 4;
+void gemm_big_set_group(int g) { g_big_group_m = g >= 1 && g <= 64 ? g : 4; }
+
 // one MX-fp8 16x16x128 MFMA from two 16-B fragment halves per operand (unit E8M0 block scales)
 __device__ __forceinline__ f32x4 mfma_f8x2(s16x8 a0, s16x8 a1, s16x8 b0, s16x8 b1, f32x4 c) {
   typedef int __attribute__((ext_vector_type(4))) i32x4_t;
@@ -685,7 +689,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict
                                                           const void* __restrict__ B, int64_t ldb,
                                                           const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
                                                           int64_t ldy, int M, int N, int K, int act, int glu,
-                                                          const float* __restrict__ xs, const float* __restrict__ ws) {
+                                                          const float* __restrict__ xs, const float* __restrict__ ws,
+                                                          int group_m) {
   constexpr int ES = F8 ? 1 : 2;  // operand bytes per element
   constexpr int HALF = 16384, BUF = 4 * HALF;
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
@@ -694,8 +699,14 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict
   const int li = lane & 15, g = lane >> 4;
   const int wr = w >> 2, wc = w & 3;
   const int ntn = (N + 255) / 256, ntm = (M + 255) / 256;
+  // XCD-contiguous tile ranges, grouped GM M-tiles high: the 32 workgroups an XCD runs at once cover a
+  // 4 x 8 block of tiles, so its L2 fills 4 A + 8 B panels per round instead of ~1 A + 32 B panels
+  // (PMC: 4 TB/s of L2 fills and 47 % of wave cycles waiting before this)
+  const int GM = group_m;
   const int tile = xcd_remap(blockIdx.x, ntn * ntm);
-  const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
+  const int grp = tile / (GM * ntn), gidx = tile - grp * (GM * ntn);
+  const int gm = min(GM, ntm - grp * GM);
+  const int m0 = (grp * GM + gidx % gm) * 256, n0 = (gidx / gm) * 256;
   const int nk = K * ES / 128;  // 128-byte K-tiles
 
   // staging: half h (0,1: A rows 128h.., 2,3: B rows 128(h-2)..), 2 x 1-KiB glds per wave; lane ->
@@ -795,6 +806,12 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict
     __builtin_amdgcn_s_setprio(0);
   }
 
+  if constexpr (!F8) {
+    // bf16: through LDS in row chunks, 16-B row stores (the 128 KiB ring is free after the last tile)
+    tile_store_lds<256, 256, 8, 4, 512, 2 * BUF>(acc, smem, wr * 128, wc * 64, m0, n0, M, N, nullptr, Y, ldy, bias,
+                                                 act, glu);
+    return;
+  }
   // epilogue (C layout: col = lane&15 -> n, row = 4*(lane>>4)+i -> m)
   const int wn0 = n0 + wc * 64;
 #pragma unroll
@@ -1166,7 +1183,7 @@ int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq
     if (K % 128) throw std::runtime_error("gemm_f8f8: the 256x256 tile needs K % 128 == 0");
     gemm_big_kernel<true><<<((M + 255) / 256) * ((N + 255) / 256), 512, 0, st>>>(
         xq, ldx, wq, ldw, (const bf16_t*)bias, (bf16_t*)y, ldy, M, N, K, act, glu ? 1 : 0, (const float*)xs,
-        (const float*)wsc);
+        (const float*)wsc, g_big_group_m);
     HIP_CHECK_LAUNCH();
     return 0;
   }
@@ -1526,7 +1543,7 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   if (f8 && tsel == 4) tsel = 1;
   if (tsel == 4) {
     gemm_big_kernel<false><<<tiles_of(M, N, 256, 256), 512, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, M, N, K, act, g,
-                                                                     nullptr, nullptr);
+                                                                     nullptr, nullptr, g_big_group_m);
     HIP_CHECK_LAUNCH();
     return 0;
   }
