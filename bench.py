@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--gen-len", type=int, default=128)
     ap.add_argument("--fp8", action="store_true")
+    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="paged KV cache storage: bf16, or fp8 e4m3 rows with per-row scales")
     ap.add_argument("--greedy", action="store_true")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--secondary", default="gpt2-xl",
@@ -88,7 +90,7 @@ def run_config(args, model_name, tp, batch, progress, dp=False):
     model = build_model(model_name, tp if not dp else None, "bf16", dev, fp8=args.fp8, random_init=True)
     max_len = min(model.cfg.max_position_embeddings, max(256, args.prompt_len + args.gen_len))
     eng = LLMEngine(model, max_num_seqs=local_batch, max_batched_tokens=max(8192, local_batch * args.prompt_len),
-                    block_size=16, max_model_len=max_len, use_graphs=not args.no_graphs)
+                    block_size=16, max_model_len=max_len, use_graphs=not args.no_graphs, kv_dtype=args.kv_dtype)
     rng = np.random.default_rng(1234 + (tp.rank if dp else 0))
     V = model.cfg.vocab_size
 
@@ -168,6 +170,7 @@ def run_config(args, model_name, tp, batch, progress, dp=False):
         "config": {"model": model_name, "global_batch": batch, "seq_len": args.prompt_len + args.gen_len,
                    "prompt_len": args.prompt_len, "gen_len": args.gen_len, "parallelism": par,
                    "sampling": "greedy" if args.greedy else "temperature=1.0,top_p=0.95,top_k=50",
+                   "kv_cache": args.kv_dtype,
                    "engine_stats": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()},
                    **({"phase_ms": eng.phase_summary()} if eng.timer.enabled else {})},
     }

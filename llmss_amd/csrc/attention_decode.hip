@@ -143,14 +143,23 @@ __device__ __forceinline__ float token_sum(float s) {
   return s;
 }
 
-template <int D, int GB, int UNROLL, bool FUSED, bool PIPE = false>
+// KV8: the paged cache holds fp8 rows (D e4m3 bytes + fp32 scale at byte D, 16-B tail; reference.py
+// kv_rows_quant): each lane loads 8 bytes per token instead of 16 and the row scales multiply the score
+// (K) and the probability (V) instead of every element.
+template <int D, int GB, int UNROLL, bool FUSED, bool PIPE = false, bool KV8 = false>
 __global__ __launch_bounds__(256, (!FUSED && GB == 1) ? 8 : 1) void attn_decode_kernel(
-    const bf16_t* __restrict__ q, int64_t q_stride, bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
+    const bf16_t* __restrict__ q, int64_t q_stride, void* __restrict__ kcv, void* __restrict__ vcv,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, bf16_t* __restrict__ out,
     int64_t out_stride, float* __restrict__ part_o, float* __restrict__ part_ml, int nh, int nkv, int G, int ngroups,
     int block_size, int part_size, float scale_log2, FusedRope fr) {
   constexpr int LPT = D / 8;
   constexpr int TPW = 64 / LPT;
+  constexpr int RB = KV8 ? D + 16 : D;  // cache row, in cache elements (bytes for fp8 rows)
+  static_assert(!(KV8 && FUSED), "the fused new-token path writes bf16 rows");
+  bf16_t* __restrict__ kc = (bf16_t*)kcv;
+  bf16_t* __restrict__ vc = (bf16_t*)vcv;
+  const unsigned char* __restrict__ kc8 = (const unsigned char*)kcv;
+  const unsigned char* __restrict__ vc8 = (const unsigned char*)vcv;
   const int b = blockIdx.x;
   const int kvh = blockIdx.y / ngroups, grp = blockIdx.y % ngroups;
   const int split = blockIdx.z, nsplit = gridDim.z;
@@ -204,8 +213,8 @@ __global__ __launch_bounds__(256, (!FUSED && GB == 1) ? 8 : 1) void attn_decode_
   const int start = split * part_size;
   const int end = min(ctx, start + part_size);
   const int* bt = block_tables + (int64_t)b * bt_stride;
-  const int64_t head_off = (int64_t)kvh * block_size * D + sub * 8;
-  const int64_t page_stride = (int64_t)nkv * block_size * D;
+  const int64_t head_off = (int64_t)kvh * block_size * RB + sub * 8;
+  const int64_t page_stride = (int64_t)nkv * block_size * RB;
   constexpr int STEP = 4 * TPW;  // tokens per workgroup-iteration
   // FUSED: the new token (position ctx-1) comes from registers, never from the cache this launch writes
   const bool has_new = FUSED && ctx >= 1 && end == ctx && start < end;
@@ -252,37 +261,63 @@ __global__ __launch_bounds__(256, (!FUSED && GB == 1) ? 8 : 1) void attn_decode_
   auto kv_addr = [&](int t) -> int64_t {
     const int pi = t / block_size;
     const int page = lds_pages ? s_pages[pi - pg0] : bt[pi];
-    return page * page_stride + head_off + (int64_t)(t % block_size) * D;
+    return page * page_stride + head_off + (int64_t)(t % block_size) * RB;
   };
-  auto load_tokens = [&](int tb, u16x8 (&kv)[UNROLL], u16x8 (&vv)[UNROLL]) {
+  // a token's K / V registers: bf16 rows 16 B per lane; fp8 rows 8 B per lane + the row's two scales
+  struct KVRegs {
+    u16x8 k[UNROLL], v[UNROLL];
+    u32x2 k8[UNROLL], v8[UNROLL];
+    float ks[UNROLL], vs[UNROLL];
+  };
+  auto load_tokens = [&](int tb, KVRegs& r) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const int t = tb + u * STEP;
       const int64_t a = kv_addr(t < lend ? t : start);
       // read once per step: non-temporal (guide 'nt-weights'; +10-15% on streamed reads)
-      kv[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(kc + a));
-      vv[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(vc + a));
+      if constexpr (KV8) {
+        r.k8[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(kc8 + a));
+        r.v8[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(vc8 + a));
+        r.ks[u] = *reinterpret_cast<const float*>(kc8 + a - sub * 8 + D);
+        r.vs[u] = *reinterpret_cast<const float*>(vc8 + a - sub * 8 + D);
+      } else {
+        r.k[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(kc + a));
+        r.v[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(vc + a));
+      }
     }
   };
-  auto consume = [&](int tb, const u16x8 (&kv)[UNROLL], const u16x8 (&vv)[UNROLL]) {
+  auto consume = [&](int tb, const KVRegs& r) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const bool ok = tb + u * STEP < lend;
-      float kf[8], vf[8];
+      float kf[8], vf[8], ks = 1.f, vs = 1.f;
+      if constexpr (KV8) {
+        const f32x2 k0 = __builtin_amdgcn_cvt_pk_f32_fp8(r.k8[u][0], false), k1 = __builtin_amdgcn_cvt_pk_f32_fp8(r.k8[u][0], true);
+        const f32x2 k2 = __builtin_amdgcn_cvt_pk_f32_fp8(r.k8[u][1], false), k3 = __builtin_amdgcn_cvt_pk_f32_fp8(r.k8[u][1], true);
+        const f32x2 v0 = __builtin_amdgcn_cvt_pk_f32_fp8(r.v8[u][0], false), v1 = __builtin_amdgcn_cvt_pk_f32_fp8(r.v8[u][0], true);
+        const f32x2 v2 = __builtin_amdgcn_cvt_pk_f32_fp8(r.v8[u][1], false), v3 = __builtin_amdgcn_cvt_pk_f32_fp8(r.v8[u][1], true);
+        kf[0] = k0[0]; kf[1] = k0[1]; kf[2] = k1[0]; kf[3] = k1[1]; kf[4] = k2[0]; kf[5] = k2[1]; kf[6] = k3[0]; kf[7] = k3[1];
+        vf[0] = v0[0]; vf[1] = v0[1]; vf[2] = v1[0]; vf[3] = v1[1]; vf[4] = v2[0]; vf[5] = v2[1]; vf[6] = v3[0]; vf[7] = v3[1];
+        ks = r.ks[u];
+        vs = r.vs[u];
+      } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { kf[j] = bf2f(kv[u][j]); vf[j] = bf2f(vv[u][j]); }
+        for (int j = 0; j < 8; ++j) { kf[j] = bf2f(r.k[u][j]); vf[j] = bf2f(r.v[u][j]); }
+      }
 #pragma unroll
       for (int h = 0; h < GB; ++h) {
         float s = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) s = fmaf(qv[h][j], kf[j], s);
         s = token_sum<LPT>(s);
+        if constexpr (KV8) s *= ks;
         if (ok) {
           const float mn = fmaxf(m[h], s);
           const float alpha = exp2f(m[h] - mn), p = exp2f(s - mn);
           l[h] = l[h] * alpha + p;
+          const float pv = KV8 ? p * vs : p;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[h][j] = fmaf(acc[h][j], alpha, p * vf[j]);
+          for (int j = 0; j < 8; ++j) acc[h][j] = fmaf(acc[h][j], alpha, pv * vf[j]);
           m[h] = mn;
         }
       }
@@ -292,21 +327,21 @@ __global__ __launch_bounds__(256, (!FUSED && GB == 1) ? 8 : 1) void attn_decode_
     // two register sets: the loads of the next UNROLL tokens per slot are in flight while the
     // current ones are consumed (the compiler's counted vmcnt waits only for the set it reads)
     constexpr int CH = STEP * UNROLL;
-    u16x8 kA[UNROLL], vA[UNROLL], kB[UNROLL], vB[UNROLL];
+    KVRegs A, Bq;
     int tb = start + w * TPW + slot;
-    if (start < lend) load_tokens(tb, kA, vA);
+    if (start < lend) load_tokens(tb, A);
     for (; tb - slot - w * TPW < lend; tb += 2 * CH) {
-      load_tokens(tb + CH, kB, vB);
-      consume(tb, kA, vA);
+      load_tokens(tb + CH, Bq);
+      consume(tb, A);
       if (tb + CH - slot - w * TPW >= lend) break;
-      load_tokens(tb + 2 * CH, kA, vA);
-      consume(tb + CH, kB, vB);
+      load_tokens(tb + 2 * CH, A);
+      consume(tb + CH, Bq);
     }
   } else {
     for (int tb = start + w * TPW + slot; tb < lend; tb += STEP * UNROLL) {
-      u16x8 kv[UNROLL], vv[UNROLL];
-      load_tokens(tb, kv, vv);
-      consume(tb, kv, vv);
+      KVRegs R;
+      load_tokens(tb, R);
+      consume(tb, R);
     }
   }
 
@@ -394,25 +429,31 @@ void attn_decode_set_unroll(int u) { g_decode_unroll = (u == 1 || u == 2 || u ==
 template <int D, int GB>
 static void launch_decode_t(const bf16_t* q, int64_t qs, bf16_t* kc, bf16_t* vc, const int* bt, int bts,
                             const int* cl, bf16_t* out, int64_t os, float* po, float* pml, int B, int nh, int nkv,
-                            int bs, int nsplit, int psize, float scale, hipStream_t st, const FusedRope* fr) {
+                            int bs, int nsplit, int psize, float scale, hipStream_t st, const FusedRope* fr, bool kv8) {
   const int G = nh / nkv;
   const int ngroups = (G + GB - 1) / GB;
   dim3 grid(B, nkv * ngroups, nsplit);
   const float sl2 = scale * kLog2e;
-#define AD(U_, FUSED_, PIPE_)                                                                                   \
-  attn_decode_kernel<D, GB, U_, FUSED_, PIPE_><<<grid, 256, 0, st>>>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, nh, \
-                                                                    nkv, G, ngroups, bs, psize, sl2,             \
-                                                                    fr ? *fr : FusedRope{})
+#define AD(U_, FUSED_, PIPE_, KV8_)                                                                               \
+  attn_decode_kernel<D, GB, U_, FUSED_, PIPE_, KV8_><<<grid, 256, 0, st>>>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, \
+                                                                          nh, nkv, G, ngroups, bs, psize, sl2,      \
+                                                                          fr ? *fr : FusedRope{})
   if (fr) {
-    AD(2, true, false);
+    AD(2, true, false, false);
+  } else if (kv8) {
+    switch (g_decode_unroll) {
+      case 2: AD(2, false, false, true); break;
+      case 12: AD(2, false, true, true); break;
+      default: AD(1, false, true, true); break;
+    }
   } else {
     switch (g_decode_unroll) {
-      case 1: AD(1, false, false); break;
-      case 2: AD(2, false, false); break;
-      case 4: AD(4, false, false); break;
-      case 12: AD(2, false, true); break;
-      case 14: AD(4, false, true); break;
-      default: AD(1, false, true); break;
+      case 1: AD(1, false, false, false); break;
+      case 2: AD(2, false, false, false); break;
+      case 4: AD(4, false, false, false); break;
+      case 12: AD(2, false, true, false); break;
+      case 14: AD(4, false, true, false); break;
+      default: AD(1, false, true, false); break;
     }
   }
 #undef AD
@@ -426,19 +467,20 @@ static void launch_decode_t(const bf16_t* q, int64_t qs, bf16_t* kc, bf16_t* vc,
 template <int D>
 static void launch_decode_d(const bf16_t* q, int64_t qs, bf16_t* kc, bf16_t* vc, const int* bt, int bts,
                             const int* cl, bf16_t* out, int64_t os, float* po, float* pml, int B, int nh, int nkv,
-                            int bs, int nsplit, int psize, float scale, hipStream_t st, const FusedRope* fr) {
+                            int bs, int nsplit, int psize, float scale, hipStream_t st, const FusedRope* fr, bool kv8) {
   const int G = nh / nkv;
-  if (G == 1) launch_decode_t<D, 1>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, fr);
-  else if (G == 2) launch_decode_t<D, 2>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, fr);
-  else if (G <= 4) launch_decode_t<D, 4>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, fr);
-  else launch_decode_t<D, 8>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, fr);
+  if (G == 1) launch_decode_t<D, 1>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, fr, kv8);
+  else if (G == 2) launch_decode_t<D, 2>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, fr, kv8);
+  else if (G <= 4) launch_decode_t<D, 4>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, fr, kv8);
+  else launch_decode_t<D, 8>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, fr, kv8);
 }
 
 static void attn_decode_dispatch(const void* q, int64_t q_stride, void* kc, void* vc, const void* block_tables,
                                  int bt_stride, const void* ctx_lens, void* out, int64_t out_stride, void* part_o,
                                  void* part_ml, int B, int nh, int nkv, int D, int block_size, int nsplit,
-                                 int part_size, float scale, hipStream_t st, const FusedRope* fr) {
+                                 int part_size, float scale, hipStream_t st, const FusedRope* fr, bool kv8 = false) {
   if (nh % nkv) throw std::runtime_error("attn_decode: nh must be a multiple of nkv");
+  if (kv8 && fr) throw std::runtime_error("attn_decode: the fused path writes bf16 cache rows");
   if (nsplit > 1 && (!part_o || !part_ml)) throw std::runtime_error("attn_decode: split needs workspaces");
   if (B == 0) return;
   auto Q = (const bf16_t*)q;
@@ -450,9 +492,9 @@ static void attn_decode_dispatch(const void* q, int64_t q_stride, void* kc, void
   auto PO = (float*)part_o;
   auto PML = (float*)part_ml;
   switch (D) {
-    case 64: launch_decode_d<64>(Q, q_stride, K, V, BT, bt_stride, CL, O, out_stride, PO, PML, B, nh, nkv, block_size, nsplit, part_size, scale, st, fr); break;
-    case 128: launch_decode_d<128>(Q, q_stride, K, V, BT, bt_stride, CL, O, out_stride, PO, PML, B, nh, nkv, block_size, nsplit, part_size, scale, st, fr); break;
-    case 256: launch_decode_d<256>(Q, q_stride, K, V, BT, bt_stride, CL, O, out_stride, PO, PML, B, nh, nkv, block_size, nsplit, part_size, scale, st, fr); break;
+    case 64: launch_decode_d<64>(Q, q_stride, K, V, BT, bt_stride, CL, O, out_stride, PO, PML, B, nh, nkv, block_size, nsplit, part_size, scale, st, fr, kv8); break;
+    case 128: launch_decode_d<128>(Q, q_stride, K, V, BT, bt_stride, CL, O, out_stride, PO, PML, B, nh, nkv, block_size, nsplit, part_size, scale, st, fr, kv8); break;
+    case 256: launch_decode_d<256>(Q, q_stride, K, V, BT, bt_stride, CL, O, out_stride, PO, PML, B, nh, nkv, block_size, nsplit, part_size, scale, st, fr, kv8); break;
     default: throw std::runtime_error("attn_decode: head_dim must be 64, 128 or 256");
   }
 }
@@ -460,10 +502,10 @@ static void attn_decode_dispatch(const void* q, int64_t q_stride, void* kc, void
 void launch_attn_decode(const void* q, int64_t q_stride, const void* kc, const void* vc, const void* block_tables,
                         int bt_stride, const void* ctx_lens, void* out, int64_t out_stride, void* part_o,
                         void* part_ml, int B, int nh, int nkv, int D, int block_size, int nsplit, int part_size,
-                        float scale, hipStream_t st) {
+                        float scale, hipStream_t st, bool kv8) {
   attn_decode_dispatch(q, q_stride, const_cast<void*>(kc), const_cast<void*>(vc), block_tables, bt_stride, ctx_lens,
                        out, out_stride, part_o, part_ml, B, nh, nkv, D, block_size, nsplit, part_size, scale, st,
-                       nullptr);
+                       nullptr, kv8);
 }
 
 // decode attention with the rope + KV-cache write of the new token fused in (q = the QKV GEMM output

@@ -21,9 +21,11 @@
 
 constexpr float kLog2eX = 1.4426950408889634f;
 
-template <int D>
+// KV8: fp8 cache rows (D e4m3 bytes + fp32 scale at byte D; reference.py kv_rows_quant), dequantised to
+// bf16 while the tile is staged into LDS.
+template <int D, bool KV8>
 __global__ __launch_bounds__(256) void attn_extend_kernel(
-    const bf16_t* __restrict__ q, int64_t q_stride, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+    const bf16_t* __restrict__ q, int64_t q_stride, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
     bf16_t* __restrict__ out, int64_t out_stride, int nh, int nkv, int GE, int bs, float scale_log2) {
   constexpr int BKV = 64;
@@ -66,7 +68,12 @@ __global__ __launch_bounds__(256) void attn_extend_kernel(
   const int wave_qhi = p0 + min(qlen - 1, r0 + (16 * w + 15) / GE);
   const int* bt = block_tables + (int64_t)b * max_blocks;
   constexpr int CH = D / 8;
-  const int64_t head_stride = (int64_t)bs * D;  // one kv head of one block
+  constexpr int RB = KV8 ? D + 16 : D;         // cache row (elements of the cache dtype)
+  const int64_t head_stride = (int64_t)bs * RB;  // one kv head of one block
+  const bf16_t* __restrict__ kc = (const bf16_t*)kcv;
+  const bf16_t* __restrict__ vc = (const bf16_t*)vcv;
+  const unsigned char* __restrict__ kc8 = (const unsigned char*)kcv;
+  const unsigned char* __restrict__ vc8 = (const unsigned char*)vcv;
   for (int kv0 = 0; kv0 < kv_end; kv0 += BKV) {
     __syncthreads();
 #pragma unroll
@@ -74,9 +81,28 @@ __global__ __launch_bounds__(256) void attn_extend_kernel(
       const int r = c / CH, ch = c % CH;
       const int key = min(kv0 + r, kv_end - 1);
       const int blk = bt[key / bs];
-      const int64_t off = ((int64_t)blk * nkv + kvh) * head_stride + (int64_t)(key % bs) * D + ch * 8;
-      *reinterpret_cast<u16x8*>(&Ks[r * LD + ch * 8]) = *reinterpret_cast<const u16x8*>(kc + off);
-      *reinterpret_cast<u16x8*>(&Vs[r * LD + ch * 8]) = *reinterpret_cast<const u16x8*>(vc + off);
+      const int64_t rowoff = ((int64_t)blk * nkv + kvh) * head_stride + (int64_t)(key % bs) * RB;
+      if constexpr (KV8) {
+        const u32x2 k8 = *reinterpret_cast<const u32x2*>(kc8 + rowoff + ch * 8);
+        const u32x2 v8 = *reinterpret_cast<const u32x2*>(vc8 + rowoff + ch * 8);
+        const float ks = *reinterpret_cast<const float*>(kc8 + rowoff + D);
+        const float vs = *reinterpret_cast<const float*>(vc8 + rowoff + D);
+        u16x8 kb, vb;
+#pragma unroll
+        for (int hw = 0; hw < 2; ++hw) {
+          const f32x2 a = __builtin_amdgcn_cvt_pk_f32_fp8(k8[hw], false), c = __builtin_amdgcn_cvt_pk_f32_fp8(k8[hw], true);
+          const f32x2 x = __builtin_amdgcn_cvt_pk_f32_fp8(v8[hw], false), y = __builtin_amdgcn_cvt_pk_f32_fp8(v8[hw], true);
+          kb[4 * hw] = f2bf(a[0] * ks); kb[4 * hw + 1] = f2bf(a[1] * ks);
+          kb[4 * hw + 2] = f2bf(c[0] * ks); kb[4 * hw + 3] = f2bf(c[1] * ks);
+          vb[4 * hw] = f2bf(x[0] * vs); vb[4 * hw + 1] = f2bf(x[1] * vs);
+          vb[4 * hw + 2] = f2bf(y[0] * vs); vb[4 * hw + 3] = f2bf(y[1] * vs);
+        }
+        *reinterpret_cast<u16x8*>(&Ks[r * LD + ch * 8]) = kb;
+        *reinterpret_cast<u16x8*>(&Vs[r * LD + ch * 8]) = vb;
+      } else {
+        *reinterpret_cast<u16x8*>(&Ks[r * LD + ch * 8]) = *reinterpret_cast<const u16x8*>(kc + rowoff + ch * 8);
+        *reinterpret_cast<u16x8*>(&Vs[r * LD + ch * 8]) = *reinterpret_cast<const u16x8*>(vc + rowoff + ch * 8);
+      }
     }
     __syncthreads();
     if (kv0 > wave_qhi) continue;  // whole tile in this wave's causal future (barriers stay uniform)
@@ -160,23 +186,29 @@ static int extend_group(int G) {
 void launch_attn_extend(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
                         const void* block_tables, int max_blocks, const void* cu_q, const void* ctx_lens, void* out,
                         int64_t out_stride, int B, int max_qlen, int nh, int nkv, int D, int bs, float scale,
-                        hipStream_t st) {
+                        hipStream_t st, bool kv8) {
   if (nh % nkv) throw std::runtime_error("attn_extend: nh must be a multiple of nkv");
   if (B == 0 || max_qlen == 0) return;
   const int G = nh / nkv, GE = extend_group(G);
   const int rows = 64 / GE;
   dim3 grid((max_qlen + rows - 1) / rows, nkv * (G / GE), B);
   auto Q = (const bf16_t*)q;
-  auto K = (const bf16_t*)k_cache;
-  auto V = (const bf16_t*)v_cache;
+  auto K = k_cache;
+  auto V = v_cache;
   auto BT = (const int*)block_tables;
   auto CU = (const int*)cu_q;
   auto CL = (const int*)ctx_lens;
   auto O = (bf16_t*)out;
   const float sl = scale * kLog2eX;
 #define LX(D_)                                                                                                   \
-  attn_extend_kernel<D_><<<grid, 256, 0, st>>>(Q, q_stride, K, V, BT, max_blocks, CU, CL, O, out_stride, nh, nkv, GE, \
-                                               bs, sl)
+  do {                                                                                                           \
+    if (kv8)                                                                                                     \
+      attn_extend_kernel<D_, true><<<grid, 256, 0, st>>>(Q, q_stride, K, V, BT, max_blocks, CU, CL, O, out_stride, nh, \
+                                                         nkv, GE, bs, sl);                                       \
+    else                                                                                                         \
+      attn_extend_kernel<D_, false><<<grid, 256, 0, st>>>(Q, q_stride, K, V, BT, max_blocks, CU, CL, O, out_stride,   \
+                                                          nh, nkv, GE, bs, sl);                                  \
+  } while (0)
   switch (D) {
     case 64: LX(64); break;
     case 128: LX(128); break;

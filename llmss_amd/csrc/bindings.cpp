@@ -17,11 +17,11 @@ void launch_embed(const void* ids, const void* pos, const void* wte, const void*
 void launch_rope_cache(void* qkv, int64_t row_stride, const void* pos, const void* cos_t, const void* sin_t, void* kc,
                        void* vc, const void* slot, int T, int nh, int nkv, int D, int rot, int block_size, int k_off,
                        int v_off, int style, bool do_rope, const void* part, int S, int64_t slab, const void* bias,
-                       hipStream_t st);
+                       hipStream_t st, bool kv8);
 void launch_attn_decode(const void* q, int64_t q_stride, const void* kc, const void* vc, const void* block_tables,
                         int bt_stride, const void* ctx_lens, void* out, int64_t out_stride, void* part_o,
                         void* part_ml, int B, int nh, int nkv, int D, int block_size, int nsplit, int part_size,
-                        float scale, hipStream_t st);
+                        float scale, hipStream_t st, bool kv8);
 void launch_attn_prefill(const void* qkv, int64_t row_stride, int T, const void* cu_seqlens, void* out,
                          int64_t out_stride, int B, int max_seqlen, int nh, int nkv, int D, int k_off, int v_off,
                          float scale, hipStream_t st);
@@ -36,7 +36,7 @@ void launch_ce_loss(const void* logits, int64_t ld, bool fp32, const void* label
 void launch_attn_extend(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
                         const void* block_tables, int max_blocks, const void* cu_q, const void* ctx_lens, void* out,
                         int64_t out_stride, int B, int max_qlen, int nh, int nkv, int D, int bs, float scale,
-                        hipStream_t st);
+                        hipStream_t st, bool kv8);
 void launch_attn_decode_fused(const void* qkv, int64_t q_stride, const void* part, int S, int64_t slab,
                               const void* bias, int N, const void* pos, const void* cos_t, const void* sin_t,
                               const void* slots, int rot, int style, int k_off, int v_off, void* kc, void* vc,
@@ -86,15 +86,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("rope_cache", [](uintptr_t qkv, int64_t rs, uintptr_t pos, uintptr_t cos_t, uintptr_t sin_t, uintptr_t kc,
                          uintptr_t vc, uintptr_t slot, int T, int nh, int nkv, int D, int rot, int bs, int k_off,
                          int v_off, int style, bool do_rope, uintptr_t part, int nslab, int64_t slab, uintptr_t bias,
-                         uintptr_t st) {
+                         uintptr_t st, bool kv8) {
     launch_rope_cache(P(qkv), rs, CP(pos), CP(cos_t), CP(sin_t), P(kc), P(vc), CP(slot), T, nh, nkv, D, rot, bs, k_off,
-                      v_off, style, do_rope, CP(part), nslab, slab, CP(bias), S(st));
+                      v_off, style, do_rope, CP(part), nslab, slab, CP(bias), S(st), kv8);
   });
   m.def("attn_decode", [](uintptr_t q, int64_t qs, uintptr_t kc, uintptr_t vc, uintptr_t bt, int bts, uintptr_t cl,
                           uintptr_t out, int64_t os, uintptr_t po, uintptr_t pml, int B, int nh, int nkv, int D, int bs,
-                          int nsplit, int psize, float scale, uintptr_t st) {
+                          int nsplit, int psize, float scale, uintptr_t st, bool kv8) {
     launch_attn_decode(CP(q), qs, CP(kc), CP(vc), CP(bt), bts, CP(cl), P(out), os, P(po), P(pml), B, nh, nkv, D, bs,
-                       nsplit, psize, scale, S(st));
+                       nsplit, psize, scale, S(st), kv8);
   });
   m.def("attn_decode_fused", [](uintptr_t qkv, int64_t qs, uintptr_t part, int S, int64_t slab, uintptr_t bias, int N,
                                 uintptr_t pos, uintptr_t cos_t, uintptr_t sin_t, uintptr_t slots, int rot, int style,
@@ -124,9 +124,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("attn_extend", [](uintptr_t q, int64_t qs, uintptr_t kc, uintptr_t vc, uintptr_t bt, int maxb, uintptr_t cu,
                           uintptr_t cl, uintptr_t out, int64_t os, int B, int maxq, int nh, int nkv, int D, int bs,
-                          float scale, uintptr_t st) {
+                          float scale, uintptr_t st, bool kv8) {
     launch_attn_extend(CP(q), qs, CP(kc), CP(vc), CP(bt), maxb, CP(cu), CP(cl), P(out), os, B, maxq, nh, nkv, D, bs,
-                       scale, S(st));
+                       scale, S(st), kv8);
   });
   m.def("gemm", [](uintptr_t x, int64_t ldx, uintptr_t w, int64_t ldw, bool fp8, uintptr_t ws, uintptr_t bias,
                    uintptr_t y, int64_t ldy, int M, int N, int K, int act, bool glu, uintptr_t work, int64_t wbytes,

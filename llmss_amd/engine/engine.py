@@ -136,8 +136,13 @@ class LLMEngine:
                  block_size: int = 16, num_blocks: Optional[int] = None, max_model_len: Optional[int] = None,
                  kv_fraction: float = 0.9, use_graphs: Optional[bool] = None, eos_token_id: Optional[int] = None,
                  graph_buckets: Optional[Sequence[int]] = None, check_tokens: Optional[bool] = None,
-                 autotune: Optional[bool] = None, prefill_chunk: Optional[int] = None):
+                 autotune: Optional[bool] = None, prefill_chunk: Optional[int] = None,
+                 kv_dtype: Optional[str] = None):
         self.model = model
+        if kv_dtype is not None:  # "bf16" (model dtype) or "fp8" (e4m3 rows + per-row scale)
+            if kv_dtype not in ("bf16", "fp8"):
+                raise ValueError(f"kv_dtype must be 'bf16' or 'fp8', not {kv_dtype!r}")
+            model.kv_fp8 = kv_dtype == "fp8"
         self.cfg = model.cfg
         self.tp = model.tp
         self.device = model.device
@@ -221,7 +226,7 @@ class LLMEngine:
                 "max_num_seqs": self.max_num_seqs, "max_batched_tokens": self.max_batched_tokens,
                 "buckets": list(self.buckets), "graphs": bool(self.use_graphs),
                 "async_decode": self.async_decode, "eos": self.eos, "prefill_chunk": self.prefill_chunk,
-                "dist_sampling": self.dist_sampling,
+                "dist_sampling": self.dist_sampling, "kv_fp8": bool(self.model.kv_fp8),
                 "overlap_rows": self.model.overlap_rows, "bucket_bytes": self.model.bucket_bytes,
                 "tbo_min": self.model.tbo_min,
                 "fp8": any(L.qkv.w_scale is not None for L in self.model.w.layers[:1])}

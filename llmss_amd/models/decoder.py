@@ -85,6 +85,8 @@ class DecoderLM:
         # fused RoPE+KV-write+attention decode: correct, but measured slower (its prologue halves the
         # attention kernel's occupancy), so opt-in
         self.fused_decode = os.environ.get("LLMSS_FUSED_DECODE", "0") == "1"
+        # fp8 (e4m3 + per-row scale) paged KV cache (LLMSS_KV_DTYPE=fp8 or LLMEngine(kv_dtype="fp8"))
+        self.kv_fp8 = os.environ.get("LLMSS_KV_DTYPE", "bf16") == "fp8"
         # decode steps of at least this many sequences run as two interleaved micro-batches so each
         # one's all-reduces overlap the other's compute; only when collectives cost time. Opt-in
         # (0 = off): measured on MI355X (bench/tbo_probe.py, Llama-2-7B TP=8 shard, batch 512, 8
@@ -104,22 +106,27 @@ class DecoderLM:
 
     # --------------------------------------------------------------------------------- KV
     def kv_cache_shape(self, num_blocks: int, block_size: int):
-        return (num_blocks, self.plan.nkv_l, block_size, self.cfg.head_dim)
+        # fp8 KV (kv_fp8): each (token, kv head) row = head_dim e4m3 bytes + a 16-B tail with its fp32
+        # scale (ops/reference.py kv_rows_quant); decode attention then streams 0.56x the bytes
+        row = self.cfg.head_dim + ops.ref.KV8_TAIL if self.kv_fp8 else self.cfg.head_dim
+        return (num_blocks, self.plan.nkv_l, block_size, row)
 
     def kv_bytes_per_block(self, block_size: int) -> int:
-        return 2 * self.cfg.num_layers * self.plan.nkv_l * block_size * self.cfg.head_dim * 2
+        row = self.cfg.head_dim + ops.ref.KV8_TAIL if self.kv_fp8 else self.cfg.head_dim * 2
+        return 2 * self.cfg.num_layers * self.plan.nkv_l * block_size * row
 
     def allocate_kv_cache(self, num_blocks: int, block_size: int):
         shp = self.kv_cache_shape(num_blocks, block_size)
-        return [(torch.zeros(shp, dtype=self.dtype, device=self.device),
-                 torch.zeros(shp, dtype=self.dtype, device=self.device)) for _ in range(self.cfg.num_layers)]
+        dt = torch.uint8 if self.kv_fp8 else self.dtype
+        return [(torch.zeros(shp, dtype=dt, device=self.device),
+                 torch.zeros(shp, dtype=dt, device=self.device)) for _ in range(self.cfg.num_layers)]
 
     # ---------------------------------------------------------------------------- forward
     def _attention(self, qkv, inp: StepInput, kc, vc):
         cfg, p = self.cfg, self.plan
         D = cfg.head_dim
         do_rope = cfg.position == "rope"
-        if inp.kind == "decode" and qkv.is_cuda and self.fused_decode and \
+        if inp.kind == "decode" and qkv.is_cuda and self.fused_decode and not self.kv_fp8 and \
                 _hip_ops().fused_decode_ok(D, cfg.rotary_dim, cfg.rope_style, do_rope):
             # one launch: RoPE + paged KV write of the new token + attention (no rope_cache kernel)
             return _hip_ops().attn_decode_fused(

@@ -118,10 +118,9 @@ def rope_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, ro
     if do_rope and rot > 0:
         _check(cos.dtype == torch.float32 and cos.is_contiguous() and cos.shape[1] == rot // 2, "cos table")
         _check(sin.shape == cos.shape and sin.is_contiguous(), "sin table")
+    kv8 = k_cache is not None and k_cache.dtype == torch.uint8
     if k_cache is not None:
-        _check(k_cache.dtype == torch.bfloat16 and k_cache.is_contiguous() and k_cache.dim() == 4, "k_cache")
-        _check(k_cache.shape[1] == nkv and k_cache.shape[3] == D, "k_cache shape [nb, nkv, bs, D]")
-        _check(v_cache.shape == k_cache.shape and v_cache.is_contiguous(), "v_cache")
+        _kv_cache_check(k_cache, v_cache, nkv, D)
         _check(slots is not None and slots.dtype == torch.int64 and slots.numel() == T, "slots")
         bs = k_cache.shape[2]
     else:
@@ -131,8 +130,21 @@ def rope_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, ro
                      _ptr(slots) if k_cache is not None else 0, T, nh, nkv, D, rot,
                      bs, nh * D, (nh + nkv) * D, 1 if style == "gptj" else 0, bool(do_rope and rot > 0),
                      part.buf.data_ptr() if part else 0, part.S if part else 0, part.M * part.N if part else 0,
-                     _ptr(part.bias) if part else 0, _stream())
+                     _ptr(part.bias) if part else 0, _stream(), kv8)
     return qkv
+
+
+def _kv_cache_check(k_cache, v_cache, nkv, D):
+    """bf16 [nb, nkv, bs, D] caches, or fp8 rows [nb, nkv, bs, D + 16] uint8 (ops/reference.py kv_rows_quant)."""
+    kv8 = k_cache.dtype == torch.uint8
+    _check(k_cache.is_cuda and k_cache.dtype in (torch.bfloat16, torch.uint8) and k_cache.is_contiguous()
+           and k_cache.dim() == 4, "k_cache bf16 / uint8 (fp8 rows) [nb, nkv, bs, row]")
+    _check(k_cache.shape[1] == nkv and k_cache.shape[3] == (D + _ref.KV8_TAIL if kv8 else D),
+           f"k_cache shape [nb, nkv, bs, {'D + 16' if kv8 else 'D'}]")
+    _check(v_cache.shape == k_cache.shape and v_cache.dtype == k_cache.dtype and v_cache.is_contiguous(), "v_cache")
+    if kv8:
+        _check(D % 16 == 0 and 256 % (D // 8) == 0, "fp8 KV cache needs head_dim 64/128/256")
+    return kv8
 
 
 # -------------------------------------------------------------------------------- attention
@@ -159,9 +171,7 @@ def attn_extend(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_qlen, nh,
     _bf16_rows(q, "q")
     _check(q.shape[1] >= nh * D, "q too narrow")
     _check(D in (64, 128, 256), "extend attention supports head_dim 64/128/256")
-    _check(k_cache.dtype == torch.bfloat16 and k_cache.is_contiguous() and k_cache.dim() == 4, "k_cache")
-    _check(k_cache.shape[1] == nkv and k_cache.shape[3] == D, "k_cache shape [nb, nkv, bs, D]")
-    _check(v_cache.shape == k_cache.shape and v_cache.is_contiguous(), "v_cache")
+    kv8 = _kv_cache_check(k_cache, v_cache, nkv, D)
     _check(nh % nkv == 0, "nh % nkv")
     B = cu_q.numel() - 1
     for t, nm in ((cu_q, "cu_q"), (ctx_lens, "ctx_lens"), (block_tables, "block_tables")):
@@ -174,7 +184,7 @@ def attn_extend(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_qlen, nh,
     _check(y.shape[0] >= T and y.shape[1] >= nh * D, "out shape")
     lib().attn_extend(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
                       block_tables.shape[1], cu_q.data_ptr(), ctx_lens.data_ptr(), y.data_ptr(), y.stride(0), B,
-                      int(max_qlen), nh, nkv, D, bs, float(scale), _stream())
+                      int(max_qlen), nh, nkv, D, bs, float(scale), _stream(), kv8)
     return y
 
 
@@ -238,9 +248,7 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale, 
     _check(q.is_cuda and q.dtype == torch.bfloat16 and q.stride(-1) == 1 and q.dim() == 2, "q [B, >=nh*D]")
     _check(q.shape[1] >= nh * D, "q too narrow")
     _check(D in (64, 128, 256), "decode attention supports head_dim 64/128/256")
-    _check(k_cache.dtype == torch.bfloat16 and k_cache.is_contiguous() and k_cache.shape[1] == nkv
-           and k_cache.shape[3] == D, "k_cache [nb, nkv, bs, D]")
-    _check(v_cache.shape == k_cache.shape and v_cache.is_contiguous(), "v_cache")
+    kv8 = _kv_cache_check(k_cache, v_cache, nkv, D)
     _check(block_tables.dtype == torch.int32 and block_tables.dim() == 2 and block_tables.shape[0] >= B
            and block_tables.stride(1) == 1, "block_tables int32 [B, maxb]")
     _check(ctx_lens.dtype == torch.int32 and ctx_lens.numel() >= B and ctx_lens.is_contiguous(), "ctx_lens int32")
@@ -252,7 +260,7 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale, 
     po, pml = _DECODE_WS.get(B, nh, nsplit, D, q.device) if nsplit > 1 else (None, None)
     lib().attn_decode(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
                       block_tables.stride(0), ctx_lens.data_ptr(), y.data_ptr(), y.stride(0), _ptr(po), _ptr(pml),
-                      B, nh, nkv, D, bs, nsplit, psize, float(scale), _stream())
+                      B, nh, nkv, D, bs, nsplit, psize, float(scale), _stream(), kv8)
     return y
 
 

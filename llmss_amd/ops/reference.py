@@ -82,6 +82,32 @@ def apply_rope(x: torch.Tensor, positions: torch.Tensor, cos: torch.Tensor, sin:
     return out.to(x.dtype)
 
 
+# fp8 KV cache rows: one (token, kv head) row = D e4m3 bytes + a 16-byte tail holding the row's fp32
+# scale (bytes D..D+3; D+4..D+15 zero): scale = absmax / 448, value = e4m3 * scale. 16-B aligned rows,
+# 0.56x the bytes of a bf16 row at D = 128.
+KV8_TAIL = 16
+
+
+def kv_rows_quant(x: torch.Tensor) -> torch.Tensor:
+    """[..., D] float -> [..., D + 16] uint8 fp8 cache rows (csrc kernels: same arithmetic)."""
+    xf = x.float()
+    D = xf.shape[-1]
+    amax = xf.abs().amax(-1, keepdim=True)
+    sc = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    q = (xf * (1.0 / sc)).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).view(torch.uint8)
+    rows = torch.zeros(*xf.shape[:-1], D + KV8_TAIL, dtype=torch.uint8, device=x.device)
+    rows[..., :D] = q
+    rows[..., D:D + 4] = sc.contiguous().view(torch.uint8)
+    return rows
+
+
+def kv_rows_dequant(rows: torch.Tensor, D: int) -> torch.Tensor:
+    """[..., D + 16] uint8 fp8 cache rows -> [..., D] fp32."""
+    q = rows[..., :D].contiguous().view(torch.float8_e4m3fn).float()
+    sc = rows[..., D:D + 4].contiguous().view(torch.float32)
+    return q * sc
+
+
 def rope_cache(qkv: torch.Tensor, positions, cos, sin, k_cache, v_cache, slots, nh: int, nkv: int, D: int,
                rot: int, style: str, do_rope: bool = True) -> None:
     """In place: rotate q and k inside qkv; write rotated k and v to the paged cache at slots."""
@@ -97,9 +123,13 @@ def rope_cache(qkv: torch.Tensor, positions, cos, sin, k_cache, v_cache, slots, 
         valid = slots >= 0
         sl = slots[valid]
         blk, off = sl // bs, sl % bs
-        # cache [num_blocks, nkv, bs, D]
-        k_cache[blk, :, off, :] = k[valid].to(k_cache.dtype)
-        v_cache[blk, :, off, :] = v[valid].to(v_cache.dtype)
+        # cache [num_blocks, nkv, bs, D] (or fp8 rows [.., D + 16] uint8)
+        if k_cache.dtype == torch.uint8:
+            k_cache[blk, :, off, :] = kv_rows_quant(k[valid])
+            v_cache[blk, :, off, :] = kv_rows_quant(v[valid])
+        else:
+            k_cache[blk, :, off, :] = k[valid].to(k_cache.dtype)
+            v_cache[blk, :, off, :] = v[valid].to(v_cache.dtype)
 
 
 def attn_prefill(qkv: torch.Tensor, cu_seqlens, nh: int, nkv: int, D: int, scale: float) -> torch.Tensor:
@@ -127,11 +157,13 @@ def attn_prefill(qkv: torch.Tensor, cu_seqlens, nh: int, nkv: int, D: int, scale
 
 
 def gather_kv(cache: torch.Tensor, block_table_row: torch.Tensor, ctx: int) -> torch.Tensor:
-    """Paged cache [nb, nkv, bs, D] -> contiguous [nkv, ctx, D] for one sequence."""
+    """Paged cache [nb, nkv, bs, D] -> contiguous [nkv, ctx, D] for one sequence (fp8 rows dequantised
+    to fp32)."""
     bs = cache.shape[2]
     nblk = (ctx + bs - 1) // bs
     blocks = cache[block_table_row[:nblk].long()]  # [nblk, nkv, bs, D]
-    return blocks.permute(1, 0, 2, 3).reshape(cache.shape[1], nblk * bs, cache.shape[3])[:, :ctx]
+    out = blocks.permute(1, 0, 2, 3).reshape(cache.shape[1], nblk * bs, cache.shape[3])[:, :ctx]
+    return kv_rows_dequant(out, cache.shape[3] - KV8_TAIL) if cache.dtype == torch.uint8 else out
 
 
 def attn_decode(q: torch.Tensor, k_cache, v_cache, block_tables, ctx_lens, nh: int, nkv: int, D: int,
