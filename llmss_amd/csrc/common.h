@@ -230,7 +230,72 @@ __device__ __forceinline__ void tile_store_lds(const f32x4 (&acc)[MT][NT], char*
   }
 }
 
-#define HIP_CHECK_LAUNCH()                                                               \
+// In-launch split-K combine (guide "Projection GEMM at M = 256" item 2, write-through form; the
+// hand-off is row 1 of MI355X_MICROARCH "Valid forms"): every K-slice workgroup of a tile stores
+// its accumulators write-through (sc1, aux 16) into its slab of the tile's workspace region, EVERY
+// wave drains its stores, then one lane takes a ticket on the tile's counter (relaxed agent atomic).
+// The workgroup that draws ticket S-1 reads all S slabs back with sc1 loads (every load of the
+// handed-off bytes is sc1, so no acquire fence), summing in slice order 0..S-1 - bit-identical to
+// the separate splitk_reduce kernel whatever the arrival order - and finishes the tile; it also
+// resets the counter for the next launch (counters start zeroed). Returns true in that workgroup.
+// Slab layout: per wave, per (mt, nt) accumulator tile, 64 lanes x 16 B = one 1-KiB row, so each
+// store / load wave-instruction moves a whole contiguous KiB. The slabs are read G at a time (all
+// loads of a group issued before any add) so the reducer pays ceil(S / G) round trips, not S, and
+// no load sits behind a per-element condition (a select after the load instead).
+template <int MT, int NT>
+__device__ __forceinline__ bool splitk_combine(f32x4 (&acc)[MT][NT], float* ws, int* cnt, int tile, int S, int z,
+                                               int wid, int nwaves, int lane, int* lds_word) {
+  constexpr int G = MT * NT * 4 <= 32 ? 4 : (MT * NT * 4 <= 64 ? 2 : 1);
+  const int tile_f = nwaves * MT * NT * 256;  // floats per slab
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(ws + (int64_t)tile * S * tile_f, (short)0,
+                                                    (int)((uint32_t)S * (uint32_t)tile_f * 4u), 0x00020000);
+  const uint32_t base = (uint32_t)((wid * MT * NT * 64 + lane) * 16);
+  const uint32_t slab_b = (uint32_t)tile_f * 4u;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mt][nt]), rs,
+                                             base + (uint32_t)((mt * NT + nt) * 1024), (uint32_t)z * slab_b, 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains before the ticket
+  __syncthreads();
+  if (threadIdx.x == 0) *lds_word = __hip_atomic_fetch_add(cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (*lds_word != S - 1) return false;
+  if (threadIdx.x == 0) __hip_atomic_store(cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s0 = 0; s0 < S; s0 += G) {
+    u32x4 v[G][MT][NT];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const uint32_t so = (uint32_t)min(s0 + j, S - 1) * slab_b;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          v[j][mt][nt] = __builtin_amdgcn_raw_buffer_load_b128(rs, base + (uint32_t)((mt * NT + nt) * 1024), so, 16);
+    }
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const bool use = s0 + j < S;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const f32x4 p = __builtin_bit_cast(f32x4, v[j][mt][nt]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[mt][nt][i] += use ? p[i] : 0.f;
+        }
+    }
+  }
+  return true;
+}
+
+#define HIP_CHECK_LAUNCH()                                                            \
   do {                                                                                   \
     hipError_t e__ = hipGetLastError();                                                  \
     if (e__ != hipSuccess) throw std::runtime_error(std::string("HIP launch failed: ") + \

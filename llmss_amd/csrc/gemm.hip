@@ -549,7 +549,8 @@ __global__ __launch_bounds__(64 * NW) void gemm_tiled_kernel(const bf16_t* __res
                                                          const void* __restrict__ B, int64_t ldb,
                                                          const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
                                                          int64_t ldy, float* __restrict__ part, int M, int N, int K,
-                                                         int act, int glu, const float* __restrict__ wscale) {
+                                                         int act, int glu, const float* __restrict__ wscale,
+                                                         int* __restrict__ cnt) {
   constexpr int MTW = BM / (8 * NW), NTW = BN / 32;  // 16x16 tiles per wave (waves NW/2 x 2)
   constexpr int A_BYTES = BM * TBK * 2, B_BYTES = TiledB<BN, F8, NW>::BYTES, STAGE = A_BYTES + B_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
@@ -610,6 +611,15 @@ __global__ __launch_bounds__(64 * NW) void gemm_tiled_kernel(const bf16_t* __res
       else tiled_compute<MTW, NTW, false, F8>(cA, cA + A_BYTES, acc, wr, wc, li, g, t * TBK, K);
       cur = cur == NS - 1 ? 0 : cur + 1;
     }
+  }
+  // cnt: split-K slices combine in this launch (common.h splitk_combine); the last arriver of the
+  // tile finishes it with the normal bf16 epilogue, the others are done
+  if (cnt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!splitk_combine<MTW, NTW>(acc, part, cnt, (n0 / BN) * ntm + m0 / BM, gridDim.y, zk, w, NW, lane,
+                                  reinterpret_cast<int*>(smem)))
+      return;
+    part = nullptr;
   }
   // epilogue (C layout: col = lane&15 -> n, row = 4*(lane>>4)+i -> m)
   const int wn0 = n0 + wc * (NTW * 16);
@@ -1408,7 +1418,7 @@ static int tiles_of(int M, int N, int bm, int bn) { return ((M + bm - 1) / bm) *
 bool gemm_mid_dims(int tsel, int* bm, int* bn, int* threads);
 void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
-                     int split, hipStream_t st, bool packed = false);
+                     int split, hipStream_t st, bool packed = false, int* cnt = nullptr);
 
 // tsel 8-12: gemm_mid (gemm_mid.hip: buffer-descriptor staging, 128x128 / 256x128 / 64x256 / 64x128 / 128x256)
 static int tile_dims(int tsel, int* bm, int* bn) {
@@ -1468,22 +1478,27 @@ static bool wnt_ok(int tsel_raw, int M, int tsel) {
   return !(tsel_raw & 64) && M <= bm;
 }
 
-// per-tile arrival counters of the stream-K combine: zeroed once, reset by every last arriver
-static int* g_sk_counters = nullptr;
-static int g_sk_capacity = 0;
+// per-tile arrival counters of the stream-K and split-K combines, one buffer per device: zeroed
+// once, reset by every last arriver (consecutive GEMMs on one stream never overlap)
+static std::mutex g_sk_mu;
+static int* g_sk_counters[64] = {};
+static int g_sk_capacity[64] = {};
 
 static int* sk_counters(int n) {
-  if (n <= g_sk_capacity) return g_sk_counters;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) throw std::runtime_error("gemm counters: bad device");
+  std::lock_guard<std::mutex> lk(g_sk_mu);
+  if (n <= g_sk_capacity[dev]) return g_sk_counters[dev];
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   (void)hipStreamIsCapturing(nullptr, &cs);
-  if (cs != hipStreamCaptureStatusNone) throw std::runtime_error("stream-K counters must be allocated before capture");
+  if (cs != hipStreamCaptureStatusNone) throw std::runtime_error("gemm counters must be allocated before capture");
   int cap = std::max(n, 1 << 16);
   int* p = nullptr;
-  if (hipMalloc(&p, (size_t)cap * sizeof(int)) != hipSuccess) throw std::runtime_error("stream-K counters: hipMalloc");
-  if (hipMemset(p, 0, (size_t)cap * sizeof(int)) != hipSuccess) throw std::runtime_error("stream-K counters: memset");
+  if (hipMalloc(&p, (size_t)cap * sizeof(int)) != hipSuccess) throw std::runtime_error("gemm counters: hipMalloc");
+  if (hipMemset(p, 0, (size_t)cap * sizeof(int)) != hipSuccess) throw std::runtime_error("gemm counters: memset");
   (void)hipDeviceSynchronize();
-  g_sk_counters = p;  // the old (smaller) buffer is left to the process: launches may still reference it
-  g_sk_capacity = cap;
+  g_sk_counters[dev] = p;  // the old (smaller) buffer is left to the process: launches may still reference it
+  g_sk_capacity[dev] = cap;
   return p;
 }
 
@@ -1556,13 +1571,18 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   int bm, bn;
   tile_dims(tsel, &bm, &bn);
   const int nt = tiles_of(M, N, bm, bn);
-  if ((int64_t)s * M * N * 4 > ws_bytes) s = 1;
+  // hint bit 8: split-K slices combine in-launch (last arriver per tile, common.h splitk_combine):
+  // slabs [tile][S][bm*bn] in the workspace, finished bf16 output, no reduce launch
+  int* cnt = nullptr;
+  if ((tsel_raw & 256) && s > 1 && (int64_t)nt * s * bm * bn * 4 <= ws_bytes && Y) cnt = sk_counters(nt);
+  if (!cnt && (int64_t)s * M * N * 4 > ws_bytes) s = 1;
   float* part = s > 1 ? (float*)workspace : nullptr;
-  const int act_k = s > 1 ? 0 : act, glu_k = s > 1 ? 0 : g;
+  const int act_k = s > 1 && !cnt ? 0 : act, glu_k = s > 1 && !cnt ? 0 : g;
   dim3 grid(nt, s);
   if (tsel >= 8 && tsel <= 12) {
     launch_gemm_mid(tsel, ns, wnt_ok(tsel_raw, M, tsel), X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, part, M, N, K,
-                    act_k, glu_k, s, st);
+                    act_k, glu_k, s, st, false, cnt);
+    if (cnt) return 0;
     if (s > 1 && partial_out && !g && act == 0) return s;
     if (s > 1) {
       const int nout = g ? N / 2 : N;
@@ -1579,10 +1599,10 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   do {                                                                                                             \
     if (wnt)                                                                                                       \
       gemm_tiled_kernel<BM_, BN_, NS_, true, false, 8><<<grid, 512, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N, K, \
-                                                                             act_k, glu_k, nullptr);               \
+                                                                             act_k, glu_k, nullptr, cnt);          \
     else                                                                                                           \
       gemm_tiled_kernel<BM_, BN_, NS_, false, false, 8><<<grid, 512, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N,  \
-                                                                              K, act_k, glu_k, nullptr);           \
+                                                                              K, act_k, glu_k, nullptr, cnt);      \
   } while (0)
     if (tsel == 5) {
       if (ns == 3) LT8(256, 128, 3); else LT8(256, 128, 2);
@@ -1593,7 +1613,7 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   } else {
 #define LT1(BM_, BN_, NS_, WNT_, F8_)                                                                              \
   gemm_tiled_kernel<BM_, BN_, NS_, WNT_, F8_><<<grid, 256, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N, K, act_k,  \
-                                                                    glu_k, wscale)
+                                                                    glu_k, wscale, cnt)
 #define LT(BM_, BN_, NS_)                                                                                          \
   do {                                                                                                             \
     if (f8) {                                                                                                      \
@@ -1615,6 +1635,7 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
 #undef LT
 #undef LT1
   HIP_CHECK_LAUNCH();
+  if (cnt) return 0;
   if (s > 1 && partial_out && !g && act == 0) return s;
   if (s > 1) {
     const int nout = g ? N / 2 : N;
@@ -1644,6 +1665,13 @@ int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int n
     int tsel = tiled_hint;
     if ((tsel & 128) && !w_fp8 && (tsel & 15) < 5) return 0;  // stream-K combines in-kernel
     if (w_fp8 && ((tsel & 15) == 4 || (tsel & 15) >= 5)) tsel = (tsel & ~15) | 1;
+    if ((tsel & 256) && (tsel & 15) != 4) {  // split-K combined in-launch
+      int s2 = split_hint, t2 = tsel;
+      gemm_tiled_plan(M, N, K, &t2, &s2, false);
+      int bm, bn;
+      tile_dims(t2 & 15, &bm, &bn);
+      if (s2 > 1 && (int64_t)tiles_of(M, N, bm, bn) * s2 * bm * bn * 4 <= ws_bytes) return 0;
+    }
     s = split_hint;
     gemm_tiled_plan(M, N, K, &tsel, &s, false);
     if ((tsel & 15) == 4 || (tsel & 128)) return 0;
@@ -1654,8 +1682,8 @@ int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int n
 
 void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk) {
   if (gemm_tuned_get(M, N, K, false, w_fp8 ? 1 : 0, nt, splitk)) {
-    if ((*nt >> 8) & 128) {
-      *splitk = 1;  // stream-K finishes its tiles in-kernel: no partial slabs for the consumer
+    if ((*nt >> 8) & (128 | 256)) {
+      *splitk = 1;  // stream-K / split-K combine finish their tiles in-kernel: no partial slabs for the consumer
     } else if (*nt >> 8) {  // tiled hint: the split the kernel will really use
       int tsel = *nt >> 8;
       gemm_tiled_plan(M, N, K, &tsel, splitk, false);

@@ -84,6 +84,16 @@ def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, 
     if M >= 256:
         mids += [(9, 16)]
     out += [((t | d) << 8, s) for t, d in mids for s in (1, 2, 4, 8)]
+    # split-K combined inside the launch (hint bit 256, csrc/common.h splitk_combine): finished bf16
+    # output with no reduce launch - for SwiGLU / activation GEMMs and row-parallel outputs that an
+    # all-reduce needs whole; odd splits too (grid just under a multiple of the CU count)
+    comb = [(3, 16), (2, 16), (11, 16), (10, 16)]
+    if M > 64:
+        comb += [(1, 0), (8, 16), (12, 16)]
+    if M >= 256:
+        comb += [(9, 0)]
+    nk = -(-K // 64)
+    out += [((t | d | 256) << 8, s) for t, d in comb for s in (2, 3, 4, 6, 8) if nk // s >= 2]
     return out
 
 

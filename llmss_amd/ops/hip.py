@@ -338,6 +338,7 @@ _GEMM_WS = GemmWorkspace()
 def reserve_workspace(device, gemm_bytes: int = 64 << 20, decode_rows: int = 0, nh: int = 0, D: int = 128,
                       nsplit: int = 1):
     _GEMM_WS.get(gemm_bytes, device)
+    lib().gemm_reserve_streamk(1 << 16)  # per-tile counters of the in-launch split-K combines
     if decode_rows and nsplit > 1:
         _DECODE_WS.get(decode_rows, nh, nsplit, D, device)
 

@@ -188,6 +188,37 @@ def test_gemm_tiled_variants(tile, stages, split, M, N, K):
           R.linear(x.float(), w.float(), None, glu=True), 2e-2)
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3, 5, 6, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("split", [2, 3, 8])
+@pytest.mark.parametrize("M,N,K", [(64, 1536, 4096), (200, 4800, 1600), (37, 256, 64 * 5 + 16), (512, 2752, 4096)])
+def test_gemm_splitk_combine_in_launch(tile, split, M, N, K):
+    """Hint bit 256: the K slices of a tile combine inside the launch (last arriver per tile sums the
+    write-through slabs in slice order and runs the epilogue). Bit-identical to the same plan with a
+    separate reduce launch; repeated calls check the self-resetting tile counters; NaN-filled outputs
+    and a NaN-poisoned workspace check that every element is written from fresh slabs."""
+    torch.manual_seed(0)
+    x, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
+    b = rnd(N, scale=0.1)
+    d = 16 if tile not in (5, 9) else 0
+    hint, comb = (tile | d) << 8, (tile | d | 256) << 8
+    H._GEMM_WS.get(64 << 20, x.device).fill_(float("nan"))
+    for act, glu, bias in (("gelu_tanh", False, b), ("none", True, None), ("none", False, b)):
+        nout = N // 2 if glu else N
+        ref = H.linear(x, w, bias, act=act, glu=glu, nt_hint=hint, split_hint=split)
+        for _ in range(3):
+            y = torch.full((M, nout), float("nan"), dtype=torch.bfloat16, device=dev)
+            got = H.linear(x, w, bias, act=act, glu=glu, nt_hint=comb, split_hint=split, out=y)
+            if act == "none":  # the same fp32 sums in the same order
+                assert torch.equal(got, ref), (act, glu, (got.float() - ref.float()).abs().max().item())
+            else:  # GELU compiled into two kernels may contract differently: at most 1 bf16 ulp
+                close(got, ref, 0, rtol=1e-2)
+        close(got, R.linear(x.float(), w.float(), None if bias is None else bias.float(), act=act, glu=glu), 2e-2)
+    # a consumer that could take slabs gets the finished output instead
+    p = H.linear(x, w, None, nt_hint=comb, split_hint=split, partial_ok=True)
+    assert not isinstance(p, H.PartialSum)
+    close(p, R.linear(x.float(), w.float(), None), 2e-2)
+
+
 @pytest.mark.parametrize("tile", [0, 8, 9, 10, 11, 12])
 @pytest.mark.parametrize("stages", [2, 4, 6])
 @pytest.mark.parametrize("split", [0, 1, 3])
