@@ -31,6 +31,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="all")
     ap.add_argument("--iters", type=int, default=16)
+    ap.add_argument("--stream", action="store_true", help="also time the weight-streaming kernels (nt + 16 * variant)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     H.reserve_workspace(dev)
@@ -51,16 +52,19 @@ def main():
                 torch.cuda.synchronize()
                 return A._time(f, a.iters)
 
-            res = {"slab": [], "comb": []}
-            for nt, s in A.candidates(M, N, K, glu, False):
+            res = {"slab": [], "comb": [], "stream": []}
+            cands = list(A.candidates(M, N, K, glu, False))
+            if a.stream:
+                cands += [(nt + 16 * v, s) for v in (1, 2) for nt in (1, 2) for s in (1, 2, 4, 8)]
+            for nt, s in cands:
                 try:
                     t = cost(nt, s)
                 except (RuntimeError, ValueError):
                     continue
-                res["comb" if (nt >> 8) & 256 else "slab"].append((t, nt, s))
+                res["stream" if nt & 0xff else ("comb" if (nt >> 8) & 256 else "slab")].append((t, nt, s))
             t0 = cost(0, 0)
             line = f"{grp:5s} {name:8s} M={M:4d} N={N:5d} K={K:5d} static {t0:6.1f}us"
-            for k in ("slab", "comb"):
+            for k in ("slab", "comb", "stream"):
                 top = sorted(res[k])[:3]
                 line += f" | {k}: " + ", ".join(f"{t:.1f} ({nt:#x}/s{s})" for t, nt, s in top)
             print(line, flush=True)

@@ -37,7 +37,7 @@ def timeit(fn, iters=50):
     torch.cuda.synchronize()
     if GRAPH:
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             for i in range(iters):
                 fn(i)
         g.replay()

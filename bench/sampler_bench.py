@@ -26,7 +26,7 @@ def main():
                     f()
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     for _ in range(20):
                         f()
                 g.replay()

@@ -62,7 +62,7 @@ def main():
         body(cross, mode)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             body(cross, mode)
         g.replay()
         torch.cuda.synchronize()

@@ -43,6 +43,10 @@ void launch_attn_decode_fused(const void* qkv, int64_t q_stride, const void* par
                               const void* block_tables, int bt_stride, const void* ctx_lens, void* out,
                               int64_t out_stride, void* part_o, void* part_ml, int B, int nh, int nkv, int D,
                               int block_size, int nsplit, int part_size, float scale, hipStream_t st);
+int launch_gemm_qkv_args(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y, int64_t ldy,
+                         int M, int N, int K, void* workspace, int64_t ws_bytes, int nt_hint, int split_hint,
+                         const void* pos, const void* cos_t, const void* sin_t, void* kc, void* vc, const void* slot,
+                         int nh, int nkv, int D, int rot, int block_size, int style, bool do_rope, hipStream_t st);
 int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_fp8, const void* w_scale,
                 const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace,
                 int64_t ws_bytes, int nt_hint, int split_hint, bool partial_out, hipStream_t st);
@@ -133,6 +137,14 @@ PYBIND11_MODULE(_C, m) {
                    int nt_hint, int split_hint, bool partial_out, uintptr_t st) {
     return launch_gemm(CP(x), ldx, CP(w), ldw, fp8, CP(ws), CP(bias), P(y), ldy, M, N, K, act, glu, P(work), wbytes,
                        nt_hint, split_hint, partial_out, S(st));
+  });
+  m.def("gemm_qkv", [](uintptr_t x, int64_t ldx, uintptr_t w, int64_t ldw, uintptr_t bias, uintptr_t y, int64_t ldy,
+                       int M, int N, int K, uintptr_t work, int64_t wbytes, int nt_hint, int split_hint, uintptr_t pos,
+                       uintptr_t cos_t, uintptr_t sin_t, uintptr_t kc, uintptr_t vc, uintptr_t slot, int nh, int nkv,
+                       int D, int rot, int bs, int style, bool do_rope, uintptr_t st) {
+    return launch_gemm_qkv_args(CP(x), ldx, CP(w), ldw, CP(bias), P(y), ldy, M, N, K, P(work), wbytes, nt_hint,
+                                split_hint, CP(pos), CP(cos_t), CP(sin_t), P(kc), P(vc), CP(slot), nh, nkv, D, rot, bs,
+                                style, do_rope, S(st));
   });
   m.def("gemm_plan", [](int M, int N, int K, bool fp8) {
     int nt, s;

@@ -136,6 +136,70 @@ __device__ __forceinline__ TileWork tile_work(int ntm, int ntn, int bm, int bn) 
   return {(t - nt * ntm) * bm, nt * bn, z};
 }
 
+// QKV-projection epilogue (decode / prompt chunks): instead of the separate RoPE + paged-KV-write kernel
+// (embed_rope.hip rope_cache_kernel, whose semantics this reproduces), the GEMM's LDS-staged epilogue
+// rounds each (token m, 8 columns) group to bf16 as the unfused output would be, rotates q / k columns
+// (neox: the partner column d +- rot/2 is read from the same tile row - the host only takes this path
+// with head-aligned tiles; gptj: pairs inside the group), stores the row to the qkv buffer and the k / v
+// groups to their paged-cache rows (bf16 caches). D == 0: not a QKV projection.
+struct QkvEpi {
+  const int64_t* pos;
+  const float* cos_t;
+  const float* sin_t;
+  bf16_t* kc;
+  bf16_t* vc;
+  const int64_t* slot;
+  int nh, nkv, D, rot, block_size, style, do_rope;
+};
+
+__device__ __forceinline__ void qkv_epi8(const QkvEpi& e, const float* crow, int c, int n, int m,
+                                         const bf16_t* __restrict__ bias, bf16_t* dst) {
+  const int D = e.D, nq = e.nh * D, nk = e.nkv * D;
+  const int d = n % D;  // column inside its head (q, k and v regions all start at multiples of D)
+  float x[8], y[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    x[i] = bf2f(f2bf(crow[c + i] + (bias ? bf2f(bias[n + i]) : 0.f)));
+    y[i] = x[i];
+  }
+  const bool is_v = n >= nq + nk;
+  if (e.do_rope && !is_v && d < e.rot) {
+    const int rh = e.rot >> 1;
+    const int64_t p = e.pos[m];
+    if (e.style == 1) {  // gptj: interleaved pairs (2i, 2i + 1), angle d / 2 + i
+      const float* cs = e.cos_t + p * rh + (d >> 1);
+      const float* sn = e.sin_t + p * rh + (d >> 1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        y[2 * i] = x[2 * i] * cs[i] - x[2 * i + 1] * sn[i];
+        y[2 * i + 1] = x[2 * i + 1] * cs[i] + x[2 * i] * sn[i];
+      }
+    } else {  // neox: halves [0, rh) and [rh, rot) rotate against each other
+      const bool lo = d < rh;
+      const int a = lo ? d : d - rh, sh = lo ? rh : -rh;
+      const float* cs = e.cos_t + p * rh + a;
+      const float* sn = e.sin_t + p * rh + a;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float xp = bf2f(f2bf(crow[c + sh + i] + (bias ? bf2f(bias[n + sh + i]) : 0.f)));
+        y[i] = lo ? x[i] * cs[i] - xp * sn[i] : x[i] * cs[i] + xp * sn[i];
+      }
+    }
+  }
+  u16x8 o;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = f2bf(y[i]);
+  *reinterpret_cast<u16x8*>(dst) = o;
+  if (n >= nq && e.kc) {
+    const int64_t s = e.slot[m];
+    if (s >= 0) {
+      const int h = (n - (is_v ? nq + nk : nq)) / D;
+      const int64_t row = ((s / e.block_size) * e.nkv + h) * (int64_t)e.block_size + s % e.block_size;
+      *reinterpret_cast<u16x8*>((is_v ? e.vc : e.kc) + row * D + d) = o;
+    }
+  }
+}
+
 // Cooperative GEMM epilogue through LDS. A wave's accumulators (MT x NT mfma_f32_16x16x32 tiles in
 // the C layout: lane (li = lane & 15, g = lane >> 4) holds rows 4g..4g+3 of column li) are written
 // row-major into a padded fp32 image in LDS, then every thread stores 16 B row-contiguous pieces:
@@ -148,7 +212,7 @@ template <int BM, int BN, int MT, int NT, int NTHR, int LDSB>
 __device__ __forceinline__ void tile_store_lds(const f32x4 (&acc)[MT][NT], char* lds, int wrow0, int wcol0, int m0,
                                                int n0, int M, int N, float* __restrict__ part,
                                                bf16_t* __restrict__ Y, int64_t ldy, const bf16_t* __restrict__ bias,
-                                               int act, int glu) {
+                                               int act, int glu, const QkvEpi& qe = QkvEpi{}) {
   constexpr int LDW = BN + 4;  // padded row: the 4 rows a wave-instruction writes hit different banks
   constexpr int RMAX = LDSB / (LDW * 4);
   constexpr int R = (RMAX >= BM ? BM : RMAX) / 16 * 16;
@@ -209,6 +273,10 @@ __device__ __forceinline__ void tile_store_lds(const f32x4 (&acc)[MT][NT], char*
         const int r = v / VPR, c = (v - r * VPR) * 8;
         const int m = m0 + r0 + r, n = n0 + c;
         if (m >= M || n >= N) continue;
+        if (qe.D) {  // QKV projection: RoPE + paged KV write (N % 8 == 0, ldy % 8 == 0: host-checked)
+          qkv_epi8(qe, &ct[r * LDW], c, n, m, bias, Y + (int64_t)m * ldy + n);
+          continue;
+        }
         u16x8 o;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {

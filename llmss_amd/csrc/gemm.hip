@@ -550,7 +550,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_tiled_kernel(const bf16_t* __res
                                                          const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
                                                          int64_t ldy, float* __restrict__ part, int M, int N, int K,
                                                          int act, int glu, const float* __restrict__ wscale,
-                                                         int* __restrict__ cnt) {
+                                                         int* __restrict__ cnt, QkvEpi qe) {
   constexpr int MTW = BM / (8 * NW), NTW = BN / 32;  // 16x16 tiles per wave (waves NW/2 x 2)
   constexpr int A_BYTES = BM * TBK * 2, B_BYTES = TiledB<BN, F8, NW>::BYTES, STAGE = A_BYTES + B_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
@@ -620,6 +620,14 @@ __global__ __launch_bounds__(64 * NW) void gemm_tiled_kernel(const bf16_t* __res
                                   reinterpret_cast<int*>(smem)))
       return;
     part = nullptr;
+  }
+  if constexpr (!F8) {
+    if (qe.D) {  // QKV projection: RoPE + paged KV write in the LDS-staged epilogue (unsplit / combined)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      tile_store_lds<BM, BN, MTW, NTW, 64 * NW, NS * STAGE>(acc, smem, wr * (MTW * 16), wc * (NTW * 16), m0, n0, M,
+                                                             N, nullptr, Y, ldy, bias, 0, 0, qe);
+      return;
+    }
   }
   // epilogue (C layout: col = lane&15 -> n, row = 4*(lane>>4)+i -> m)
   const int wn0 = n0 + wc * (NTW * 16);
@@ -1314,7 +1322,7 @@ int gemm_skinny_splitk(int M, int N, int K) {
 
 int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const bf16_t* B, bf16_t* Y, int64_t ldy,
                  int M, int N, int K, int act, int g, int tsel, int split_hint, void* workspace, int64_t ws_bytes,
-                 bool partial_out, hipStream_t st, const float* wscale = nullptr);
+                 bool partial_out, hipStream_t st, const float* wscale = nullptr, const QkvEpi* qe = nullptr);
 
 int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int nt_hint, int split_hint,
                        int64_t ws_bytes);
@@ -1418,7 +1426,8 @@ static int tiles_of(int M, int N, int bm, int bn) { return ((M + bm - 1) / bm) *
 bool gemm_mid_dims(int tsel, int* bm, int* bn, int* threads);
 void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
-                     int split, hipStream_t st, bool packed = false, int* cnt = nullptr);
+                     int split, hipStream_t st, bool packed = false, int* cnt = nullptr,
+                     const QkvEpi* qe = nullptr);
 
 // tsel 8-12: gemm_mid (gemm_mid.hip: buffer-descriptor staging, 128x128 / 256x128 / 64x256 / 64x128 / 128x256)
 static int tile_dims(int tsel, int* bm, int* bn) {
@@ -1544,7 +1553,8 @@ static bool launch_streamk(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_
 
 int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const bf16_t* B, bf16_t* Y, int64_t ldy,
                  int M, int N, int K, int act, int g, int tsel, int split_hint, void* workspace, int64_t ws_bytes,
-                 bool partial_out, hipStream_t st, const float* wscale) {
+                 bool partial_out, hipStream_t st, const float* wscale, const QkvEpi* qe) {
+  const QkvEpi qv = qe ? *qe : QkvEpi{};
   const int tsel_raw = tsel;
   int s = split_hint;
   const bool f8 = wscale != nullptr;  // fp8-e4m3 weights (W8A16): half the weight bytes of a decode step
@@ -1576,12 +1586,13 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   int* cnt = nullptr;
   if ((tsel_raw & 256) && s > 1 && (int64_t)nt * s * bm * bn * 4 <= ws_bytes && Y) cnt = sk_counters(nt);
   if (!cnt && (int64_t)s * M * N * 4 > ws_bytes) s = 1;
+  if (qe && (s > 1 && !cnt)) throw std::runtime_error("gemm: the QKV epilogue needs an unsplit or in-launch-combined plan");
   float* part = s > 1 ? (float*)workspace : nullptr;
   const int act_k = s > 1 && !cnt ? 0 : act, glu_k = s > 1 && !cnt ? 0 : g;
   dim3 grid(nt, s);
   if (tsel >= 8 && tsel <= 12) {
     launch_gemm_mid(tsel, ns, wnt_ok(tsel_raw, M, tsel), X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, part, M, N, K,
-                    act_k, glu_k, s, st, false, cnt);
+                    act_k, glu_k, s, st, false, cnt, qe);
     if (cnt) return 0;
     if (s > 1 && partial_out && !g && act == 0) return s;
     if (s > 1) {
@@ -1599,10 +1610,10 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   do {                                                                                                             \
     if (wnt)                                                                                                       \
       gemm_tiled_kernel<BM_, BN_, NS_, true, false, 8><<<grid, 512, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N, K, \
-                                                                             act_k, glu_k, nullptr, cnt);          \
+                                                                             act_k, glu_k, nullptr, cnt, qv);      \
     else                                                                                                           \
       gemm_tiled_kernel<BM_, BN_, NS_, false, false, 8><<<grid, 512, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N,  \
-                                                                              K, act_k, glu_k, nullptr, cnt);      \
+                                                                              K, act_k, glu_k, nullptr, cnt, qv);  \
   } while (0)
     if (tsel == 5) {
       if (ns == 3) LT8(256, 128, 3); else LT8(256, 128, 2);
@@ -1613,7 +1624,7 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   } else {
 #define LT1(BM_, BN_, NS_, WNT_, F8_)                                                                              \
   gemm_tiled_kernel<BM_, BN_, NS_, WNT_, F8_><<<grid, 256, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, part, M, N, K, act_k,  \
-                                                                    glu_k, wscale, cnt)
+                                                                    glu_k, wscale, cnt, qv)
 #define LT(BM_, BN_, NS_)                                                                                          \
   do {                                                                                                             \
     if (f8) {                                                                                                      \
@@ -1678,6 +1689,45 @@ int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int n
   }
   if ((int64_t)s * M * N * 4 > ws_bytes) s = 1;
   return s > 1 ? s : 0;
+}
+
+// QKV projection with the RoPE + paged-KV-write epilogue (common.h qkv_epi8) instead of a separate
+// rope_cache launch. Plan: the hints, else the tuned entry of kind 3 (ops/autotune.py "qkv_epi"), else
+// the static tiled plan; a split plan always runs as an in-launch combine (the epilogue needs finished
+// sums). Returns 0 when launched, -1 when this shape / plan cannot take the epilogue (stream / big-tile
+// / stream-K plans, fp8 weights, neox RoPE on tiles that are not head-aligned) - the caller then runs
+// the plain GEMM and the rope_cache kernel.
+int launch_gemm_qkv(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y, int64_t ldy,
+                    int M, int N, int K, void* workspace, int64_t ws_bytes, int nt_hint, int split_hint,
+                    const QkvEpi& qe, hipStream_t st) {
+  if (M == 0) return 0;
+  if (qe.D <= 0 || qe.D % 8 || N != (qe.nh + 2 * qe.nkv) * qe.D || N % 8 || ldy % 8 || K % 16) return -1;
+  if (qe.do_rope && (qe.rot % 8 || qe.rot > qe.D || (qe.style == 0 && qe.rot % 16))) return -1;
+  if (nt_hint == 0 && split_hint == 0) gemm_tuned_get(M, N, K, false, 3, &nt_hint, &split_hint);
+  if (nt_hint & 0xff) return -1;  // streaming kernels have no LDS-staged epilogue
+  int tsel = nt_hint >> 8, s = split_hint;
+  gemm_tiled_plan(M, N, K, &tsel, &s, false);
+  const int t = tsel & 15;
+  if (t == 4 || (tsel & 128)) return -1;
+  int bm, bn;
+  tile_dims(t, &bm, &bn);
+  if (qe.do_rope && qe.style == 0 && bn % qe.D) return -1;  // neox partner columns must share the tile
+  if (s > 1) {
+    if ((int64_t)tiles_of(M, N, bm, bn) * s * bm * bn * 4 > ws_bytes) return -1;
+    tsel |= 256;
+  }
+  launch_tiled((const bf16_t*)x, ldx, w, ldw, (const bf16_t*)bias, (bf16_t*)y, ldy, M, N, K, 0, 0, tsel, s, workspace,
+               ws_bytes, false, st, nullptr, &qe);
+  return 0;
+}
+
+int launch_gemm_qkv_args(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y, int64_t ldy,
+                         int M, int N, int K, void* workspace, int64_t ws_bytes, int nt_hint, int split_hint,
+                         const void* pos, const void* cos_t, const void* sin_t, void* kc, void* vc, const void* slot,
+                         int nh, int nkv, int D, int rot, int block_size, int style, bool do_rope, hipStream_t st) {
+  const QkvEpi qe{(const int64_t*)pos, (const float*)cos_t, (const float*)sin_t, (bf16_t*)kc, (bf16_t*)vc,
+                  (const int64_t*)slot, nh, nkv, D, rot, block_size, style, do_rope ? 1 : 0};
+  return launch_gemm_qkv(x, ldx, w, ldw, bias, y, ldy, M, N, K, workspace, ws_bytes, nt_hint, split_hint, qe, st);
 }
 
 void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk) {

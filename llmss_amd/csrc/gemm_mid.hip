@@ -27,7 +27,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
                                                               const bf16_t* __restrict__ B, int64_t ldb,
                                                               const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
                                                               int64_t ldy, float* __restrict__ part, int M, int N, int K,
-                                                              int act, int glu, int* __restrict__ cnt) {
+                                                              int act, int glu, int* __restrict__ cnt, QkvEpi qe) {
   constexpr int NW = WM * WN;
   constexpr int MT = BM / WM / 16, NT = BN / WN / 16;  // 16x16 accumulator tiles per wave
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
   // step) and tile_store_lds waits for this wave's last fragment reads before its first barrier
   tile_store_lds<BM, BN, MT, NT, 64 * NW, NS * STAGE>(acc, smem, wm * (MT * 16), wn * (NT * 16), m0, n0, M, N,
                                                         part ? part + (int64_t)zk * M * N : nullptr, Y, ldy, bias,
-                                                        act, glu);
+                                                        act, glu, qe);
 }
 
 // tsel 8: 128x128 (2x2 waves), 9: 256x128 (4x2), 10: 64x256 (1x4), 11: 64x128 (1x4), 12: 128x256 (2x4)
@@ -198,7 +198,8 @@ static int mid_depth(int bm, int bn, int want) {
 
 void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
-                     int split, hipStream_t st, bool packed, int* cnt) {
+                     int split, hipStream_t st, bool packed, int* cnt, const QkvEpi* qe) {
+  const QkvEpi qv = qe ? *qe : QkvEpi{};
   int bm, bn, thr;
   if (!gemm_mid_dims(tsel, &bm, &bn, &thr)) throw std::runtime_error("gemm_mid: bad tile code");
   if (glu && (bn / (thr / 64 / (bm == 256 ? 4 : (bm == 128 ? 2 : 1))) / 16) % 2)
@@ -212,7 +213,7 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
   dim3 grid(tiles, split);
 #define MID1(BM_, BN_, WM_, WN_, NS_, WNT_, PK_)                                                                   \
   gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, WNT_, PK_><<<grid, 64 * WM_ * WN_, 0, st>>>(X, ldx, W, ldw, bias, Y, ldy, \
-                                                                                      part, M, N, K, act, glu, cnt)
+                                                                                      part, M, N, K, act, glu, cnt, qv)
 #define MID(BM_, BN_, WM_, WN_, NS_)                                                                             \
   do {                                                                                                         \
     if (packed) {                                                                                              \

@@ -601,10 +601,13 @@ class LLMEngine:
                         self._decode_forward(b, buf, dist=d)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        # thread-local capture: the RCCL communicator's watchdog thread keeps querying the events of earlier
+        # collectives; under the default global capture mode such a query from another thread aborts the
+        # process ("operation not permitted when stream is capturing")
         for b in reversed(self.buckets):
             for d in modes:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
+                with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                     self._decode_forward(b, buf, dist=d)
                 self.graphs[(b, d)] = g
         torch.cuda.synchronize()

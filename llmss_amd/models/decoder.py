@@ -94,6 +94,9 @@ class DecoderLM:
         # full-batch ones) and each cross-stream hand-off inside a HIP graph ~10 us, more than a
         # modelled 52 us all-reduce hides: 2639 vs 2519 us per step (profiles/r1_tbo/)
         self.tbo_min = int(os.environ.get("LLMSS_TP_DECODE_OVERLAP_MIN", "0"))
+        # QKV GEMM epilogue with RoPE + paged KV write (one launch instead of two) wherever the autotuner
+        # installed a faster plan for it (LLMSS_QKV_EPI=0: always GEMM + rope_cache)
+        self.qkv_epi = os.environ.get("LLMSS_QKV_EPI", "1") != "0"
         self._comm_stream = None
 
     @property
@@ -122,19 +125,35 @@ class DecoderLM:
                  torch.zeros(shp, dtype=dt, device=self.device)) for _ in range(self.cfg.num_layers)]
 
     # ---------------------------------------------------------------------------- forward
-    def _attention(self, qkv, inp: StepInput, kc, vc):
+    def _qkv_rope_cache(self, L, y, inp: StepInput, kc, vc):
+        """QKV projection, RoPE and the paged KV write of the step's tokens -> the bf16 qkv rows.
+
+        Where the autotuner found it faster (a kind-3 plan for this M, ops/autotune.py tune_qkv_epilogue)
+        this is ONE GEMM launch whose epilogue rotates q / k and stores k / v to the cache; otherwise the
+        GEMM (split-K slabs allowed) followed by the rope_cache kernel, which sums the slabs itself."""
+        cfg, p = self.cfg, self.plan
+        do_rope = cfg.position == "rope"
+        if y.is_cuda and self.qkv_epi and not self.kv_fp8 and L.qkv.w.dim() == 2 and L.qkv.w_scale is None \
+                and _hip_ops().lib().gemm_tuned_get(y.shape[0], L.qkv.N, L.qkv.K, False, 3) is not None:
+            out = _hip_ops().linear_qkv(y, L.qkv.w, L.qkv.b, inp.positions, self.w.cos, self.w.sin, kc, vc, inp.slots,
+                                        p.nh_l, p.nkv_l, cfg.head_dim, cfg.rotary_dim, cfg.rope_style, do_rope)
+            if out is not None:
+                return out
+        return ops.rope_cache(L.qkv(y, partial_ok=True), inp.positions, self.w.cos, self.w.sin, kc, vc, inp.slots,
+                              p.nh_l, p.nkv_l, cfg.head_dim, cfg.rotary_dim, cfg.rope_style, do_rope=do_rope)
+
+    def _attention(self, L, y, inp: StepInput, kc, vc):
         cfg, p = self.cfg, self.plan
         D = cfg.head_dim
         do_rope = cfg.position == "rope"
-        if inp.kind == "decode" and qkv.is_cuda and self.fused_decode and not self.kv_fp8 and \
+        if inp.kind == "decode" and y.is_cuda and self.fused_decode and not self.kv_fp8 and \
                 _hip_ops().fused_decode_ok(D, cfg.rotary_dim, cfg.rope_style, do_rope):
             # one launch: RoPE + paged KV write of the new token + attention (no rope_cache kernel)
             return _hip_ops().attn_decode_fused(
-                qkv, inp.positions, self.w.cos, self.w.sin, kc, vc, inp.slots, inp.block_tables, inp.ctx_lens,
-                p.nh_l, p.nkv_l, D, cfg.rotary_dim, cfg.rope_style, self.scale, inp.max_ctx, do_rope=do_rope,
-                splits=inp.decode_splits)
-        qkv = ops.rope_cache(qkv, inp.positions, self.w.cos, self.w.sin, kc, vc, inp.slots, p.nh_l, p.nkv_l, D,
-                             cfg.rotary_dim, cfg.rope_style, do_rope=cfg.position == "rope")
+                L.qkv(y, partial_ok=True), inp.positions, self.w.cos, self.w.sin, kc, vc, inp.slots,
+                inp.block_tables, inp.ctx_lens, p.nh_l, p.nkv_l, D, cfg.rotary_dim, cfg.rope_style, self.scale,
+                inp.max_ctx, do_rope=do_rope, splits=inp.decode_splits)
+        qkv = self._qkv_rope_cache(L, y, inp, kc, vc)
         if inp.kind == "prefill":
             return ops.attn_prefill(qkv, inp.cu_seqlens, inp.max_seqlen, p.nh_l, p.nkv_l, D, self.scale)
         if inp.kind == "extend":
@@ -269,7 +288,7 @@ class DecoderLM:
                 for j in (0, 1):
                     ready(pend[j])
                     y, res[j] = ops.add_norm(delta[j], L.ln1_w, L.ln1_b, eps, rms, res[j])
-                    a = self._attention(L.qkv(y, partial_ok=True), subs[j], kc, vc)
+                    a = self._attention(L, y, subs[j], kc, vc)
                     delta[j] = L.o(a).add_(L.down(L.up(y, self.act)))
                     pend[j] = reduce(delta[j])
                 continue
@@ -277,7 +296,7 @@ class DecoderLM:
             for j in (0, 1):
                 ready(pend[j])
                 y, res[j] = ops.add_norm(delta[j], L.ln1_w, L.ln1_b, eps, rms, res[j])
-                a = self._attention(L.qkv(y, partial_ok=True), subs[j], kc, vc)
+                a = self._attention(L, y, subs[j], kc, vc)
                 o[j] = L.o(a)
                 pend[j] = reduce(o[j])
             for j in (0, 1):
@@ -306,7 +325,7 @@ class DecoderLM:
             kc, vc = kv_caches[i]
             y, residual = ops.add_norm(delta, L.ln1_w, L.ln1_b, eps, rms, residual)
             # column-parallel QKV: its split-K partials are summed inside the rope/cache kernel
-            a = self._attention(L.qkv(y, partial_ok=True), inp, kc, vc)
+            a = self._attention(L, y, inp, kc, vc)
             if cfg.parallel_block:  # GPT-J: one all-reduce for attention + MLP
                 delta = self._reduce_rows(lambda a_, y_: L.o(a_).add_(L.down(L.up(y_, self.act))), a, y)
             elif fuse:

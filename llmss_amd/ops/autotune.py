@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import itertools
 import math
+import os
 import time
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -102,7 +103,7 @@ def _time(fn, iters: int) -> float:
     run them): timing a host loop instead measures Python launch overhead (~10 us per call) for
     every kernel shorter than that, which is most TP-sharded decode GEMMs."""
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         for i in range(iters):
             fn(i)
     g.replay()
@@ -187,9 +188,106 @@ def model_shapes(model) -> Dict[str, GemmShape]:
     return out
 
 
+def qkv_epi_candidates(M: int, N: int, K: int, D: int, neox_rope: bool) -> List[Tuple[int, int]]:
+    """(nt_hint, split) plans that can run the QKV RoPE + KV-write epilogue: tiled / gemm_mid tiles, unsplit
+    or combined in-launch (a split plan runs as a combine); neox RoPE needs head-aligned tiles (BN % D)."""
+    tiles = [(3, 64, (16, 32)), (2, 128, (16, 32)), (11, 128, (16, 32)), (10, 256, (16,))]
+    if M > 64:
+        tiles += [(1, 128, (0, 16)), (8, 128, (16,)), (12, 256, (16,))]
+    if M >= 256:
+        tiles += [(9, 128, (0,))]
+    nk = -(-K // 64)
+    out = []
+    for t, bn, depths in tiles:
+        if neox_rope and bn % D:
+            continue
+        for d in depths:
+            out += [((t | d | (256 if s > 1 else 0)) << 8, s) for s in (1, 2, 3, 4, 6, 8) if s == 1 or nk // s >= 2]
+    return out
+
+
+def tune_qkv_epilogue(model, ms: Sequence[int], native=None, iters: int = 16) -> Dict[int, Tuple[float, float]]:
+    """Per decode bucket M: GEMM + rope_cache (the tuned QKV plan, its slabs summed by the rope kernel) vs
+    the fused QKV GEMM whose epilogue applies RoPE and writes the paged KV cache (hip.linear_qkv). Where the
+    fused launch is faster its plan goes into the native table as kind 3, which the decoder's QKV step
+    consults. Returns {M: (unfused us, fused us)}."""
+    from .. import _native
+    from . import hip as H
+
+    lib = native or _native()
+    cfg, p, L = model.cfg, model.plan, model.w.layers[0]
+    if L.qkv.packed or L.qkv.w_scale is not None or getattr(model, "kv_fp8", False):
+        return {}
+    dev = model.device
+    N, K, D = L.qkv.N, L.qkv.K, cfg.head_dim
+    do_rope = cfg.position == "rope"
+    rot, style = cfg.rotary_dim, cfg.rope_style
+    neox = do_rope and style != "gptj"
+    ncopy = max(2, min(64, math.ceil((600 << 20) / (N * K * 2))))
+    g = torch.Generator(device=dev)
+    g.manual_seed(4321)
+    base = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(torch.bfloat16)
+    ws = [base.clone() for _ in range(ncopy)]
+    bias = L.qkv.b
+    res = {}
+    for M in sorted(set(int(m) for m in ms)):
+        bs = 16
+        nb = -(-M // bs) + 1
+        kc = torch.zeros(nb, p.nkv_l, bs, D, dtype=torch.bfloat16, device=dev)
+        vc = torch.zeros_like(kc)
+        slots = torch.arange(M, device=dev, dtype=torch.int64)
+        pos = torch.arange(M, device=dev, dtype=torch.int64) % min(cfg.max_position_embeddings, 256)
+        x = (torch.randn(M, K, device=dev, generator=g) * 0.5).to(torch.bfloat16)
+
+        def unfused(i):
+            q = H.linear(x, ws[i % ncopy], bias, partial_ok=True)
+            H.rope_cache(q, pos, model.w.cos, model.w.sin, kc, vc, slots, p.nh_l, p.nkv_l, D, rot, style, do_rope)
+
+        def fused_fn(nt, s):
+            def f(i):
+                y = H.linear_qkv(x, ws[i % ncopy], bias, pos, model.w.cos, model.w.sin, kc, vc, slots, p.nh_l,
+                                 p.nkv_l, D, rot, style, do_rope, nt_hint=nt, split_hint=s)
+                if y is None:
+                    raise RuntimeError("plan cannot take the QKV epilogue")
+            return f
+
+        unfused(0)
+        torch.cuda.synchronize(dev)
+        t_un = _time(unfused, iters)
+        best = (0, 0, float("inf"))
+        for nt, s in qkv_epi_candidates(M, N, K, D, neox):
+            try:
+                f = fused_fn(nt, s)
+                f(0)
+                torch.cuda.synchronize(dev)
+                t = _time(f, iters)
+            except (RuntimeError, ValueError):
+                continue
+            if t < best[2]:
+                best = (nt, s, t)
+        if best[0] and best[2] < t_un * 0.98:
+            lib.gemm_tuned_set(M, N, K, False, 3, best[0], best[1])
+            _QKV_PLANS[(M, N, K)] = (best[0], best[1])
+        res[M] = (t_un, best[2])
+    del ws
+    log.info("QKV RoPE/KV-write epilogue: %s", ", ".join(
+        f"M={m} {'fused' if f < u * 0.98 else 'unfused'} {min(u, f):.1f}us (unfused {u:.1f})" for m, (u, f) in res.items()))
+    return res
+
+
 # process-wide results: a second engine in the same process reuses the first one's plans, so both
 # run bit-identical kernels (and skip the tuning time)
 _DONE: Dict[Tuple[int, GemmShape, str], Tuple[int, int, float, float]] = {}
+_QKV_DONE: Dict[tuple, Dict[int, Tuple[float, float]]] = {}
+_QKV_PLANS: Dict[tuple, Tuple[int, int]] = {}
+
+
+def _reinstall_qkv(lib, model, results):
+    L = model.w.layers[0]
+    for M in results:
+        plan = _QKV_PLANS.get((M, L.qkv.N, L.qkv.K))
+        if plan:
+            lib.gemm_tuned_set(M, L.qkv.N, L.qkv.K, False, 3, plan[0], plan[1])
 
 
 def tune_model(model, ms: Sequence[int], native=None) -> Dict[Tuple[str, int], Tuple[int, int, float, float]]:
@@ -210,6 +308,15 @@ def tune_model(model, ms: Sequence[int], native=None) -> Dict[Tuple[str, int], T
             if nt:
                 lib.gemm_tuned_set(M, shp.N, shp.K, shp.glu, 2 if shp.packed else int(shp.fp8), nt, s)
             res[(name, M)] = done[key]
+    if os.environ.get("LLMSS_QKV_EPI", "1") != "0":
+        key = ("qkv_epi", tuple(sorted(set(int(m) for m in ms))), model_shapes(model)["qkv"], str(dev),
+               model.cfg.head_dim, model.cfg.rotary_dim, model.cfg.rope_style, model.cfg.position)
+        if key not in _QKV_DONE:
+            _QKV_DONE[key] = tune_qkv_epilogue(model, ms, lib)
+        else:  # re-install this process's earlier winners
+            _reinstall_qkv(lib, model, _QKV_DONE[key])
+        for M, (u, f) in _QKV_DONE[key].items():
+            res[("qkv_epi", M)] = (0, 0, min(u, f), u)
     torch.cuda.synchronize(dev)
     gain = sum(v[3] - v[2] for v in res.values())
     log.info("autotuned %d GEMM shapes in %.1fs (sum of per-call gains %.1f us)", len(res),

@@ -495,6 +495,43 @@ def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hi
     return y
 
 
+def linear_qkv(x, w, bias, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, rot, style, do_rope=True,
+               nt_hint=0, split_hint=0):
+    """QKV projection whose GEMM epilogue applies RoPE and writes k / v into the paged cache (one launch
+    instead of GEMM + rope_cache; same values). Returns the bf16 [T, N] qkv tensor, or None when this
+    weight / cache / plan cannot take the fused epilogue (packed or fp8 weights, fp8 KV rows, streaming or
+    big-tile plans, neox RoPE on tiles that are not head-aligned): the caller then runs linear + rope_cache."""
+    if w.dim() != 2 or w.dtype != torch.bfloat16 or (k_cache is not None and k_cache.dtype != torch.bfloat16):
+        return None
+    M, K = x.shape
+    _bf16_rows(x, "x")
+    _bf16_rows(w, "w")
+    _check(w.is_contiguous() and w.shape[1] == K, "w [N, K] contiguous")
+    N = w.shape[0]
+    _check(N == (nh + 2 * nkv) * D and D % 8 == 0, "qkv width")
+    if bias is not None:
+        _check(bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.numel() == N, "bias [N] bf16")
+    _check(positions.dtype == torch.int64 and positions.numel() == M and positions.is_contiguous(), "positions")
+    do_rope = bool(do_rope and rot > 0)
+    if do_rope:
+        _check(cos.dtype == torch.float32 and cos.is_contiguous() and cos.shape[1] == rot // 2, "cos table")
+        _check(sin.shape == cos.shape and sin.is_contiguous(), "sin table")
+    bs = 1
+    if k_cache is not None:
+        _kv_cache_check(k_cache, v_cache, nkv, D)
+        _check(slots is not None and slots.dtype == torch.int64 and slots.numel() == M and slots.is_contiguous(),
+               "slots")
+        bs = k_cache.shape[2]
+    ws = _GEMM_WS.get(64 << 20, x.device)
+    y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    rc = lib().gemm_qkv(x.data_ptr(), x.stride(0), w.data_ptr(), K, _ptr(bias), y.data_ptr(), y.stride(0), M, N, K,
+                        ws.data_ptr(), ws.numel() * 4, int(nt_hint), int(split_hint), positions.data_ptr(),
+                        _ptr(cos) if do_rope else 0, _ptr(sin) if do_rope else 0, _ptr(k_cache), _ptr(v_cache),
+                        _ptr(slots) if k_cache is not None else 0, nh, nkv, D, rot, bs, 1 if style == "gptj" else 0,
+                        do_rope, _stream())
+    return y if rc == 0 else None
+
+
 def add_norm_partial(p: PartialSum, weight, bias, eps, rms, residual, out=None):
     T, H = p.M, p.N
     _check(residual is not None and residual.is_contiguous() and residual.shape == (T, H), "residual [T, H]")

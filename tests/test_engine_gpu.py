@@ -176,6 +176,29 @@ def test_rccl_collectives_inside_decode_graphs():
     assert e_eager.generate(prompts, sp) == out_g
 
 
+def test_graph_capture_while_rccl_watchdog_polls():
+    """Regression: with the RCCL communicator's watchdog thread tracking earlier collectives, a capture in
+    torch's default (global) mode aborted the process when the watchdog queried an event mid-capture
+    ("operation not permitted when stream is capturing"). Engine and autotuner capture thread-locally."""
+    import os
+
+    import torch.distributed as dist
+
+    from llmss_amd.ops import autotune as A
+
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    t = torch.ones(1 << 16, device="cuda")
+    for i in range(60):
+        for _ in range(4):  # eager collectives: work items the watchdog polls
+            dist.all_reduce(t)
+        A._time(lambda j: dist.all_reduce(t), 4)  # captures with a collective inside
+    torch.cuda.synchronize()
+    assert torch.isfinite(t).all()
+
+
 def _one_member_tp():
     import os
 

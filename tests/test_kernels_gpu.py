@@ -101,6 +101,46 @@ def test_rope_cache_from_split_k_partials(style, T):
     close(vc1, vc2, 2e-2)
 
 
+@pytest.mark.parametrize("style,D,rot,nh,nkv,bias", [("neox", 128, 128, 8, 2, False), ("gptj", 256, 64, 4, 4, True),
+                                                      ("none", 64, 0, 6, 6, True), ("neox", 64, 64, 8, 1, False)])
+@pytest.mark.parametrize("tile", [1, 2, 3, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("split", [1, 3])
+@pytest.mark.parametrize("T", [40, 300])
+def test_qkv_gemm_rope_cache_epilogue(style, D, rot, nh, nkv, bias, tile, split, T):
+    """QKV GEMM whose epilogue applies RoPE and writes the paged KV cache (one launch) == GEMM + rope_cache:
+    q/k/v rows and every cache row, with a skipped slot (-1) and NaN-filled caches whose unwritten rows
+    must stay untouched. Plans the epilogue cannot take (neox on tiles narrower than a head) return None."""
+    torch.manual_seed(0)
+    K, bs, nb = 512, 16, 40
+    N = (nh + 2 * nkv) * D
+    x, w = rnd(T, K), rnd(N, K, scale=K ** -0.5)
+    b = rnd(N, scale=0.1) if bias else None
+    do_rope = style != "none"
+    st = "gptj" if style == "gptj" else "neox"
+    pos = torch.randint(0, 120, (T,), device=dev)
+    cos, sin = R.rope_tables(128, rot if do_rope else 64, 10000.0, dev)
+    slots = torch.randperm(nb * bs, device=dev)[:T]
+    slots[5] = -1
+    kc1 = torch.full((nb, nkv, bs, D), float("nan"), dtype=torch.bfloat16, device=dev)
+    vc1 = torch.full_like(kc1, float("nan"))
+    d = 16 if tile not in (1, 9) else 0
+    hint = (tile | d) << 8
+    y = H.linear_qkv(x, w, b, pos, cos, sin, kc1, vc1, slots, nh, nkv, D, rot, st, do_rope, nt_hint=hint,
+                     split_hint=split)
+    bn = {1: 128, 2: 128, 3: 64, 8: 128, 9: 128, 10: 256, 11: 128, 12: 256}[tile]
+    if do_rope and st == "neox" and bn % D:
+        assert y is None
+        return
+    assert y is not None
+    q2 = H.linear(x, w, b)
+    kc2, vc2 = torch.full_like(kc1, float("nan")), torch.full_like(vc1, float("nan"))
+    R.rope_cache(q2, pos, cos, sin, kc2, vc2, slots, nh, nkv, D, rot, st, do_rope=do_rope)
+    close(y, q2, 1e-2)
+    for a, r in ((kc1, kc2), (vc1, vc2)):
+        assert torch.equal(a.isnan(), r.isnan())
+        close(a.nan_to_num(0), r.nan_to_num(0), 1e-2)
+
+
 @pytest.mark.parametrize("version", [1, 2])
 @pytest.mark.parametrize("D,nh,nkv", [(64, 4, 4), (128, 8, 2), (128, 16, 1), (256, 4, 4), (128, 12, 4), (128, 16, 2),
                                       (64, 6, 3), (256, 8, 2)])
