@@ -152,50 +152,90 @@ struct QkvEpi {
   int nh, nkv, D, rot, block_size, style, do_rope;
 };
 
-__device__ __forceinline__ void qkv_epi8(const QkvEpi& e, const float* crow, int c, int n, int m,
-                                         const bf16_t* __restrict__ bias, bf16_t* dst) {
-  const int D = e.D, nq = e.nh * D, nk = e.nkv * D;
-  const int d = n % D;  // column inside its head (q, k and v regions all start at multiples of D)
-  float x[8], y[8];
+// One LDS row chunk of the QKV epilogue: each thread owns ITEMS (row, 8-column) groups of the chunk and
+// processes them G at a time in three phases - (1) every group's position and cache slot, (2) every
+// group's cos / sin rows, (3) rotate, round, store - so each thread pays two dependent memory round trips
+// per G groups instead of per group (the loads sit behind no per-group branch: addresses are clamped).
+template <int BN, int NTHR, int R>
+__device__ __forceinline__ void qkv_store_chunk(const QkvEpi& e, const float* ct, int ldw, int rows, int r0, int m0,
+                                                int n0, int M, int N, bf16_t* __restrict__ Y, int64_t ldy,
+                                                const bf16_t* __restrict__ bias) {
+  constexpr int VPR = BN / 8, ITEMS = (R * VPR + NTHR - 1) / NTHR, G = ITEMS < 4 ? ITEMS : 4;
+  const int D = e.D, nq = e.nh * D, nk = e.nkv * D, rh = e.rot >> 1;
+  const bool rope = e.do_rope != 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    x[i] = bf2f(f2bf(crow[c + i] + (bias ? bf2f(bias[n + i]) : 0.f)));
-    y[i] = x[i];
-  }
-  const bool is_v = n >= nq + nk;
-  if (e.do_rope && !is_v && d < e.rot) {
-    const int rh = e.rot >> 1;
-    const int64_t p = e.pos[m];
-    if (e.style == 1) {  // gptj: interleaved pairs (2i, 2i + 1), angle d / 2 + i
-      const float* cs = e.cos_t + p * rh + (d >> 1);
-      const float* sn = e.sin_t + p * rh + (d >> 1);
+  for (int i0 = 0; i0 < ITEMS; i0 += G) {
+    int rr[G], cc[G], mm[G];
+    bool ok[G];
+    int64_t p[G], sl[G];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        y[2 * i] = x[2 * i] * cs[i] - x[2 * i + 1] * sn[i];
-        y[2 * i + 1] = x[2 * i + 1] * cs[i] + x[2 * i] * sn[i];
-      }
-    } else {  // neox: halves [0, rh) and [rh, rot) rotate against each other
-      const bool lo = d < rh;
-      const int a = lo ? d : d - rh, sh = lo ? rh : -rh;
-      const float* cs = e.cos_t + p * rh + a;
-      const float* sn = e.sin_t + p * rh + a;
+    for (int j = 0; j < G; ++j) {  // phase 1: positions and slots
+      const int v = threadIdx.x + (i0 + j) * NTHR;
+      rr[j] = v / VPR;
+      cc[j] = (v - rr[j] * VPR) * 8;
+      mm[j] = m0 + r0 + rr[j];
+      ok[j] = i0 + j < ITEMS && rr[j] < rows && mm[j] < M && n0 + cc[j] < N;
+      const int mc = min(mm[j], M - 1);
+      p[j] = rope ? e.pos[mc] : 0;
+      sl[j] = e.kc ? e.slot[mc] : -1;
+    }
+    f32x4 cs[G][2], sn[G][2];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float xp = bf2f(f2bf(crow[c + sh + i] + (bias ? bf2f(bias[n + sh + i]) : 0.f)));
-        y[i] = lo ? x[i] * cs[i] - xp * sn[i] : x[i] * cs[i] + xp * sn[i];
+    for (int j = 0; j < G; ++j) {  // phase 2: cos / sin of each group's rotation angles
+      if (rope) {
+        const int n = n0 + cc[j], d = n % D;
+        const bool lo = d < rh;
+        int a = e.style == 1 ? (d >> 1) : (lo ? d : d - rh);
+        a = (n < nq + nk && d < e.rot) ? a : 0;  // columns that do not rotate read a valid (unused) entry
+        const float* cp = e.cos_t + p[j] * rh + a;
+        const float* sp = e.sin_t + p[j] * rh + a;
+        cs[j][0] = *reinterpret_cast<const f32x4*>(cp);
+        sn[j][0] = *reinterpret_cast<const f32x4*>(sp);
+        if (e.style != 1 && rh >= 8) {  // neox uses 8 angles per group (rh % 8 == 0: host-checked)
+          cs[j][1] = *reinterpret_cast<const f32x4*>(cp + 4);
+          sn[j][1] = *reinterpret_cast<const f32x4*>(sp + 4);
+        }
       }
     }
-  }
-  u16x8 o;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) o[i] = f2bf(y[i]);
-  *reinterpret_cast<u16x8*>(dst) = o;
-  if (n >= nq && e.kc) {
-    const int64_t s = e.slot[m];
-    if (s >= 0) {
-      const int h = (n - (is_v ? nq + nk : nq)) / D;
-      const int64_t row = ((s / e.block_size) * e.nkv + h) * (int64_t)e.block_size + s % e.block_size;
-      *reinterpret_cast<u16x8*>((is_v ? e.vc : e.kc) + row * D + d) = o;
+    for (int j = 0; j < G; ++j) {  // phase 3: bias, bf16 rounding, rotation, stores
+      if (!ok[j]) continue;
+      const int c = cc[j], n = n0 + c, d = n % D, m = mm[j];
+      const float* crow = ct + rr[j] * ldw;
+      float x[8], y[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        x[i] = bf2f(f2bf(crow[c + i] + (bias ? bf2f(bias[n + i]) : 0.f)));
+        y[i] = x[i];
+      }
+      const bool is_v = n >= nq + nk;
+      if (rope && !is_v && d < e.rot) {
+        if (e.style == 1) {  // gptj: interleaved pairs (2i, 2i + 1), angle d / 2 + i
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            y[2 * i] = x[2 * i] * cs[j][0][i] - x[2 * i + 1] * sn[j][0][i];
+            y[2 * i + 1] = x[2 * i + 1] * cs[j][0][i] + x[2 * i] * sn[j][0][i];
+          }
+        } else {  // neox: halves [0, rh) and [rh, rot) rotate against each other
+          const bool lo = d < rh;
+          const int sh = lo ? rh : -rh;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float xp = bf2f(f2bf(crow[c + sh + i] + (bias ? bf2f(bias[n + sh + i]) : 0.f)));
+            const float cv = cs[j][i >> 2][i & 3], sv = sn[j][i >> 2][i & 3];
+            y[i] = lo ? x[i] * cv - xp * sv : x[i] * cv + xp * sv;
+          }
+        }
+      }
+      u16x8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = f2bf(y[i]);
+      *reinterpret_cast<u16x8*>(Y + (int64_t)m * ldy + n) = o;
+      if (n >= nq && sl[j] >= 0) {
+        const int h = (n - (is_v ? nq + nk : nq)) / D;
+        const int64_t row = ((sl[j] / e.block_size) * e.nkv + h) * (int64_t)e.block_size + sl[j] % e.block_size;
+        *reinterpret_cast<u16x8*>((is_v ? e.vc : e.kc) + row * D + d) = o;
+      }
     }
   }
 }
@@ -236,7 +276,9 @@ __device__ __forceinline__ void tile_store_lds(const f32x4 (&acc)[MT][NT], char*
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const int rows = BM - r0 < R ? BM - r0 : R;  // the last chunk may be shorter
-    if (part) {  // fp32 slab rows: 4 floats (16 B) per thread-step
+    if (qe.D) {  // QKV projection: RoPE + paged KV write (N % 8 == 0, ldy % 8 == 0: host-checked)
+      qkv_store_chunk<BN, NTHR, R>(qe, ct, LDW, rows, r0, m0, n0, M, N, Y, ldy, bias);
+    } else if (part) {  // fp32 slab rows: 4 floats (16 B) per thread-step
       constexpr int VPR = BN / 4;
       for (int v = threadIdx.x; v < rows * VPR; v += NTHR) {
         const int r = v / VPR, c = (v - r * VPR) * 4;
@@ -273,10 +315,6 @@ __device__ __forceinline__ void tile_store_lds(const f32x4 (&acc)[MT][NT], char*
         const int r = v / VPR, c = (v - r * VPR) * 8;
         const int m = m0 + r0 + r, n = n0 + c;
         if (m >= M || n >= N) continue;
-        if (qe.D) {  // QKV projection: RoPE + paged KV write (N % 8 == 0, ldy % 8 == 0: host-checked)
-          qkv_epi8(qe, &ct[r * LDW], c, n, m, bias, Y + (int64_t)m * ldy + n);
-          continue;
-        }
         u16x8 o;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
