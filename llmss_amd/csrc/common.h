@@ -60,6 +60,25 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
+// Block-wide sums of two values with one pair of barriers. `red` must hold >= 32 floats.
+__device__ __forceinline__ f32x2 block_sum2(float a, float b, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  a = warp_sum(a);
+  b = warp_sum(b);
+  __syncthreads();
+  if (lane == 0) {
+    red[wid] = a;
+    red[16 + wid] = b;
+  }
+  __syncthreads();
+  f32x2 t = {0.f, 0.f};
+  for (int i = 0; i < nw; ++i) {
+    t[0] += red[i];
+    t[1] += red[16 + i];
+  }
+  return t;
+}
+
 __device__ __forceinline__ float block_max(float v, float* red) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
   v = warp_max(v);
