@@ -20,6 +20,11 @@ CONFIGS = [  # name, M, K, nh, nkv, D, rot, style, bias
     ("llama7b tp8", 512, 4096, 4, 4, 128, 128, "neox", False),
     ("gpt2-xl", 64, 1600, 25, 25, 64, 0, "none", True),
     ("llama13b tp8", 512, 5120, 5, 5, 128, 128, "neox", False),
+    # the same Llama shapes with q/k head dims interleaved at load (neox pairs made adjacent, gptj-style
+    # rotation in the epilogue): any tile width can rotate in-register
+    ("llama7b tp1 il", 64, 4096, 32, 32, 128, 128, "gptj", False),
+    ("llama7b tp8 il", 512, 4096, 4, 4, 128, 128, "gptj", False),
+    ("llama13b tp8 il", 512, 5120, 5, 5, 128, 128, "gptj", False),
 ]
 
 
@@ -67,7 +72,7 @@ def main():
             except (RuntimeError, ValueError):
                 continue
         fused.sort()
-        print(f"{name:13s} M={M:4d} N={N:5d} K={K:5d} unfused {best_un[0]:6.1f}us {best_un[1]} | fused: "
+        print(f"{name:15s} M={M:4d} N={N:5d} K={K:5d} unfused {best_un[0]:6.1f}us {best_un[1]} | fused: "
               + ", ".join(f"{t:.1f} ({nt}/s{s})" for t, nt, s in fused[:3]), flush=True)
         del ws
 

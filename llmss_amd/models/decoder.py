@@ -21,6 +21,8 @@ followed by an all-gather of [B, V/tp] logits.
 """
 from __future__ import annotations
 
+import dataclasses
+
 import os
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
@@ -67,6 +69,9 @@ class StepInput:
 
 class DecoderLM:
     def __init__(self, cfg: ModelConfig, weights: ModelWeights, tp: Optional[TPGroup] = None):
+        if weights.rope_interleaved and cfg.rope_style == "neox":
+            # q / k head dims were interleaved at load: the same rotation in its gptj (adjacent-pair) form
+            cfg = dataclasses.replace(cfg, rope_style="gptj")
         self.cfg = cfg
         self.w = weights
         self.tp = tp or TPGroup()

@@ -145,6 +145,9 @@ class ModelWeights:
     cos: Optional[torch.Tensor] = None
     sin: Optional[torch.Tensor] = None
     extra: dict = field(default_factory=dict)
+    # neox RoPE models: q / k head dims were interleaved at load (ref.rope_interleave_rows), so the
+    # model applies gptj-style RoPE to them (DecoderLM.rope_style)
+    rope_interleaved: bool = False
 
     def nbytes(self) -> int:
         """Device bytes held (views sharing one allocation, like a tied embedding / head, count once)."""
@@ -191,8 +194,16 @@ def _finish(cfg: ModelConfig, plan: ShardPlan, wte, wpe, layers_raw, lnf_w, lnf_
             return Linear(q, b, s, glu)
         return Linear(w, b, None, glu)
 
+    # neox RoPE: interleave the q / k head dims (LLMSS_ROPE_INTERLEAVE=0 keeps the checkpoint order)
+    il = cfg.position == "rope" and cfg.rope_style == "neox" and os.environ.get("LLMSS_ROPE_INTERLEAVE", "1") != "0"
     layers = []
     for d in layers_raw:
+        if il:
+            d = dict(d)
+            d["qkv_w"] = ref.rope_interleave_rows(d["qkv_w"], plan.nh_l, plan.nkv_l, cfg.head_dim, cfg.rotary_dim)
+            if d.get("qkv_b") is not None:
+                d["qkv_b"] = ref.rope_interleave_rows(d["qkv_b"], plan.nh_l, plan.nkv_l, cfg.head_dim,
+                                                      cfg.rotary_dim)
         if cfg.gated_mlp:
             up_w = ref.glu_interleave(d["gate_w"], d["up_w"], 0)
             up_b = ref.glu_interleave(d["gate_b"], d["up_b"], 0) if d.get("gate_b") is not None else None
@@ -224,7 +235,8 @@ def _finish(cfg: ModelConfig, plan: ShardPlan, wte, wpe, layers_raw, lnf_w, lnf_
         if n:
             hw[:n] = head_w[lo:lo + n]
         wte_d, head = dev(wte), lin(hw, hb)
-    mw = ModelWeights(wte=wte_d, wpe=dev(wpe), layers=layers, lnf_w=dev(lnf_w), lnf_b=dev(lnf_b), head=head)
+    mw = ModelWeights(wte=wte_d, wpe=dev(wpe), layers=layers, lnf_w=dev(lnf_w), lnf_b=dev(lnf_b), head=head,
+                      rope_interleaved=il)
     if cfg.position == "rope":
         cos, sin = ref.rope_tables(cfg.max_position_embeddings, cfg.rotary_dim, cfg.rope_theta, device)
         mw.cos, mw.sin = cos, sin
@@ -469,7 +481,8 @@ def save_shard(mw: ModelWeights, path: str) -> None:
     # clone: a tied head is a view of the embedding table (safetensors refuses shared storage)
     tensors = {k: v.detach().cpu().contiguous().clone() for k, v in _flat(mw).items()}
     meta = {"format": "llmss_amd-shard-v1", "layers": str(len(mw.layers)),
-            "glu": str(int(mw.layers[0].up.glu)) if mw.layers else "0"}
+            "glu": str(int(mw.layers[0].up.glu)) if mw.layers else "0",
+            "rope_interleaved": str(int(mw.rope_interleaved))}
     if mw.head.w.untyped_storage().data_ptr() == mw.wte.untyped_storage().data_ptr():
         es = mw.wte.element_size()
         meta["tied_head_row"] = str((mw.head.w.data_ptr() - mw.wte.data_ptr()) // (es * mw.wte.shape[1]))
@@ -511,7 +524,8 @@ def load_shard(cfg: ModelConfig, path: str, device, dtype) -> ModelWeights:
         table = torch.zeros(rows, wte.shape[1], dtype=wte.dtype, device=wte.device)
         table[:wte.shape[0]] = wte
         wte, head = table[:wte.shape[0]], Linear(table[lo:lo + head.w.shape[0]], head.b, head.w_scale, head.glu)
-    mw = ModelWeights(wte=wte, wpe=get("wpe"), layers=layers, lnf_w=get("lnf_w"), lnf_b=get("lnf_b"), head=head)
+    mw = ModelWeights(wte=wte, wpe=get("wpe"), layers=layers, lnf_w=get("lnf_w"), lnf_b=get("lnf_b"), head=head,
+                      rope_interleaved=meta.get("rope_interleaved", "0") == "1")
     if cfg.position == "rope":
         mw.cos, mw.sin = ref.rope_tables(cfg.max_position_embeddings, cfg.rotary_dim, cfg.rope_theta, device)
     return mw

@@ -119,13 +119,15 @@ def _time(fn, iters: int) -> float:
 
 
 def tune_shape(M: int, shape: GemmShape, device, weight_budget: int = 600 << 20, iters: int = 16,
-               cands: Optional[Sequence[Tuple[int, int]]] = None) -> Tuple[int, int, float, float]:
-    """Best (nt_hint, split, us, default_us) for one shape."""
+               cands: Optional[Sequence[Tuple[int, int]]] = None,
+               copies: Optional[int] = None) -> Tuple[int, int, float, float]:
+    """Best (nt_hint, split, us, default_us) for one shape (``copies``: weight copies to rotate over instead
+    of enough to exceed ``weight_budget``; 1 = cache-resident weights, a diagnostic)."""
     from . import hip as H
 
     N, K = shape.N, shape.K
     wbytes = N * K * (1 if shape.fp8 else 2)
-    ncopy = max(2, min(64, math.ceil(weight_budget / wbytes)))
+    ncopy = copies or max(2, min(64, math.ceil(weight_budget / wbytes)))
     g = torch.Generator(device=device)
     g.manual_seed(1234)
     x = (torch.randn(M, K, device=device, generator=g) * 0.5).to(torch.bfloat16)

@@ -61,6 +61,27 @@ def rope_tables(max_pos: int, rot: int, theta: float, device=None):
     return ang.cos().float().to(device), ang.sin().float().to(device)
 
 
+def rope_interleave_perm(D: int, rot: int) -> torch.Tensor:
+    """Head-dim order that turns neox RoPE (pairs (j, j + rot/2)) into adjacent pairs (2j, 2j + 1): new
+    dim 2j <- old j, 2j + 1 <- old j + rot/2, dims >= rot unchanged. Applied to the q and k rows of the
+    fused QKV weight at load, attention scores are unchanged (q and k permute alike, V does not) and the
+    rotation becomes the gptj form, which the QKV GEMM epilogue applies in-register for any tile width."""
+    h = rot // 2
+    first = torch.stack([torch.arange(h), torch.arange(h) + h], 1).reshape(-1)
+    return torch.cat([first, torch.arange(rot, D)])
+
+
+def rope_interleave_rows(t: torch.Tensor, nh: int, nkv: int, D: int, rot: int) -> torch.Tensor:
+    """Permute the q and k head rows of a fused [(nh + 2 nkv) * D, ...] QKV weight / bias (see
+    rope_interleave_perm); v rows stay."""
+    perm = rope_interleave_perm(D, rot).to(t.device)
+    nqk = (nh + nkv) * D
+    idx = (torch.arange(nh + nkv, device=t.device)[:, None] * D + perm[None, :]).reshape(-1)
+    out = t.clone()
+    out[:nqk] = t[idx]
+    return out
+
+
 def apply_rope(x: torch.Tensor, positions: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, rot: int,
                style: str) -> torch.Tensor:
     """x [T, H, D] -> rotated copy (first ``rot`` dims), fp32 math, x.dtype out."""

@@ -137,3 +137,29 @@ def test_tied_head_shares_the_embedding_table(tp, rank):
     table = plan.vocab_padded * cfg.hidden_size * 4
     assert w.nbytes() < table + sum(t.numel() * 4 for L in w.layers for t in (L.qkv.w, L.o.w, L.up.w, L.down.w)) * 1.01 \
         + (w.wpe.numel() * 4) + 10 * cfg.hidden_size * 4 * 8
+
+
+def test_rope_interleave_matches_checkpoint_order(ckpts, monkeypatch, tmp_path):
+    """neox RoPE models load with q / k head dims interleaved (gptj-form rotation, fusable into the QKV
+    GEMM epilogue): same logits as the checkpoint order; the shard cache keeps the flag."""
+    from llmss_amd.models.weights import load_shard, save_shard
+
+    d, _ = ckpts["llama"]
+    cfg, w_il = _load(d)
+    monkeypatch.setenv("LLMSS_ROPE_INTERLEAVE", "0")
+    _, w_ck = _load(d)
+    monkeypatch.delenv("LLMSS_ROPE_INTERLEAVE")
+    assert w_il.rope_interleaved and not w_ck.rope_interleaved
+    assert DecoderLM(cfg, w_il).cfg.rope_style == "gptj" and DecoderLM(cfg, w_ck).cfg.rope_style == "neox"
+    ids = torch.randint(0, 100, (13,))
+    outs = []
+    for w in (w_il, w_ck):
+        m = DecoderLM(cfg, w)
+        kv = m.allocate_kv_cache(8, 4)
+        outs.append(m(StepInput("prefill", ids, torch.arange(13), torch.arange(13),
+                                cu_seqlens=torch.tensor([0, 13], dtype=torch.int32), max_seqlen=13,
+                                last_idx=torch.tensor([12])), kv))
+    assert (outs[0] - outs[1]).abs().max() < 1e-4
+    p = str(tmp_path / "shard.safetensors")
+    save_shard(w_il, p)
+    assert load_shard(cfg, p, "cpu", torch.float32).rope_interleaved
