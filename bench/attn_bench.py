@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--heads", default="32:32,32:8")
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--random-pages", action="store_true", help="scatter pages (default: engine-like sequential)")
+    ap.add_argument("--splits", default="", help="context splits to sweep (default: the engine's decode_splits)")
+    ap.add_argument("--unrolls", default="1,2,4,11,12,14")
     a = ap.parse_args()
     dev, bs, D = "cuda", 16, a.D
     for hk in a.heads.split(","):
@@ -36,13 +38,19 @@ def main():
             q = torch.randn(a.B, (nh + 2 * nkv) * D, device=dev).to(torch.bfloat16)
             out = torch.empty(a.B, nh * D, device=dev, dtype=torch.bfloat16)
             res = {"B": a.B, "nh": nh, "nkv": nkv, "ctx": ctx, "MB": round(kv_bytes / 1e6, 1)}
-            for u in (1, 2, 4, 11, 12, 14):
+            for u, sp in [(u, sp) for u in map(int, a.unrolls.split(",")) for sp in
+                          (map(int, a.splits.split(",")) if a.splits else [0])]:
                 H.lib().attn_decode_set_unroll(u)
+                spl = None
+                if sp:
+                    ps = -(-ctx // sp)
+                    ps = -(-ps // bs) * bs
+                    spl = (-(-ctx // ps), ps)
                 it = [0]
 
                 def f():
                     i = it[0] = (it[0] + 1) % ncopy
-                    H.attn_decode(q, kcs[i], vcs[i], bt, cl, nh, nkv, D, D ** -0.5, ctx, out=out)
+                    H.attn_decode(q, kcs[i], vcs[i], bt, cl, nh, nkv, D, D ** -0.5, ctx, out=out, splits=spl)
                 for _ in range(5):
                     f()
                 torch.cuda.synchronize()
@@ -53,8 +61,9 @@ def main():
                 e.record()
                 torch.cuda.synchronize()
                 us = s.elapsed_time(e) * 1e3 / 50
-                res[f"u{u}_us"] = round(us, 2)
-                res[f"u{u}_TBps"] = round(kv_bytes / us / 1e6, 2)
+                tag = f"u{u}" + (f"s{sp}" if sp else "")
+                res[f"{tag}_us"] = round(us, 2)
+                res[f"{tag}_TBps"] = round(kv_bytes / us / 1e6, 2)
             H.lib().attn_decode_set_unroll(0)  # back to the default
             print(res, flush=True)
 

@@ -25,7 +25,7 @@ def _to_gpu(w):
     layers = [LayerWeights(t(L.ln1_w), t(L.ln1_b), t(L.ln2_w), t(L.ln2_b), lin(L.qkv), lin(L.o), lin(L.up), lin(L.down))
               for L in w.layers]
     return ModelWeights(t(w.wte), t(w.wpe), layers, t(w.lnf_w), t(w.lnf_b), lin(w.head),
-                        t(w.cos, True), t(w.sin, True))
+                        t(w.cos, True), t(w.sin, True), rope_interleaved=w.rope_interleaved)
 
 
 @pytest.mark.parametrize("name", ["tiny-gpt2", "tiny-gptj", "tiny-bigcode", "tiny-llama"])
