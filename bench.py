@@ -71,7 +71,8 @@ def main():
     if args.secondary not in ("", "none") and args.simulate_tp <= 1 and args.secondary != args.model:
         # second BASELINE headline config (GPT-2-XL TP=1, 25 heads: no TP split), driver-timed in the same run;
         # with N GPUs every rank serves its own TP=1 replica (data parallel) and the node total is reported
-        torch.cuda.empty_cache()
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
         res["secondary"] = run_config(args, args.secondary, tp, args.batch_per_gpu * world, progress, dp=True)
     if rank == 0:
         print(json.dumps(res))
@@ -85,7 +86,9 @@ def run_config(args, model_name, tp, batch, progress, dp=False):
     from llmss_amd.engine import LLMEngine, SamplingParams, build_model
 
     world = args.gpus
-    dev = torch.device("cuda", torch.cuda.current_device())
+    # GPU: this rank's device. CPU (no GPU): the PyTorch reference path over gloo - a functional rehearsal
+    # of the multi-rank bench (tests/test_bench_dist.py), not a performance number
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     local_batch = batch // world if dp else batch
     model = build_model(model_name, tp if not dp else None, "bf16", dev, fp8=args.fp8, random_init=True)
     max_len = min(model.cfg.max_position_embeddings, max(256, args.prompt_len + args.gen_len))
@@ -110,6 +113,10 @@ def run_config(args, model_name, tp, batch, progress, dp=False):
         reqs = eng.pop_finished()
         return n, [r.metrics() for r in reqs]
 
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
     def barrier():
         if world > 1 and args.simulate_tp <= 1:
             torch.distributed.barrier()
@@ -126,7 +133,7 @@ def run_config(args, model_name, tp, batch, progress, dp=False):
         one_step()
         progress(f"warmup {i}: {time.perf_counter() - t:.3f}s")
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     total, mets = 0, []
     for i in range(args.steps):
@@ -134,7 +141,7 @@ def run_config(args, model_name, tp, batch, progress, dp=False):
         total += n
         mets.extend(m)
         progress(f"step {i}: {n} tokens, {time.perf_counter() - t0:.3f}s elapsed")
-    torch.cuda.synchronize()
+    sync()
     barrier()
     el = time.perf_counter() - t0
     if world > 1 and args.simulate_tp <= 1:  # slowest rank's clock; node total of generated tokens
