@@ -248,11 +248,14 @@ __global__ __launch_bounds__(256, (!FUSED && GB == 1) ? 8 : 1) void attn_decode_
   }
 
   // page ids of this workgroup's context range, staged once in LDS: the token loop then needs no
-  // dependent block-table load (an L2 round trip) in front of every K/V load
+  // dependent block-table load (an L2 round trip) in front of every K/V load. The staged range is the
+  // whole partition's pages (clamped to the table row), not the context's: it does not depend on
+  // ctx_lens, so the table loads issue beside the ctx_lens / q loads instead of one round trip after
+  // them (entries past the sequence's last page are loaded but never used)
   constexpr int kMaxPages = 256;
   __shared__ int s_pages[kMaxPages];
   const int pg0 = start / block_size;
-  const int npg = end > start ? (end - 1) / block_size - pg0 + 1 : 0;
+  const int npg = min((start + part_size - 1) / block_size + 1, bt_stride) - pg0;
   const bool lds_pages = npg <= kMaxPages;
   if (lds_pages) {
     for (int i = threadIdx.x; i < npg; i += blockDim.x) s_pages[i] = bt[pg0 + i];
