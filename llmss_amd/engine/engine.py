@@ -431,7 +431,7 @@ class LLMEngine:
             max_seqlen=int(qlens[nd:].max()), last_idx=d((ends - 1)[smp]),
             block_tables=d(batch.block_table.astype(np.int32)) if kind == "extend" else None,
             ctx_lens=d(ctx.astype(np.int32)) if kind == "extend" else None, max_ctx=self.max_model_len,
-            num_decode=nd, has_prefix=has_prefix)
+            num_decode=nd, has_prefix=has_prefix, cu_host=cu if kind == "prefill" else None)
         reqs = [r for r, f in zip(reqs, smp) if f]
         if not reqs:
             self.model.hidden_states(inp, self.kv)  # prompt chunks only: fill the cache, nothing to sample

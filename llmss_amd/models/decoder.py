@@ -25,7 +25,7 @@ import dataclasses
 
 import os
 from dataclasses import dataclass
-from typing import List, Optional, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 
@@ -65,6 +65,7 @@ class StepInput:
     last_idx: Optional[torch.Tensor] = None  # rows feeding the LM head ([B] int64); None = all rows
     num_decode: int = 0  # extend: leading single-token decode rows
     has_prefix: bool = False  # extend: a prompt chunk continues a cached prefix
+    cu_host: Optional[Sequence[int]] = None  # prefill: cu_seqlens on the host (micro-batch split points)
 
 
 class DecoderLM:
@@ -99,6 +100,10 @@ class DecoderLM:
         # full-batch ones) and each cross-stream hand-off inside a HIP graph ~10 us, more than a
         # modelled 52 us all-reduce hides: 2639 vs 2519 us per step (profiles/r1_tbo/)
         self.tbo_min = int(os.environ.get("LLMSS_TP_DECODE_OVERLAP_MIN", "0"))
+        # prefill steps of at least this many tokens (and >= 2 sequences) run as two micro-batches split at
+        # a sequence boundary, so one half's all-reduces (hundreds of MiB each at TP=8) overlap the other
+        # half's GEMMs and attention; only when collectives cost time (0 = off)
+        self.tbo_prefill_min = int(os.environ.get("LLMSS_TP_PREFILL_OVERLAP_MIN", "8192"))
         # QKV GEMM epilogue with RoPE + paged KV write (one launch instead of two) wherever the autotuner
         # installed a faster plan for it (LLMSS_QKV_EPI=0: always GEMM + rope_cache)
         self.qkv_epi = os.environ.get("LLMSS_QKV_EPI", "1") != "0"
@@ -236,6 +241,27 @@ class DecoderLM:
             return 0
         return (B // 2 + 7) // 8 * 8 if B >= 32 else B // 2
 
+    def prefill_split(self, inp: StepInput) -> Optional[Tuple[int, int]]:
+        """(sequence index j, token row h) splitting a prefill step into sequences [0, j) / [j, B) with about
+        half the tokens each, or None (no split: small step, one sequence, or no communication)."""
+        if inp.kind != "prefill" or inp.cu_host is None or self.tbo_prefill_min <= 0 or not self.tp.comm_active:
+            return None
+        cu = [int(c) for c in inp.cu_host]
+        T = cu[-1]
+        if len(cu) < 3 or T < self.tbo_prefill_min:
+            return None
+        j = min(range(1, len(cu) - 1), key=lambda i: abs(2 * cu[i] - T))
+        return j, cu[j]
+
+    def _sub_prefill(self, inp: StepInput, j: int, h: int) -> Tuple[StepInput, StepInput]:
+        cu = inp.cu_seqlens
+        lens = [int(b) - int(a) for a, b in zip(inp.cu_host[:-1], inp.cu_host[1:])]
+
+        def part(r0, r1, c, ls):
+            return StepInput("prefill", inp.input_ids[r0:r1], inp.positions[r0:r1], inp.slots[r0:r1], cu_seqlens=c,
+                             max_seqlen=max(ls))
+        return part(0, h, cu[:j + 1], lens[:j]), part(h, int(inp.cu_host[-1]), cu[j:] - h, lens[j:])
+
     def _sub_step(self, inp: StepInput, r0: int, r1: int, block_size: int) -> StepInput:
         splits = inp.decode_splits
         if splits is not None and inp.input_ids.is_cuda:
@@ -244,8 +270,9 @@ class DecoderLM:
                          block_tables=inp.block_tables[r0:r1], ctx_lens=inp.ctx_lens[r0:r1], max_ctx=inp.max_ctx,
                          decode_splits=splits)
 
-    def _hidden_states_overlap(self, inp: StepInput, kv_caches, h: int) -> torch.Tensor:
-        """Decode step as two micro-batches (rows [0, h) and [h, B)) interleaved layer by layer.
+    def _hidden_states_overlap(self, inp: StepInput, kv_caches, h: int, subs=None) -> torch.Tensor:
+        """Decode step (or prefill step: ``subs`` from _sub_prefill) as two micro-batches (rows [0, h) and
+        [h, B)) interleaved layer by layer.
 
         Compute-stream order per layer: A.attn, B.attn, A.mlp, B.mlp. Each block's all-reduce goes
         to the high-priority comm stream and the compute stream waits for it (event) only right
@@ -258,7 +285,8 @@ class DecoderLM:
         eps, rms = cfg.norm_eps, self.rms
         B = inp.input_ids.shape[0]
         bs = kv_caches[0][0].shape[2]
-        subs = (self._sub_step(inp, 0, h, bs), self._sub_step(inp, h, B, bs))
+        if subs is None:
+            subs = (self._sub_step(inp, 0, h, bs), self._sub_step(inp, h, B, bs))
         rows = ((0, h), (h, B))
         on_gpu = inp.input_ids.is_cuda
         cur = torch.cuda.current_stream() if on_gpu else None
@@ -320,6 +348,10 @@ class DecoderLM:
             h = self.overlap_split(inp.input_ids.shape[0])
             if h:
                 return self._hidden_states_overlap(inp, kv_caches, h)
+        elif inp.kind == "prefill":
+            sp = self.prefill_split(inp)
+            if sp is not None:
+                return self._hidden_states_overlap(inp, kv_caches, sp[1], subs=self._sub_prefill(inp, *sp))
         cfg, w = self.cfg, self.w
         eps, rms = cfg.norm_eps, self.rms
         x = ops.embed(inp.input_ids, w.wte, inp.positions if w.wpe is not None else None, w.wpe)

@@ -31,6 +31,9 @@ def _worker(rank, world, port, ckpt, prompts, q, env=None):
     m = build_model(ckpt, tp, "fp32", "cpu")
     if "LLMSS_TP_DECODE_OVERLAP_MIN" in (env or {}):
         assert m.overlap_split(3) == 1  # the 3-sequence decode steps really take the micro-batch path
+    if "LLMSS_TP_PREFILL_OVERLAP_MIN" in (env or {}):  # the 3-prompt prefill splits at a sequence boundary
+        from llmss_amd.models.decoder import StepInput
+        assert m.prefill_split(StepInput("prefill", *(torch.zeros(21),) * 3, cu_host=[0, 5, 12, 21])) == (2, 12)
     eng = LLMEngine(m, max_num_seqs=4, block_size=4, num_blocks=64, check_tokens=True)
     greedy = eng.generate(prompts, SamplingParams(max_new_tokens=8, is_greedy=True, ignore_eos=True))
     sampled = eng.generate(prompts, [SamplingParams(max_new_tokens=8, temperature=0.9, top_k=20, top_p=0.9, seed=5 + i,
@@ -59,13 +62,15 @@ def _run(world, ckpt, prompts, env=None):
 # LLMSS_TP_DECODE_OVERLAP_MIN: decode steps as two interleaved micro-batches (the 3-sequence batch splits 1 + 2)
 _ROWS = {"LLMSS_TP_OVERLAP_ROWS": "4"}
 _TBO = {"LLMSS_TP_DECODE_OVERLAP_MIN": "2"}
+_PTBO = {"LLMSS_TP_PREFILL_OVERLAP_MIN": "2"}  # prefill steps as two micro-batches split at a sequence boundary
 
 
 @pytest.mark.parametrize("name,world,overlap", [("llama", 2, None), ("gptj", 2, None), ("bigcode", 4, None),
                                                 ("gpt2", 2, None), ("bigcode_mha", 2, None), ("llama", 2, _ROWS),
                                                 ("gptj", 2, {"LLMSS_TP_OVERLAP_ROWS": "5"}), ("llama", 2, _TBO),
                                                 ("llama", 2, {"LLMSS_TP_BUCKET_BYTES": "64"}),
-                                                ("gptj", 2, _TBO), ("bigcode", 4, _TBO)])
+                                                ("gptj", 2, _TBO), ("bigcode", 4, _TBO), ("llama", 2, _PTBO),
+                                                ("gptj", 2, _PTBO), ("bigcode", 4, {**_PTBO, **_TBO})])
 def test_tp_matches_single(tmp_path, name, world, overlap):
     d = str(tmp_path / name)
     save_hf_model(name, d, vocab=101)  # 101 % world != 0 -> exercises the padded vocab-parallel head
