@@ -252,6 +252,35 @@ def test_decode_microbatch_overlap(fam):
     assert err < 5e-2, err
 
 
+@pytest.mark.parametrize("fam", ["tiny-llama", "tiny-gptj"])
+def test_prefill_microbatch_overlap(fam):
+    """Prefill split into two micro-batches at a sequence boundary (each half's RCCL all-reduces on the comm
+    stream while the other half computes) == the single prefill step: hidden states and the paged KV."""
+    tp = _one_member_tp()
+    par = fam == "tiny-gptj"
+    cfg = get_preset(fam, hidden_size=256, num_heads=4, head_dim=64, rotary_dim=16 if par else 64,
+                     intermediate_size=512, max_position_embeddings=256, **({} if par else {"num_kv_heads": 2}))
+    m = DecoderLM(cfg, random_weights(cfg, 2, 0, device="cuda", dtype=torch.bfloat16, seed=6, std=0.05), tp)
+    bs, per = 16, 4
+    lens = [37, 5, 64, 18, 51, 9]
+    ids = torch.randint(0, cfg.vocab_size, (sum(lens),), device="cuda")
+    pos = torch.cat([torch.arange(n) for n in lens]).cuda()
+    slots = torch.cat([torch.arange(n) + i * per * bs for i, n in enumerate(lens)]).cuda()
+    cu_host = [0] + [int(c) for c in torch.tensor(lens).cumsum(0)]
+    inp = StepInput("prefill", ids, pos, slots, cu_seqlens=torch.tensor(cu_host, dtype=torch.int32, device="cuda"),
+                    max_seqlen=max(lens), cu_host=cu_host)
+    kv_a, kv_b = m.allocate_kv_cache(len(lens) * per, bs), m.allocate_kv_cache(len(lens) * per, bs)
+    m.tbo_prefill_min = 0
+    ref = m.hidden_states(inp, kv_a)
+    m.tbo_prefill_min = 16
+    assert m.prefill_split(inp) == (3, 106)
+    out = m.hidden_states(inp, kv_b)
+    torch.cuda.synchronize()
+    assert (out.float() - ref.float()).abs().max().item() < 5e-2
+    for (ka, va), (kb, vb) in zip(kv_a, kv_b):  # half-batch GEMMs may pick other split-K plans: bf16 tolerance
+        assert (ka.float() - kb.float()).abs().max().item() < 5e-2 and (va.float() - vb.float()).abs().max() < 5e-2
+
+
 def test_decode_microbatch_overlap_in_graphs():
     """The micro-batch decode schedule (two streams, event joins, RCCL) captures into HIP graphs and
     replays exactly like eager; also with the modelled-comm fake group used by bench --sim-comm."""
