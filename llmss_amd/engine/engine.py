@@ -601,6 +601,16 @@ class LLMEngine:
                         self._decode_forward(b, buf, dist=d)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        # settle the caching allocator's pending cross-stream events (freed side-stream blocks) outside the
+        # capture, so no allocation during capture queries an event
+        torch.cuda.empty_cache()
+        if self.tp.is_real and not self.tp.host_staged:
+            # let the RCCL process group's watchdog retire the warm-up collectives above before capturing:
+            # their end events were recorded on the communicator's stream, which the captured collectives
+            # pull into the capture, and a watchdog query of such an event then fails
+            # ("operation not permitted on an event last recorded in a capturing stream") and aborts the
+            # process. The watchdog scans every 100 ms; with nothing in flight its list is empty after this.
+            time.sleep(0.5)
         # thread-local capture: the RCCL communicator's watchdog thread keeps querying the events of earlier
         # collectives; under the default global capture mode such a query from another thread aborts the
         # process ("operation not permitted when stream is capturing")

@@ -229,7 +229,10 @@ class DecoderLM:
             comm.wait_stream(cur)  # chunk r's GEMM done
             with torch.cuda.stream(comm):
                 self.tp.all_reduce(y)
-            y.record_stream(comm)
+            # no record_stream: `outs` holds every chunk until the compute stream has waited for the comm
+            # stream (below), so no chunk's memory is reused while its all-reduce runs - and no allocator
+            # event is left pending on the comm stream (an allocation inside a later graph capture would
+            # otherwise query it from the capturing thread)
             outs.append(y)
         cur.wait_stream(comm)
         return torch.cat(outs)
@@ -303,8 +306,8 @@ class DecoderLM:
                 self.tp.all_reduce(t)
                 ev = torch.cuda.Event()
                 ev.record(comm)
-            if diag != "norecord":
-                t.record_stream(comm)
+            # no record_stream (see _reduce_rows): the compute stream waits for `ev` before it reads t or
+            # drops its last reference (the next layer's ready(), or the final joins)
             return ev
 
         def ready(ev):
