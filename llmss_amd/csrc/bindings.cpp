@@ -28,7 +28,7 @@ void launch_attn_prefill(const void* qkv, int64_t row_stride, int T, const void*
 void attn_prefill_set_version(int v);
 void gemm_big_set_group(int g);
 void launch_cand_topk(const void* logits, int64_t ld, int B, int vl, int lo, int V, const void* temperature,
-                      const void* top_k, int K, int KC, void* pack, int64_t ldp, hipStream_t st);
+                      const void* top_k, int K, int KC, void* pack, int64_t ldp, hipStream_t st, int shards);
 void launch_sample_cand(const void* pack, int64_t ldp, int B, int groups, int KC, const void* temperature,
                         const void* top_k, const void* top_p, const void* seeds, void* out, void* out2, hipStream_t st);
 void launch_ce_loss(const void* logits, int64_t ld, bool fp32, const void* labels, int T, int V, void* loss,
@@ -116,9 +116,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_prefill_set_version", &attn_prefill_set_version);
   m.def("gemm_big_set_group", &gemm_big_set_group);
   m.def("cand_topk", [](uintptr_t lg, int64_t ld, int B, int vl, int lo, int V, uintptr_t temp, uintptr_t topk, int K,
-                        int KC, uintptr_t pack, int64_t ldp, uintptr_t st) {
-    launch_cand_topk(CP(lg), ld, B, vl, lo, V, CP(temp), CP(topk), K, KC, P(pack), ldp, S(st));
-  });
+                        int KC, uintptr_t pack, int64_t ldp, uintptr_t st, int shards) {
+    launch_cand_topk(CP(lg), ld, B, vl, lo, V, CP(temp), CP(topk), K, KC, P(pack), ldp, S(st), shards);
+  }, pybind11::arg("lg"), pybind11::arg("ld"), pybind11::arg("B"), pybind11::arg("vl"), pybind11::arg("lo"),
+     pybind11::arg("V"), pybind11::arg("temp"), pybind11::arg("topk"), pybind11::arg("K"), pybind11::arg("KC"),
+     pybind11::arg("pack"), pybind11::arg("ldp"), pybind11::arg("st"), pybind11::arg("shards") = 1);
   m.def("sample_cand", [](uintptr_t pack, int64_t ldp, int B, int groups, int KC, uintptr_t temp, uintptr_t topk,
                           uintptr_t topp, uintptr_t seeds, uintptr_t out, uintptr_t out2, uintptr_t st) {
     launch_sample_cand(CP(pack), ldp, B, groups, KC, CP(temp), CP(topk), CP(topp), CP(seeds), P(out), P(out2), S(st));

@@ -494,11 +494,15 @@ __global__ __launch_bounds__(CAND_THREADS) void cand_topk_kernel(const bf16_t* _
   __shared__ unsigned above;
   __shared__ int nout;
   const int b = blockIdx.x, t = threadIdx.x;
+  // blockIdx.y = vocab shard of this launch (one GPU's [B, V] logits cut into gridDim.y shards of vl columns,
+  // packed shard-major like the all-gathered packs of a vocab-parallel group); 0 for a TP rank's own shard
+  lo += blockIdx.y * vl;
+  pack += blockIdx.y * 2 * KC;
   const float temp = temperature ? temperature[b] : 0.f;
   const int k = top_k ? top_k[b] : 0;
   const bool greedy = !(temp > 0.f) || k == 1;
   const float scale = greedy ? 1.f : 1.f / temp;
-  const bf16_t* row = logits + (int64_t)b * ld;
+  const bf16_t* row = logits + (int64_t)b * ld + (int64_t)blockIdx.y * vl;
   float x[EPT];
   unsigned key[EPT];
 #pragma unroll
@@ -665,13 +669,14 @@ __global__ __launch_bounds__(256) void sample_cand_kernel(const float* __restric
 }
 
 void launch_cand_topk(const void* logits, int64_t ld, int B, int vl, int lo, int V, const void* temperature,
-                      const void* top_k, int K, int KC, void* pack, int64_t ldp, hipStream_t st) {
+                      const void* top_k, int K, int KC, void* pack, int64_t ldp, hipStream_t st, int shards) {
   if (B == 0) return;
   if (K < 1 || KC < K) throw std::runtime_error("cand_topk: need 1 <= K <= KC");
+  if (shards < 1 || (int64_t)shards * 2 * KC > ldp) throw std::runtime_error("cand_topk: pack row too narrow");
   const int ept = (vl + CAND_THREADS - 1) / CAND_THREADS;
 #define CT(E_)                                                                                                    \
-  cand_topk_kernel<E_><<<B, CAND_THREADS, 0, st>>>((const bf16_t*)logits, ld, vl, lo, V, (const float*)temperature, \
-                                                   (const int*)top_k, K, KC, (float*)pack, ldp)
+  cand_topk_kernel<E_><<<dim3(B, shards), CAND_THREADS, 0, st>>>((const bf16_t*)logits, ld, vl, lo, V,            \
+                                                   (const float*)temperature, (const int*)top_k, K, KC, (float*)pack, ldp)
   if (ept <= 4) CT(4);
   else if (ept <= 8) CT(8);
   else if (ept <= 16) CT(16);

@@ -125,12 +125,13 @@ def cand_ok(temperature, top_k) -> bool:
     return bool(np.all(~(t > 0) | (k == 1) | ((k >= 1) & (k <= CAND_K))))
 
 
-def sample_distributed(local, tp, lo, V, temperature, top_k, top_p, seeds, out=None):
+def sample_distributed(local, tp, lo, V, temperature, top_k, top_p, seeds, out=None, shards=1):
     """Vocab-parallel sampling without gathering logits: per-rank candidates -> all-gather -> select.
-    ``local`` = this rank's [B, V/tp] logit shard whose first column is global token ``lo``."""
+    ``local`` = this rank's [B, V/tp] logit shard whose first column is global token ``lo``; ``shards`` > 1
+    additionally cuts it into column shards inside one launch (a single GPU's full vocabulary)."""
     if local.is_cuda:
         h = _hip()
-        pack = h.cand_topk(local, lo, V, temperature, top_k)
+        pack = h.cand_topk(local, lo, V, temperature, top_k, shards=shards)
         allp = tp.all_gather_last_dim(pack)
         return h.sample_cand(allp, h.CAND_KC, temperature, top_k, top_p, seeds, out=out)
     pack = ref.cand_topk(local, lo, V, temperature, top_k, CAND_K, CAND_KC)

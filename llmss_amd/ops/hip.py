@@ -559,18 +559,25 @@ CAND_KC = 128  # candidate slots per rank and row (>= CAND_K: ties at the K-th v
 CAND_MAX_SHARD = 16384  # widest vocab shard the candidate kernel takes
 
 
-def cand_topk(local, lo, V, temperature, top_k, K=CAND_K, KC=CAND_KC, out=None):
+def cand_topk(local, lo, V, temperature, top_k, K=CAND_K, KC=CAND_KC, out=None, shards=1):
     """Per-rank candidates of a vocab-parallel logit shard: [B, 2*KC] fp32 (KC scaled values, then KC
-    global token ids as int32 bits)."""
+    global token ids as int32 bits). ``shards`` > 1: the row is cut into that many column shards sampled by
+    one launch (grid.y), packed shard-major [B, shards * 2*KC] - the layout of gathered per-rank packs, so a
+    single GPU samples its full vocabulary through the same two short kernels instead of one long
+    row-per-workgroup pass."""
     _bf16_rows(local, "local logits")
-    B, vl = local.shape
-    _check(vl <= CAND_MAX_SHARD, "vocab shard too wide for the candidate sampler")
+    B, width = local.shape
+    vl = -(-width // shards)
+    _check(shards >= 1 and vl <= CAND_MAX_SHARD, "vocab shard too wide for the candidate sampler")
     for t, dt, nm in ((temperature, torch.float32, "temperature"), (top_k, torch.int32, "top_k")):
         _check(t.dtype == dt and t.numel() >= B and t.is_contiguous() and t.is_cuda, f"{nm} must be {dt}")
-    pack = out if out is not None else torch.empty(B, 2 * KC, dtype=torch.float32, device=local.device)
-    _check(pack.shape == (B, 2 * KC) and pack.is_contiguous() and pack.dtype == torch.float32, "candidate pack")
+    pack = out if out is not None else torch.empty(B, shards * 2 * KC, dtype=torch.float32, device=local.device)
+    _check(pack.shape == (B, shards * 2 * KC) and pack.is_contiguous() and pack.dtype == torch.float32,
+           "candidate pack")
+    # columns past `width` in the last shard are masked by the kernel's lo + j < V bound only if V <= width
+    _check(V <= width or shards == 1, "sharded candidates need the vocabulary inside the logits row")
     lib().cand_topk(local.data_ptr(), local.stride(0), B, vl, int(lo), int(V), temperature.data_ptr(),
-                    top_k.data_ptr(), int(K), int(KC), pack.data_ptr(), pack.stride(0), _stream())
+                    top_k.data_ptr(), int(K), int(KC), pack.data_ptr(), pack.stride(0), _stream(), int(shards))
     return pack
 
 

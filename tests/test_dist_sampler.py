@@ -73,3 +73,23 @@ def test_gpu_candidates_equal_v3_sampler(tp, V):
     p0 = packs[0].cpu()
     ids = p0[:, 128:].view(torch.int32)
     assert bool(((ids >= 0) & (ids < vl) | (ids == 0x7fffffff)).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards,V,Vp", [(8, 32000, 32000), (8, 50257, 50304), (4, 50257, 50304), (3, 1000, 1008)])
+def test_gpu_sharded_candidates_one_gpu(shards, V, Vp):
+    """TP=1 engines sample through the candidate kernels over column shards of the full row (one launch,
+    grid.y = shard): the same tokens as the full-row v3 sampler, including padded columns past V."""
+    from llmss_amd.ops import hip as H
+
+    dev = torch.device("cuda")
+    B = 64
+    x = torch.full((B, Vp), 7.0, dtype=torch.bfloat16, device=dev)  # padding columns would win if not masked
+    x[:, :V] = _rows(B, V, V + shards).to(torch.bfloat16).to(dev)
+    temp, topk, topp, seeds = (torch.from_numpy(a).to(dev) for a in _params(B, shards))
+    full = H.sample(x, temp, topk, topp, seeds, vocab=V)
+    pack = H.cand_topk(x, 0, V, temp, topk, shards=shards)
+    assert pack.shape == (B, shards * 2 * H.CAND_KC)
+    got = H.sample_cand(pack, H.CAND_KC, temp, topk, topp, seeds)
+    assert got.tolist() == full.tolist()
+    assert int(got.max()) < V
