@@ -566,6 +566,12 @@ __global__ __launch_bounds__(256) void sample_cand_kernel(const float* __restric
   __shared__ int id[SCAND_MAX];
   __shared__ float sv[SCAND_MAX];  // sorted (value desc, index asc)
   __shared__ int sid[SCAND_MAX];
+  __shared__ float cv[SCAND_MAX];  // candidates >= the top-k boundary (unordered)
+  __shared__ int cid[SCAND_MAX];
+  __shared__ unsigned hist[256];
+  __shared__ unsigned wsum[4];
+  __shared__ int digit_s, nkeep;
+  __shared__ unsigned above_s;
   __shared__ float red[8];
   __shared__ int redi[8];
   __shared__ float thr_s;
@@ -591,22 +597,59 @@ __global__ __launch_bounds__(256) void sample_cand_kernel(const float* __restric
     float mx = -INFINITY;
     for (int i = t; i < N; i += 256) mx = fmaxf(mx, v[i]);
     mx = block_max(mx, red);
-    // exact ranks (value desc, global index asc) -> sorted copy
+    // Only the candidates >= the k-th largest value take part in the top-k / top-p decision. Ranking every
+    // candidate against every other (N^2 LDS reads, N = tp * KC = 1024 at TP=8) cost ~340 us per call; instead
+    // (1) the k-th largest key by 4 passes of 8-bit radix select (exact counts, as cand_topk), (2) compact
+    // the candidates at or above it (k plus ties: ~64), (3) exact ranks inside that small set.
+    const int n = nvalid;
+    const unsigned kk = (k > 0 && k <= n) ? (unsigned)k : 0u;  // 0: keep every real candidate
+    unsigned kth = 0u;
+    if (kk) {
+      unsigned prefix = 0u, mask = 0u, target = kk;
+      for (int shift = 24; shift >= 0; shift -= 8) {
+        hist[t] = 0u;  // 256 threads, 256 bins
+        if (t == 0) { digit_s = 0; above_s = 0u; }
+        __syncthreads();
+        for (int i = t; i < N; i += 256) {
+          const unsigned key = v[i] > -INFINITY ? fkey(v[i]) : 0u;
+          if (key != 0u && (key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
+        }
+        __syncthreads();
+        cand_find_digit(hist, target, &digit_s, &above_s, wsum);
+        const int d = digit_s;
+        const unsigned a = above_s;
+        __syncthreads();
+        target -= a;
+        prefix |= (unsigned)d << shift;
+        mask |= 255u << shift;
+      }
+      kth = prefix;
+    }
+    if (t == 0) nkeep = 0;
+    __syncthreads();
     for (int i = t; i < N; i += 256) {
-      const float a = v[i];
-      const int ai = id[i];
-      if (!(a > -INFINITY)) continue;
+      if (!(v[i] > -INFINITY) || fkey(v[i]) < kth) continue;
+      const int s = atomicAdd(&nkeep, 1);
+      cv[s] = v[i];
+      cid[s] = id[i];
+    }
+    __syncthreads();
+    const int m = nkeep;  // every candidate >= the k-th largest value (ties included), unordered
+    // exact ranks (value desc, global index asc) inside the kept set -> sorted copy
+    for (int i = t; i < m; i += 256) {
+      const float a = cv[i];
+      const int ai = cid[i];
       int r = 0;
-      for (int j = 0; j < N; ++j) {
-        const float c = v[j];
-        r += (c > a || (c == a && id[j] < ai)) ? 1 : 0;
+      for (int j = 0; j < m; ++j) {
+        const float c = cv[j];
+        r += (c > a || (c == a && cid[j] < ai)) ? 1 : 0;
       }
       sv[r] = a;
       sid[r] = ai;
     }
     __syncthreads();
     if (t == 0) {
-      const int n = nvalid;  // sv[0, n) holds every real candidate in order
+      const int n = m;  // sv[0, m) holds every candidate >= the top-k boundary, in order
       float th = -INFINITY;
       if (k > 0 && k <= n) th = sv[k - 1];  // top-k boundary value (ties at it are kept)
       if (p < 1.f) {
