@@ -62,6 +62,7 @@ def main():
             raise SystemExit("--simulate-tp runs in a single process")
         sim = tuple(float(v) for v in args.sim_comm.split(",")) if args.sim_comm else None
         tp = TPGroup(0, args.simulate_tp, fake=True, sim_comm=sim)
+        tp.replicate_gather = True  # the gathered candidates / logits have their TP=N width
 
     def progress(msg):
         if rank == 0:

@@ -48,7 +48,9 @@ def main():
     def progress(msg):
         print(f"[probe] {msg}", file=sys.stderr, flush=True)
 
-    for name, tp in (("fake group (no collectives)", TPGroup(0, a.tp, fake=True)),
+    fake = TPGroup(0, a.tp, fake=True)
+    fake.replicate_gather = True  # same gathered widths as the RCCL group below
+    for name, tp in (("fake group (no collectives)", fake),
                      ("one-member RCCL group", OneMemberTP(0, a.tp, group=dist.group.WORLD))):
         r = bench.run_config(args, a.model, tp, 64 * a.tp, progress)
         print(json.dumps({"group": name, "tokens_per_s": r["value"], "ms_per_step": r["ms_per_step"],

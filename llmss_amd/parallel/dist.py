@@ -41,6 +41,10 @@ class TPGroup:
         # then occupies the issuing stream for latency + bytes/bandwidth (a spin kernel on one
         # workgroup), so the comm/compute overlap of a TP=N schedule can be measured on one GPU.
         self.sim_comm = sim_comm if fake and size > 1 else None
+        # fake groups standing in for a TP=N rank (bench --simulate-tp): all-gathers return N copies of the
+        # local shard, so what consumes them (the candidate sampler's N groups, a full-width logits row)
+        # costs what it costs at TP=N. Off for DEBUG=1 (the reference FakeGroup returns the local tensor).
+        self.replicate_gather = False
         self._cycles_per_us = None
         # data parallelism (initialize_distributed(dp=...)): this group is replica `replica` of `dp`
         self.replica, self.dp, self.global_rank, self.ctrl_group = 0, 1, rank, None
@@ -113,6 +117,8 @@ class TPGroup:
         if not self.is_real:
             if self.sim_comm is not None and t.is_cuda:
                 self._sim_wait(self.size * t.numel() * t.element_size())
+            if self.replicate_gather and self.size > 1:
+                return torch.cat([t] * self.size, -1)
             return t
         t = t.contiguous()
         if t.is_cuda and self.host_staged:

@@ -45,7 +45,7 @@ def test_bench_two_ranks_gloo():
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["config"]["parallelism"] == "tp2"
     assert d["config"]["global_batch"] == 4
     # TP: both ranks generate the same 4 x 4 tokens per step, counted once
-    assert abs(d["value"] * d["ms_per_step"] / 1e3 - 16) < 1e-3
+    assert abs(d["value"] * d["ms_per_step"] / 1e3 - 16) < 0.05  # value and ms_per_step are rounded
     s = d["secondary"]
     assert s["config"]["parallelism"] == "dp2xtp1" and s["config"]["global_batch"] == 4
-    assert abs(s["value"] * s["ms_per_step"] / 1e3 - 16) < 1e-3  # 2 replicas x 2 requests x 4 tokens
+    assert abs(s["value"] * s["ms_per_step"] / 1e3 - 16) < 0.05  # 2 replicas x 2 requests x 4 tokens
