@@ -150,13 +150,12 @@ class EngineServicer:
             ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
         h = self.driver.submit(self._prompt_ids(req), params, deadline_s=ctx.time_remaining())
         ctx.add_callback(lambda: (not h.done.is_set()) and self.driver.abort(h.rid))
-        ids, prev = [], ""
+        from ..utils.tokenizer import StreamDecoder
+
+        dec = StreamDecoder(self.tok)  # one short-window decode per token, not the whole prefix again
         for t in h.stream():
-            ids.append(t)
-            text = self.tok.decode(ids)
-            yield Token(token_id=t, text=text[len(prev):], finished=False)
-            prev = text
-        yield Token(token_id=-1, text="", finished=True, finish_reason=h.finish_reason)
+            yield Token(token_id=t, text=dec.push(t), finished=False)
+        yield Token(token_id=-1, text=dec.flush(), finished=True, finish_reason=h.finish_reason)
 
     def Stats(self, req, ctx):
         st = dict(self.driver.engine.stats)

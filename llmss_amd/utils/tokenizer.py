@@ -52,3 +52,33 @@ def encode(tok, text: str) -> List[int]:
     if isinstance(tok, ByteTokenizer):
         return tok.encode(text)
     return tok(text, return_attention_mask=False)["input_ids"]
+
+
+class StreamDecoder:
+    """Incremental detokenisation of a token stream: each new token costs one decode of a short window
+    (the tokens since the last emitted text boundary, a few ids) instead of decoding the whole sequence
+    again - O(n) per request instead of O(n^2). Text is held back while the window ends inside a
+    multi-byte / multi-token character (decode yields U+FFFD), so the concatenated pieces equal
+    ``tok.decode(all_ids)``."""
+
+    def __init__(self, tok):
+        self.tok = tok
+        self.ids: List[int] = []
+        self.prefix = 0  # window start (ids before it are already emitted text)
+        self.read = 0  # ids [prefix, read) decode to text that has been emitted
+
+    def push(self, token_id: int) -> str:
+        self.ids.append(int(token_id))
+        emitted = self.tok.decode(self.ids[self.prefix:self.read])
+        full = self.tok.decode(self.ids[self.prefix:])
+        if len(full) > len(emitted) and not full.endswith("\ufffd"):
+            self.prefix, self.read = self.read, len(self.ids)
+            return full[len(emitted):]
+        return ""
+
+    def flush(self) -> str:
+        """Whatever is still held back (a stream that ends inside a character)."""
+        emitted = self.tok.decode(self.ids[self.prefix:self.read])
+        full = self.tok.decode(self.ids[self.prefix:])
+        self.prefix = self.read = len(self.ids)
+        return full[len(emitted):]

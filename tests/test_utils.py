@@ -80,3 +80,22 @@ def test_tokenizer_fallback_is_explicit(tmp_path):
     (broken / "tokenizer.json").write_text("{not json")
     with pytest.raises(RuntimeError):
         load_tokenizer(str(broken))
+
+
+def test_stream_decoder_matches_full_decode():
+    """Incremental detokenisation (gRPC GenerateStream): the streamed pieces concatenate to the full decode,
+    with multi-byte characters split across tokens held back until complete."""
+    import random
+
+    from llmss_amd.utils.tokenizer import ByteTokenizer, StreamDecoder
+
+    tok = ByteTokenizer()
+    rnd = random.Random(0)
+    alphabet = "ab é ö — ✓ 你好 🙂"
+    for _ in range(20):
+        text = "".join(rnd.choice(alphabet) for _ in range(rnd.randint(1, 40)))
+        ids = tok.encode(text)
+        d = StreamDecoder(tok)
+        pieces = [d.push(i) for i in ids]
+        assert "".join(pieces) + d.flush() == tok.decode(ids)
+        assert all("�" not in p for p in pieces)
