@@ -22,7 +22,6 @@ followed by an all-gather of [B, V/tp] logits.
 from __future__ import annotations
 
 import dataclasses
-
 import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
