@@ -7,6 +7,9 @@ usage: python bench/kernel_one.py decode|prefill|sample|add_norm|rope [--iters 1
   sample   temperature / top-k / top-p sampler, B=64 rows of a 32000 vocabulary
   add_norm fused residual add + RMSNorm, 64 x 4096
   rope     RoPE + paged KV write, 64 tokens, 32 heads x 128
+  gemm_big prefill GEMM (the 256 x 256 8-wave kernel), Llama-2-7B QKV at 8192 prompt tokens: 8192 x 12288 x 4096
+  cand     vocab-parallel candidate sampler at TP=8 rows: cand_topk on a [512, 4000] shard + sample_cand over
+           8 gathered groups
 """
 import argparse
 import os
@@ -78,6 +81,25 @@ def main():
 
         def f(i):
             H.rope_cache(qkv, pos, cos, sin, kc, vc, slots, nh, nkv, D, D, "neox")
+    elif a.kernel == "gemm_big":
+        M, N, K = 8192, 12288, 4096
+        x = (torch.randn(M, K, device=dev) * 0.5).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=dev) * K ** -0.5).to(torch.bfloat16)
+        y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+
+        def f(i):
+            H.linear(x, w, None, out=y)
+    elif a.kernel == "cand":
+        B, vl, tp = 512, 4000, 8
+        lg = (torch.randn(B, vl, device=dev) * 3).to(torch.bfloat16)
+        t = torch.ones(B, device=dev)
+        k = torch.full((B,), 50, dtype=torch.int32, device=dev)
+        p = torch.full((B,), 0.95, device=dev)
+        sd = torch.arange(B, dtype=torch.int64, device=dev)
+
+        def f(i):
+            pack = H.cand_topk(lg, 0, vl * tp, t, k)
+            H.sample_cand(torch.cat([pack] * tp, -1), H.CAND_KC, t, k, p, sd)
     else:
         raise SystemExit(f"unknown kernel {a.kernel}")
     for i in range(a.iters):
