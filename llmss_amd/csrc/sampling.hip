@@ -585,12 +585,17 @@ __global__ __launch_bounds__(256) void sample_cand_kernel(const float* __restric
   if (t == 0) nvalid = 0;
   __syncthreads();
   const float* row = pack + (int64_t)b * ldp;  // [groups][KC values | KC indices]
+  int myvalid = 0;
   for (int i = t; i < N; i += 256) {
     const int g = i / KC, s = i - g * KC;
     v[i] = row[(int64_t)g * 2 * KC + s];
     id[i] = reinterpret_cast<const int*>(row)[(int64_t)g * 2 * KC + KC + s];
-    if (v[i] > -INFINITY) atomicAdd(&nvalid, 1);
+    myvalid += v[i] > -INFINITY ? 1 : 0;
   }
+  // one LDS atomic per wave (a per-candidate atomic on one address serialised up to tp * KC updates per row)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) myvalid += __shfl_xor(myvalid, o, 64);
+  if ((t & 63) == 0) atomicAdd(&nvalid, myvalid);
   __syncthreads();
   float thr = -INFINITY;
   if (!greedy) {
