@@ -10,14 +10,24 @@ batching scheduler, paged KV cache, HIP-graph decode, on-device sampling with th
 default temperature=1.0 / top_p=0.95 / top_k=50). Weak scaling: the global batch is
 ``--batch-per-gpu * N``. ``value`` = total generated tokens / wall time over all ranks (max).
 
-Launch: ``python bench.py`` (N=1) or ``torchrun --nproc-per-node N bench.py --gpus N``.
+Launch: ``python bench.py`` (N=1), ``python bench.py --gpus N`` (this process becomes a GPU-free
+launcher: it starts N rank processes of itself with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set,
+forwards rank 0's JSON line, and on any rank failure or the ``--timeout`` kills the others and exits
+non-zero naming the rank), or ``torchrun --nproc-per-node N bench.py --gpus N`` (each rank directly).
+Reference launch recipe: ``torchrun --nproc_per_node 4 consumer_server.py``
+(``poc-server/producer-consumer/README.md:29-36``), ``initialize_torch_distributed`` (``dist.py:40-77``).
 """
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -50,7 +60,12 @@ def main():
     ap.add_argument("--sim-comm", default="",
                     help="with --simulate-tp: model each all-reduce / all-gather as LAT_US,GBPS (latency + bytes / "
                          "algorithmic bandwidth, a spin kernel on the collective's stream) to measure comm overlap")
+    ap.add_argument("--timeout", type=float, default=float(os.environ.get("LLMSS_BENCH_TIMEOUT_S", "2400")),
+                    help="launcher mode: kill every rank and exit 124 after this many seconds")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args))
 
     from llmss_amd.parallel.dist import TPGroup, initialize_distributed
 
@@ -68,7 +83,13 @@ def main():
         if rank == 0:
             print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
+    if world > 1 and args.simulate_tp <= 1 and torch.cuda.is_available() and tp.comm is not None:
+        comm = comm_probe(tp, progress)
+    else:
+        comm = None
     res = run_config(args, args.model, tp, args.batch_per_gpu * max(world, args.simulate_tp), progress)
+    if comm is not None:
+        res["comm_probe"] = comm
     if args.secondary not in ("", "none") and args.simulate_tp <= 1 and args.secondary != args.model:
         # second BASELINE headline config (GPT-2-XL TP=1, 25 heads: no TP split), driver-timed in the same run;
         # with N GPUs every rank serves its own TP=1 replica (data parallel) and the node total is reported
@@ -76,9 +97,151 @@ def main():
             torch.cuda.empty_cache()
         res["secondary"] = run_config(args, args.secondary, tp, args.batch_per_gpu * world, progress, dp=True)
     if rank == 0:
-        print(json.dumps(res))
+        print(json.dumps(res), flush=True)
     if tp.is_real:
+        tp.close()
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
+
+
+# ------------------------------------------------------------------------------------------ launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _pump(stream, sink, keep):
+    """Copy a child's stream line by line into `sink` (None: drop) and keep the last lines in `keep`."""
+    for line in iter(stream.readline, ""):
+        keep.append(line)
+        if sink is not None:
+            sink.write(line)
+            sink.flush()
+    stream.close()
+
+
+def launch(args) -> int:
+    """GPU-free parent: start ``args.gpus`` rank processes of this script (no exec, no GPU call here),
+    forward rank 0's stdout (the JSON line) and stderr (progress), and fail fast: the first rank that
+    exits non-zero, or the timeout, ends every rank; the exit code is the failing rank's (124 on
+    timeout) and stderr names the rank with the tail of its stderr."""
+    n = args.gpus
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    argv = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+    procs, tails, pumps = [], [], []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port)
+        p = subprocess.Popen(argv, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                             start_new_session=True)
+        out_tail, err_tail = collections.deque(maxlen=400), collections.deque(maxlen=60)
+        for stream, sink, keep in ((p.stdout, sys.stdout if r == 0 else None, out_tail),
+                                   (p.stderr, sys.stderr if r == 0 else None, err_tail)):
+            th = threading.Thread(target=_pump, args=(stream, sink, keep), daemon=True)
+            th.start()
+            pumps.append(th)
+        procs.append(p)
+        tails.append(err_tail)
+
+    def kill_all():
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        t_end = time.time() + 10
+        for p in procs:
+            try:
+                p.wait(max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
+
+    def fail(r, code, why):
+        kill_all()
+        for th in pumps:
+            th.join(timeout=2)
+        tail = "".join(tails[r]) if r is not None else ""
+        print(f"[bench launcher] {why}; stopped all {n} ranks\n--- rank {r} stderr (tail) ---\n{tail}",
+              file=sys.stderr, flush=True)
+        return code
+
+    t0 = time.time()
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r, c = bad[0]
+                return fail(r, c if c > 0 else 128 - c, f"rank {r} exited with code {c}")
+            if all(c == 0 for c in codes):
+                break
+            if time.time() - t0 > args.timeout:
+                r = next((i for i, c in enumerate(codes) if c is None), None)
+                return fail(r, 124, f"timeout after {args.timeout:.0f}s (rank {r} still running)")
+            time.sleep(0.2)
+    except KeyboardInterrupt:
+        return fail(None, 130, "interrupted")
+    for th in pumps:
+        th.join(timeout=10)
+    return 0
+
+
+# ------------------------------------------------------------------------------------------ comm probe
+def comm_probe(tp, progress) -> dict:
+    """Latency of the native RCCL all-reduce at decode / prefill message sizes, eager and inside a HIP
+    graph (20 back-to-back all-reduces per replay): per-collective microseconds on this node's xGMI."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    out = {}
+    for nbytes in (64 << 10, 512 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20):
+        x = torch.ones(nbytes // 2, dtype=torch.bfloat16, device=dev)
+        for _ in range(3):
+            tp.all_reduce(x)
+        torch.cuda.synchronize()
+        tp.barrier()
+        n = 20
+        t = time.perf_counter()
+        for _ in range(n):
+            tp.all_reduce(x)
+        torch.cuda.synchronize()
+        eager = (time.perf_counter() - t) / n * 1e6
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            tp.all_reduce(x)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            for _ in range(n):
+                tp.all_reduce(x)
+        g.replay()
+        torch.cuda.synchronize()
+        tp.barrier()
+        t = time.perf_counter()
+        for _ in range(3):
+            g.replay()
+        torch.cuda.synchronize()
+        graph = (time.perf_counter() - t) / (3 * n) * 1e6
+        out[str(nbytes)] = {"eager_us": round(eager, 1), "graph_us": round(graph, 1),
+                            "busbw_GBps": round(2 * (tp.size - 1) / tp.size * nbytes / graph / 1e3, 1)}
+        del g, x
+    progress(f"comm probe ({tp.backend}, {tp.size} ranks): " +
+             ", ".join(f"{int(k) >> 10}KiB {v['graph_us']}us" for k, v in out.items()))
+    return {"backend": tp.backend, "ranks": tp.size, "all_reduce_bf16": out}
+
+
+def _world_gather(obj):
+    out = [None] * torch.distributed.get_world_size()
+    torch.distributed.all_gather_object(out, obj)
+    return out
 
 
 def run_config(args, model_name, tp, batch, progress, dp=False):
@@ -105,7 +268,20 @@ def run_config(args, model_name, tp, batch, progress, dp=False):
         return SamplingParams(max_new_tokens=args.gen_len, is_greedy=args.greedy, temperature=1.0, top_p=0.95,
                               top_k=50, ignore_eos=True, seed=7)
 
+    fault = os.environ.get("LLMSS_FAULT_INJECT", "")  # "rank:step:kind" (kind exit | raise | hang), tests only
+    fault = tuple(fault.split(":")) if fault else None
+    my_rank = tp.global_rank if tp.is_real else int(os.environ.get("RANK", "0"))
+    steps_done = [0]
+
     def one_step():
+        if fault is not None and int(fault[0]) == my_rank and int(fault[1]) == steps_done[0]:
+            progress(f"rank {my_rank}: injected fault {fault[2]!r} at step {steps_done[0]}")
+            if fault[2] == "exit":
+                os._exit(17)
+            if fault[2] == "hang":
+                time.sleep(1e6)
+            raise RuntimeError(f"injected fault at bench step {steps_done[0]}")
+        steps_done[0] += 1
         for p in prompts():
             eng.add_request(p, params())
         n = 0
@@ -120,7 +296,7 @@ def run_config(args, model_name, tp, batch, progress, dp=False):
 
     def barrier():
         if world > 1 and args.simulate_tp <= 1:
-            torch.distributed.barrier()
+            torch.distributed.barrier()  # CPU (gloo) group with the native RCCL data plane
 
     progress(f"engine ready: {model.cfg.model_type} {'dp' if dp else 'tp'}={world} batch={batch} "
              f"kv_blocks={eng.num_blocks} graphs={sorted({b for b, _ in eng.graphs})}")
@@ -145,12 +321,12 @@ def run_config(args, model_name, tp, batch, progress, dp=False):
     sync()
     barrier()
     el = time.perf_counter() - t0
+    rank_el = [el]
     if world > 1 and args.simulate_tp <= 1:  # slowest rank's clock; node total of generated tokens
-        t = torch.tensor([el, float(total)], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t[:1], op=torch.distributed.ReduceOp.MAX)
-        if dp:
-            torch.distributed.all_reduce(t[1:], op=torch.distributed.ReduceOp.SUM)
-        el, total = float(t[0].item()), int(t[1].item())
+        allv = tp.all_gather_object((el, total)) if not dp else _world_gather((el, total))
+        rank_el = [v[0] for v in allv]
+        el = max(rank_el)
+        total = sum(v[1] for v in allv) if dp else allv[0][1]
     tpot = np.nanmedian([m["tpot_s"] for m in mets]) * 1e3
     ttft = np.nanmedian([m["ttft_s"] for m in mets]) * 1e3
     e2e = np.nanmedian([m["e2e_s"] for m in mets]) * 1e3
@@ -172,6 +348,9 @@ def run_config(args, model_name, tp, batch, progress, dp=False):
         "vs_baseline": None,
         "dtype": "fp8-weights/bf16" if args.fp8 else "bf16",
         "data": "synthetic prompts, random-init weights",
+        "rccl_world_size": (torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1),
+        "comm_backend": tp.backend if not dp else "none (independent replicas)",
+        "rank_elapsed_s": [round(v, 4) for v in rank_el],
         "p50_tpot_ms": round(float(tpot), 3),
         "p50_ttft_ms": round(float(ttft), 3),
         "p50_request_latency_ms": round(float(e2e), 3),

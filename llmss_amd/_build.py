@@ -2,7 +2,7 @@
 
 Every ``csrc/*.hip`` kernel file and the host runtime ``csrc/*.cpp`` are compiled by ``hipcc
 --offload-arch=gfx950`` (cross-compiles without a GPU) in parallel into ``build/obj`` and linked
-into ``llmss_amd/_C*.so``. No torch headers, no hipify, no CUDA compatibility layer: bindings
+into ``llmss_amd/_C*.so`` (linked against RCCL for the native communicator, csrc/comm.cpp). No torch headers, no hipify, no CUDA compatibility layer: bindings
 take raw device pointers and a HIP stream handle (see ``csrc/bindings.cpp``).
 
 Usage: ``python -m llmss_amd._build [--force] [-j N]``.
@@ -93,7 +93,7 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
     newest = max(os.path.getmtime(o) for o in objs)
     if force or not os.path.exists(out) or os.path.getmtime(out) < newest:
         tmp = out + ".tmp"
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-lpthread"]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

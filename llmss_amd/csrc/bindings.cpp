@@ -74,6 +74,7 @@ void launch_quant_fp8_rows(const void* w, void* q, void* scale, int64_t N, int64
 void launch_dequant_fp8_rows(const void* q, const void* scale, void* w, int64_t N, int64_t K, hipStream_t st);
 
 void register_runtime(py::module_& m);  // host-side C++ runtime (runtime.cpp)
+void register_comm(py::module_& m);     // RCCL communicator (comm.cpp)
 
 #define P(x) reinterpret_cast<void*>(static_cast<uintptr_t>(x))
 #define CP(x) reinterpret_cast<const void*>(static_cast<uintptr_t>(x))
@@ -192,4 +193,5 @@ PYBIND11_MODULE(_C, m) {
     launch_dequant_fp8_rows(CP(q), CP(scale), P(w), N, K, S(st));
   });
   register_runtime(m);
+  register_comm(m);
 }

@@ -149,6 +149,8 @@ class Scheduler {
       throw std::invalid_argument("Scheduler.add: prompt_len + max_new_tokens exceeds max_model_len");
     if (chunk_ < 0 && prompt_len > max_tokens_)
       throw std::invalid_argument("Scheduler.add: prompt longer than max_batched_tokens (whole-prompt mode)");
+    if ((int64_t)blocks_for(prompt_len + max_new) > (int64_t)alloc_.num_blocks())
+      throw std::invalid_argument("Scheduler.add: sequence needs more KV blocks than the whole pool holds");
     SeqState s{id, prompt_len, max_new, prompt_len, 0, {}, 0, counter_++};
     seqs_.emplace(id, s);
     waiting_.push_back(id);
@@ -184,9 +186,35 @@ class Scheduler {
 
   void abort(int64_t id) { finish(id); }
 
+  // One step. When prompt chunks hold the pool and none of them can grow while nothing decodes (the
+  // chunked-prefill livelock: every step would come back empty), the newest running sequence is
+  // preempted and the step re-planned, until the oldest prompt fits (add() guarantees one does).
   StepBatch schedule() {
     StepBatch b;
+    for (;;) {
+      bool starved = plan(b);
+      if (!b.ids.empty() || !starved) break;
+      int64_t victim = -1, oldest = -1;
+      for (auto id : running_) {
+        if (victim < 0 || get(id).order > get(victim).order) victim = id;
+        if (oldest < 0 || get(id).order < get(oldest).order) oldest = id;
+      }
+      if (victim < 0 || victim == oldest)
+        throw std::runtime_error("Scheduler: KV pool cannot hold the oldest running sequence");
+      preempt(victim);
+      b.preempted.push_back(victim);
+    }
+    if (b.ids.empty()) return b;
+    b.kind = (b.num_decode == (int)b.ids.size()) ? 2 : 1;
+    fill_tables(b);
+    return b;
+  }
+
+  // The three stages of a step into `b`; returns true when a running prompt chunk could not get its
+  // KV blocks (admission is then skipped: a new prompt would only take blocks the old one needs).
+  bool plan(StepBatch& b) {
     int budget = max_tokens_;
+    bool starved = false;
     std::vector<int64_t> order(running_.begin(), running_.end());
     std::sort(order.begin(), order.end(), [&](int64_t a, int64_t c) { return get(a).order < get(c).order; });
     // ---- 1. decodes
@@ -220,12 +248,16 @@ class Scheduler {
       auto& s = get(order[i]);
       if (s.status != 1 || s.num_tokens - s.num_computed <= 1) continue;
       const int q = chunk_len(s, budget);
-      if (q <= 0 || !grow(s, s.num_computed + q)) break;
+      if (q <= 0) break;
+      if (!grow(s, s.num_computed + q)) {
+        starved = true;
+        break;
+      }
       emit(b, s, q);
       budget -= q;
     }
     // ---- 3. admission (FCFS, stop at the first prompt that does not fit)
-    while (!waiting_.empty() && budget > 0 && (int)running_.size() < max_seqs_) {
+    while (!starved && !waiting_.empty() && budget > 0 && (int)running_.size() < max_seqs_) {
       auto& s = get(waiting_.front());
       const int q = chunk_len(s, budget);  // after preemption the whole known sequence is recomputed
       if (q <= 0 || !grow(s, q)) break;
@@ -235,12 +267,10 @@ class Scheduler {
       emit(b, s, q);
       budget -= q;
     }
-    if (b.ids.empty()) return b;
-    b.kind = (b.num_decode == (int)b.ids.size()) ? 2 : 1;
-    fill_tables(b);
-    return b;
+    return starved;
   }
 
+ public:
   int num_waiting() const { return (int)waiting_.size(); }
   int num_running() const { return (int)running_.size(); }
   // running sequences with prompt tokens still to compute (the next step is not a pure decode)

@@ -19,6 +19,7 @@ Here:
 from __future__ import annotations
 
 import collections
+import contextlib
 import math
 import os
 import time
@@ -170,6 +171,7 @@ class LLMEngine:
         self._last_rec = None  # last collected decode step (per-request constants for reuse)
         self._last_fins = None
         self._stage = 0  # pinned staging set of the next launch
+        self._t_collect = 0.0  # when the last decode step was collected (non-overlapped decode_time_s)
         self.async_decode = os.environ.get("LLMSS_ASYNC_DECODE", "1") != "0"
         self._host_prof = os.environ.get("LLMSS_HOST_PROFILE") == "1"  # host-side time per engine phase
         self.check_tokens = check_tokens if check_tokens is not None else os.environ.get("LLMSS_CHECK_TOKENS") == "1"
@@ -185,6 +187,7 @@ class LLMEngine:
         from ..ops.hip import CAND_KC, CAND_MAX_SHARD
 
         self.dist_sampling = (self.tp.size > 1 and os.environ.get("LLMSS_DIST_SAMPLER", "1") != "0"
+                              and self.tp.size * CAND_KC <= 2048  # sample_cand's gathered-candidate limit
                               and (not self.is_gpu or model.plan.v_l <= CAND_MAX_SHARD))
         # one GPU (TP=1), opt-in (LLMSS_CAND_SHARDS=8): the same two-kernel candidate sampler over column shards
         # of the vocabulary (one launch, B x shards workgroups) instead of one workgroup per row scanning all of
@@ -346,6 +349,10 @@ class LLMEngine:
             self.stats["host_collect_apply_s"] = self.stats.get("host_collect_apply_s", 0.0) + t_b - t_a
             self.stats["host_schedule_s"] = self.stats.get("host_schedule_s", 0.0) + t_c - t_b
         new_events: List[StepEvent] = []
+        if batch.kind == 0 and done is None and self.sched.has_work():
+            # the scheduler preempts its way out of a starved pool, so an idle step with work left is a bug
+            raise RuntimeError(f"scheduler returned an idle step with {self.sched.num_waiting()} waiting and "
+                               f"{self.sched.num_running()} running sequences")
         if batch.kind != 0:
             self.stats["preemptions"] += len(batch.preempted)
             ids = batch.ids
@@ -572,7 +579,11 @@ class LLMEngine:
         sel = [reqs[i] for i in rows]
         tokens = toks[rows].tolist()
         self.stats["decode_steps"] += 1
-        self.stats["decode_time_s"] += time.perf_counter() - rec["t0"]
+        # wall time without overlap: pipelined steps are in flight together, so each collected step counts from
+        # its launch or from the previous collection, whichever is later
+        now = time.perf_counter()
+        self.stats["decode_time_s"] += now - max(rec["t0"], self._t_collect)
+        self._t_collect = now
         out = self._apply(ids, sel, tokens)
         fins = self._last_fins
         nxt = self._pending[0] if self._pending else None
@@ -602,9 +613,15 @@ class LLMEngine:
         # vocab-parallel runs: graphs for both samplers (candidates when every row allows it, else the
         # gathered-logits sampler), chosen per step
         modes = (True, False) if self.dist_sampling else (False,)
+        # warm-up passes (lazy allocations, first launches). Native RCCL: with real collectives, so each
+        # algorithm's lazy peer connection happens here and not inside the capture. torch's RCCL process
+        # group: collectives suspended - its watchdog thread would otherwise still track the warm-up's work
+        # items when the capture starts, and a watchdog query of their end events (recorded on the
+        # communicator's stream, which the captured collectives pull into the capture) aborts the process
+        torch_pg = self.tp.is_real and self.tp.comm is None and not self.tp.host_staged
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
+        with torch.cuda.stream(s), (self.tp.suspended() if torch_pg else contextlib.nullcontext()):
             for b in reversed(self.buckets):
                 for d in modes:
                     for _ in range(2):
@@ -614,13 +631,6 @@ class LLMEngine:
         # settle the caching allocator's pending cross-stream events (freed side-stream blocks) outside the
         # capture, so no allocation during capture queries an event
         torch.cuda.empty_cache()
-        if self.tp.is_real and not self.tp.host_staged:
-            # let the RCCL process group's watchdog retire the warm-up collectives above before capturing:
-            # their end events were recorded on the communicator's stream, which the captured collectives
-            # pull into the capture, and a watchdog query of such an event then fails
-            # ("operation not permitted on an event last recorded in a capturing stream") and aborts the
-            # process. The watchdog scans every 100 ms; with nothing in flight its list is empty after this.
-            time.sleep(0.5)
         # thread-local capture: the RCCL communicator's watchdog thread keeps querying the events of earlier
         # collectives; under the default global capture mode such a query from another thread aborts the
         # process ("operation not permitted when stream is capturing")

@@ -113,12 +113,16 @@ class CausalLM:
         order = dec + ext
         out = torch.zeros(B, S, self.model.plan.vocab_padded, dtype=torch.float32, device=dev)
         if order:
+            # the whole step's block need first: a failed allocation then leaves the pool untouched
+            needs = [max(0, -(-(start + len(cols)) // bs) - len(past.blocks[b])) for b, cols, start in order]
+            if sum(needs) > len(self._free):
+                raise RuntimeError("CausalLM: KV pool exhausted")
+            for (b, _, _), need in zip(order, needs):
+                if need:
+                    past.blocks[b].extend(self._alloc(need))
             tok, pos, slots, qlens, ctx, bt_rows = [], [], [], [], [], []
             for b, cols, start in order:
                 n = len(cols)
-                need = -(-(start + n) // bs) - len(past.blocks[b])
-                if need > 0:
-                    past.blocks[b].extend(self._alloc(need))
                 blocks = past.blocks[b]
                 tok.append(ids_cpu[b, cols])
                 pos.append(pos_cpu[b, cols] if pos_cpu is not None else torch.arange(start, start + n))

@@ -8,14 +8,18 @@ and ``FakeGroup`` (``dist.py:14-37``). Differences, by design:
 * ``world_size == 1`` is a first-class case: :class:`TPGroup` with ``size == 1`` turns every
   collective into the identity and *never* needs a default process group (the reference's
   single-GPU ``generate.py`` crashes on an un-grouped ``dist.broadcast`` — SURVEY Q2).
-* On GPUs the backend is ``nccl`` which, on ROCm, is RCCL over xGMI. The data-plane collectives
-  are issued on the caller's current HIP stream so they can be captured into HIP graphs with
-  the rest of the decode step.
+* On GPUs the data plane is a native RCCL communicator (``llmss_amd._C.RcclComm``, csrc/comm.cpp)
+  bootstrapped over a CPU (gloo) process group: collectives are raw ``ncclAllReduce`` /
+  ``ncclAllGather`` calls on the caller's current HIP stream, so they are captured into the decode
+  HIP graphs with the rest of the step, with no torch Work / event / watchdog in the loop.
+  ``LLMSS_COMM=torch`` selects torch's ``nccl`` process group instead (RCCL as well), created with
+  the reference's high-priority-stream option (``dist.py:52-53``).
 * ``DEBUG=1`` keeps the reference's "fake" semantics: every rank computes with its own shard and
   no communication happens (shape/loader debugging only, numerically wrong by construction).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from datetime import timedelta
 from typing import List, Optional, Tuple
@@ -32,11 +36,14 @@ class TPGroup:
     """Tensor-parallel communicator (size 1, real, or fake)."""
 
     def __init__(self, rank: int = 0, size: int = 1, group=None, fake: bool = False,
-                 sim_comm: Optional[Tuple[float, float]] = None):
+                 sim_comm: Optional[Tuple[float, float]] = None, comm=None):
         self.rank = rank
         self.size = size
         self.group = group
         self.fake = fake
+        # native RCCL communicator (device tensors); `group` then is the CPU (gloo) group of the same ranks
+        self.comm = comm
+        self._suspend = False  # suspended(): data-plane collectives are skipped (shape-only warm-up)
         # fake groups only: (latency us, algorithmic GB/s) of a modelled all-reduce. Each all-reduce
         # then occupies the issuing stream for latency + bytes/bandwidth (a spin kernel on one
         # workgroup), so the comm/compute overlap of a TP=N schedule can be measured on one GPU.
@@ -90,8 +97,26 @@ class TPGroup:
         """
         st = getattr(self, "_host_staged", None)
         if st is None:
-            st = self._host_staged = self.is_real and dist.get_backend(self.group) == "gloo"
+            st = self._host_staged = self.is_real and self.comm is None and dist.get_backend(self.group) == "gloo"
         return st
+
+    @property
+    def backend(self) -> str:
+        """'rccl-native' | 'nccl' (torch's RCCL process group) | 'gloo' | 'local' | 'fake'."""
+        if self.fake:
+            return "fake"
+        if not self.is_real:
+            return "local"
+        return "rccl-native" if self.comm is not None else dist.get_backend(self.group)
+
+    def _native_ok(self, t: torch.Tensor) -> bool:
+        return self.comm is not None and t.is_cuda
+
+    @staticmethod
+    def _code(t: torch.Tensor) -> int:
+        from .. import _native
+
+        return _native().rccl_dtypes[str(t.dtype).replace("torch.", "")]
 
     @staticmethod
     def _no_capture():
@@ -99,9 +124,28 @@ class TPGroup:
             raise RuntimeError("host-staged (gloo) collectives cannot be captured into a HIP graph; "
                                "run the engine with use_graphs=False on this group")
 
+    @contextlib.contextmanager
+    def suspended(self):
+        """Skip the data-plane collectives inside the block (every rank must do the same): all_reduce
+        returns its input, all_gather_last_dim N copies of the local shard. For warm-up passes whose
+        values are discarded but whose collectives would otherwise leave work items in torch's RCCL
+        watchdog right before a graph capture (torch process-group mode only)."""
+        prev, self._suspend = self._suspend, True
+        try:
+            yield self
+        finally:
+            self._suspend = prev
+
     # ------------------------------------------------------------ data plane
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
-        if self.is_real and t.is_cuda and self.host_staged:
+        if self._suspend:
+            return t
+        if self.is_real and self._native_ok(t):
+            if not t.is_contiguous():
+                raise ValueError("all_reduce needs a contiguous tensor")
+            self.comm.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), self._code(t),
+                                 torch.cuda.current_stream().cuda_stream)
+        elif self.is_real and t.is_cuda and self.host_staged:
             self._no_capture()
             h = t.cpu()
             dist.all_reduce(h, group=self.group)
@@ -114,6 +158,8 @@ class TPGroup:
 
     def all_gather_last_dim(self, t: torch.Tensor) -> torch.Tensor:
         """Gather shards along the last dim: [..., n] -> [..., size*n]."""
+        if self._suspend and self.size > 1:
+            return torch.cat([t.contiguous()] * self.size, -1)
         if not self.is_real:
             if self.sim_comm is not None and t.is_cuda:
                 self._sim_wait(self.size * t.numel() * t.element_size())
@@ -121,7 +167,11 @@ class TPGroup:
                 return torch.cat([t] * self.size, -1)
             return t
         t = t.contiguous()
-        if t.is_cuda and self.host_staged:
+        if self._native_ok(t):
+            out = torch.empty((self.size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            self.comm.all_gather(t.data_ptr(), out.data_ptr(), t.numel(), self._code(t),
+                                 torch.cuda.current_stream().cuda_stream)
+        elif t.is_cuda and self.host_staged:
             self._no_capture()
             h = t.cpu()
             out = torch.empty((self.size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype)
@@ -134,7 +184,11 @@ class TPGroup:
         return out.movedim(0, -2).reshape(*t.shape[:-1], self.size * t.shape[-1])
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
-        if self.is_real and t.is_cuda and self.host_staged:
+        if self.is_real and self._native_ok(t):
+            if not t.is_contiguous():
+                raise ValueError("broadcast needs a contiguous tensor")
+            self.comm.broadcast(t.data_ptr(), t.numel(), self._code(t), int(src), torch.cuda.current_stream().cuda_stream)
+        elif self.is_real and t.is_cuda and self.host_staged:
             self._no_capture()
             h = t.cpu()
             dist.broadcast(h, src=self._global(src), group=self.group)
@@ -168,7 +222,7 @@ class TPGroup:
 
     # ------------------------------------------------------------ host-side agreement
     def _host_tensor_device(self):
-        if dist.get_backend(self.group) == "nccl":
+        if self.comm is None and dist.get_backend(self.group) == "nccl":
             return torch.device("cuda", torch.cuda.current_device())
         return torch.device("cpu")
 
@@ -195,14 +249,59 @@ class TPGroup:
         if bad:
             raise RuntimeError(f"{what}: tensor-parallel ranks disagree (rank: {{key: (value, rank0 value)}}): {bad}")
 
+    def close(self, abort: bool = False):
+        """Release the native communicator (``abort``: without waiting for peers, e.g. after a failure)."""
+        if self.comm is not None:
+            self.comm.abort() if abort else self.comm.destroy()
+            self.comm = None
+
     def __repr__(self):
-        kind = "fake" if self.fake else ("local" if self.size == 1 else "rccl/gloo")
-        return f"TPGroup(rank={self.rank}, size={self.size}, {kind})"
+        return f"TPGroup(rank={self.rank}, size={self.size}, {self.backend})"
 
 
 def _env_int(name: str, default: int) -> int:
     v = os.environ.get(name)
     return int(v) if v not in (None, "") else default
+
+
+def _pg_options(backend: str):
+    """torch ``nccl`` process groups get the reference's high-priority internal stream (``dist.py:52-53``)."""
+    if backend != "nccl" or not hasattr(dist, "ProcessGroupNCCL"):
+        return None
+    return dist.ProcessGroupNCCL.Options(is_high_priority_stream=True)
+
+
+def comm_mode() -> str:
+    """Data plane on GPUs: 'native' (csrc/comm.cpp RcclComm, default) or 'torch' (torch's nccl process group)."""
+    m = os.environ.get("LLMSS_COMM", "native")
+    if m not in ("native", "torch"):
+        raise ValueError(f"LLMSS_COMM must be 'native' or 'torch', not {m!r}")
+    return m
+
+
+def _native_comm(rank: int, dp: int, tp: int):
+    """One RCCL communicator per data-parallel replica (ranks r*tp .. r*tp+tp-1). Each replica leader draws a
+    unique id; the ids travel over the CPU world group (every rank joins every broadcast), then each rank
+    joins its replica's communicator and checks it with one all-reduce."""
+    from .. import _native
+
+    C = _native()
+    uids = []
+    for r in range(dp):
+        box = [C.rccl_unique_id() if rank == r * tp else None]
+        dist.broadcast_object_list(box, src=r * tp)
+        uids.append(box[0])
+    r = rank // tp
+    comm = C.RcclComm(uids[r], tp, rank - r * tp, torch.cuda.current_device())
+    t = torch.full((4,), float(rank - r * tp + 1), dtype=torch.float32, device="cuda")
+    comm.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), C.rccl_dtypes["float32"],
+                    torch.cuda.current_stream().cuda_stream)
+    want = tp * (tp + 1) / 2
+    got = t.cpu()
+    if not bool((got == want).all()):
+        comm.abort()
+        raise RuntimeError(f"rank {rank}: RCCL self-check all-reduce returned {got.tolist()}, expected {want}")
+    return comm
 
 
 def initialize_distributed(timeout_s: Optional[int] = None, backend: Optional[str] = None, dp: Optional[int] = None):
@@ -211,9 +310,14 @@ def initialize_distributed(timeout_s: Optional[int] = None, backend: Optional[st
     Returns ``(tp_group, rank, world_size)`` like the reference
     (``dist.py:40``); ``tp_group`` is a :class:`TPGroup`.
 
+    On GPUs (``backend`` None) the torch process group is CPU-only (gloo: bootstrap, control plane,
+    barriers) and the tensor data plane is a native RCCL communicator per replica (:func:`comm_mode`).
+    ``backend="gloo"`` on GPUs stages device tensors through the host (several ranks sharing one GPU in
+    tests); ``backend="nccl"`` / ``LLMSS_COMM=torch`` uses torch's RCCL process group for the data plane.
+
     ``dp`` (or ``LLMSS_DP``) > 1 splits the world into ``dp`` data-parallel replicas of
     ``world / dp`` consecutive ranks each (one node: a replica's ranks share an xGMI island). Every
-    replica gets its own data-plane communicator (RCCL / gloo) and its own gloo control group;
+    replica gets its own data-plane communicator and its own gloo control group;
     the returned TPGroup is this rank's replica (``.replica``, ``.dp``, ``.global_rank``).
     """
     if timeout_s is None:  # engine start-up (weight load, per-rank GEMM autotuning) runs between collectives
@@ -226,8 +330,9 @@ def initialize_distributed(timeout_s: Optional[int] = None, backend: Optional[st
     if use_cuda:
         n = torch.cuda.device_count()
         torch.cuda.set_device(local_rank % n)
+    native = use_cuda and backend is None and comm_mode() == "native"
     if backend is None:
-        backend = "nccl" if use_cuda else "gloo"
+        backend = "nccl" if use_cuda and not native else "gloo"
 
     dp = int(dp if dp is not None else _env_int("LLMSS_DP", 1))
     if dp < 1 or world_size % dp:
@@ -244,20 +349,26 @@ def initialize_distributed(timeout_s: Optional[int] = None, backend: Optional[st
         kwargs = dict(backend=backend, world_size=world_size, rank=rank, timeout=timedelta(seconds=timeout_s))
         if backend == "nccl":
             kwargs["device_id"] = torch.device("cuda", torch.cuda.current_device())
+            kwargs["pg_options"] = _pg_options(backend)
         dist.init_process_group(**kwargs)
-    log.info("rank %d/%d initialised backend=%s", rank, world_size, backend)
-    if dp == 1:
-        return TPGroup(rank, world_size, group=dist.group.WORLD), rank, world_size
     tp = world_size // dp
+    comm = _native_comm(rank, dp, tp) if native and tp > 1 else None
+    log.info("rank %d/%d initialised: process group %s, data plane %s", rank, world_size, backend,
+             "native RCCL" if comm is not None else backend)
+    if dp == 1:
+        return TPGroup(rank, world_size, group=dist.group.WORLD, comm=comm), rank, world_size
+    # the replica's control group carries the serving driver's leader heartbeat: its timeout is the
+    # follower's leader timeout (EngineDriver.leader_timeout_s), not the long start-up timeout above
+    ctrl_timeout = _env_int("LLMSS_LEADER_TIMEOUT_S", 300)
     mine = None
     for r in range(dp):  # new_group is collective over the world: every rank creates every group
         ranks = list(range(r * tp, (r + 1) * tp))
-        data = dist.new_group(ranks, backend=backend) if tp > 1 else None
-        ctrl = dist.new_group(ranks, backend="gloo", timeout=timedelta(seconds=timeout_s)) if tp > 1 else None
+        data = dist.new_group(ranks, backend=backend, pg_options=_pg_options(backend)) if tp > 1 else None
+        ctrl = dist.new_group(ranks, backend="gloo", timeout=timedelta(seconds=ctrl_timeout)) if tp > 1 else None
         if rank in ranks:
             mine = (r, data, ctrl)
     r, data, ctrl = mine
-    g = TPGroup(rank - r * tp, tp, group=data)
+    g = TPGroup(rank - r * tp, tp, group=data, comm=comm)
     g.replica, g.dp, g.global_rank, g.ctrl_group = r, dp, rank, ctrl
     log.info("rank %d: data-parallel replica %d/%d, tensor-parallel rank %d/%d", rank, r, dp, g.rank, tp)
     return g, rank, world_size

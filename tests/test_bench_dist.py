@@ -7,6 +7,9 @@ import os
 import socket
 import subprocess
 import sys
+import time
+
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -49,3 +52,43 @@ def test_bench_two_ranks_gloo():
     s = d["secondary"]
     assert s["config"]["parallelism"] == "dp2xtp1" and s["config"]["global_batch"] == 4
     assert abs(s["value"] * s["ms_per_step"] / 1e3 - 16) < 0.05  # 2 replicas x 2 requests x 4 tokens
+
+
+def _cpu_env(**kw):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT")}
+    env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", MASTER_ADDR="127.0.0.1", **kw)
+    return env
+
+
+_TINY = ["--model", "tiny-llama", "--secondary", "none", "--batch-per-gpu", "2", "--prompt-len", "8", "--gen-len", "4"]
+
+
+def test_bench_self_launches_ranks():
+    """`python bench.py --gpus 2` without torchrun: the process becomes a launcher for 2 ranks and forwards
+    rank 0's single JSON line."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1"]
+                       + _TINY, env=_cpu_env(), capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "tp2" and d["rccl_world_size"] == 2
+    assert len(d["rank_elapsed_s"]) == 2 and max(d["rank_elapsed_s"]) * 1e3 / 2 == pytest.approx(d["ms_per_step"],
+                                                                                                 rel=1e-2)
+
+
+@pytest.mark.parametrize("kind", ["exit", "raise", "hang"])
+def test_bench_launcher_fails_fast_on_rank_failure(kind):
+    """One rank dies (or hangs) mid-run: the launcher stops every rank and exits non-zero naming it."""
+    timeout = "40" if kind == "hang" else "600"
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--timeout", timeout] + _TINY, env=_cpu_env(LLMSS_FAULT_INJECT=f"1:1:{kind}"),
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if kind == "hang":
+        assert r.returncode == 124 and "timeout" in r.stderr
+    else:
+        assert "rank 1 exited" in r.stderr or "rank 0 exited" in r.stderr, r.stderr[-2000:]
+    assert time.time() - t0 < 200

@@ -1,0 +1,107 @@
+"""Native RCCL communicator (csrc/comm.cpp) on the one-GPU box.
+
+RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so these tests run a ONE-rank
+communicator: they check the binding (dtype codes, pointers, streams), that the calls are captured into
+HIP graphs and replay, and the TP engine end to end with the native data plane in its graphs. They are
+capture smoke tests - a one-rank all-reduce moves no data. The multi-rank behaviour (sums over xGMI,
+per-collective latency) is measured by bench.py's comm probe in the driver's multi-GPU run
+(``comm_probe`` in the bench JSON) and rehearsed on CPU by tests/test_bench_dist.py.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def comm():
+    from llmss_amd import _native
+
+    C = _native()
+    c = C.RcclComm(C.rccl_unique_id(), 1, 0, torch.cuda.current_device())
+    yield c
+    c.destroy()
+
+
+def _code(t):
+    from llmss_amd import _native
+
+    return _native().rccl_dtypes[str(t.dtype).replace("torch.", "")]
+
+
+def _st():
+    return torch.cuda.current_stream().cuda_stream
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32, torch.int64])
+def test_single_rank_collectives(comm, dtype):
+    x = (torch.arange(1000, device="cuda") % 97).to(dtype)
+    ref = x.clone()
+    comm.all_reduce(x.data_ptr(), x.data_ptr(), x.numel(), _code(x), _st())
+    out = torch.empty_like(x)
+    comm.all_gather(x.data_ptr(), out.data_ptr(), x.numel(), _code(x), _st())
+    comm.broadcast(x.data_ptr(), x.numel(), _code(x), 0, _st())
+    torch.cuda.synchronize()
+    assert torch.equal(x, ref) and torch.equal(out, ref)
+    assert comm.async_error() == ""
+
+
+def test_collective_inside_graph_replays(comm):
+    """An out-of-place all-gather (one rank: a device copy) captured into a graph reads the CURRENT input on
+    every replay - the captured node is live, not a recording of the capture-time values."""
+    x = torch.zeros(4096, dtype=torch.bfloat16, device="cuda")
+    out = torch.empty_like(x)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        comm.all_gather(x.data_ptr(), out.data_ptr(), x.numel(), _code(x), _st())
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        comm.all_reduce(x.data_ptr(), x.data_ptr(), x.numel(), _code(x), _st())
+        comm.all_gather(x.data_ptr(), out.data_ptr(), x.numel(), _code(x), _st())
+    for v in (1.0, 2.5, -3.0):
+        x.fill_(v)
+        g.replay()
+        torch.cuda.synchronize()
+        assert bool((out == v).all())
+
+
+def test_tp_engine_with_native_comm_in_graphs(comm):
+    """TP=2 shard plan with the native communicator as its data plane: every row-parallel all-reduce and
+    the candidate gather go through RcclComm, inside the captured decode graphs; graphs == eager."""
+    from llmss_amd.engine import LLMEngine, SamplingParams
+    from llmss_amd.models.config import get_preset
+    from llmss_amd.models.decoder import DecoderLM
+    from llmss_amd.models.weights import random_weights
+    from llmss_amd.parallel.dist import TPGroup
+
+    class OneRankNative(TPGroup):  # the comm has one rank; the shard plan claims 2 (gather = 2 copies)
+        def all_gather_last_dim(self, t):
+            t = t.contiguous()
+            out = torch.empty_like(t)
+            self.comm.all_gather(t.data_ptr(), out.data_ptr(), t.numel(), self._code(t), _st())
+            return torch.cat([out, out], -1)
+
+        def all_reduce_int(self, v, op="min"):
+            return int(v)
+
+        def check_consistent(self, what, fp):
+            pass
+
+        def all_gather_object(self, obj):
+            return [obj, obj]
+
+    tp = OneRankNative(0, 2, comm=comm)
+    assert tp.backend == "rccl-native" and not tp.host_staged
+    cfg = get_preset("tiny-llama", hidden_size=256, num_heads=4, num_kv_heads=2, head_dim=64, rotary_dim=64,
+                     intermediate_size=512, max_position_embeddings=256)
+    m = DecoderLM(cfg, random_weights(cfg, 2, 0, device="cuda", dtype=torch.bfloat16, seed=3, std=0.05), tp)
+    prompts = [[int(x) for x in torch.randint(0, cfg.vocab_size, (n,))] for n in (5, 17, 33)]
+    sp = SamplingParams(max_new_tokens=12, is_greedy=True, ignore_eos=True)
+    e_graph = LLMEngine(m, max_num_seqs=4, block_size=16, use_graphs=True, autotune=False)
+    assert e_graph.use_graphs and len(e_graph.graphs) > 0
+    out_g = e_graph.generate(prompts, sp)
+    del e_graph
+    e_eager = LLMEngine(m, max_num_seqs=4, block_size=16, use_graphs=False, autotune=False)
+    assert e_eager.generate(prompts, sp) == out_g

@@ -143,8 +143,11 @@ def test_tp_allreduce_overlap_streams():
 
 
 def test_rccl_collectives_inside_decode_graphs():
-    """The TP decode step (RCCL all-reduces + all-gather) must be capturable into HIP graphs: graph
-    replay == eager with a real (one-member) RCCL communicator in the loop."""
+    """Capture smoke test (torch process-group mode, LLMSS_COMM=torch): the TP decode step with its
+    all-reduces + all-gather through torch's RCCL process group captures into HIP graphs and replays ==
+    eager. The communicator has ONE member, so its in-place all-reduces move no data and need not leave a
+    node in the graph: this proves capture works, not that a multi-rank collective is in the graph (that is
+    measured by bench.py's comm probe on the driver's multi-GPU node)."""
     import os
 
     import torch.distributed as dist
@@ -177,9 +180,11 @@ def test_rccl_collectives_inside_decode_graphs():
 
 
 def test_graph_capture_while_rccl_watchdog_polls():
-    """Regression: with the RCCL communicator's watchdog thread tracking earlier collectives, a capture in
-    torch's default (global) mode aborted the process when the watchdog queried an event mid-capture
-    ("operation not permitted when stream is capturing"). Engine and autotuner capture thread-locally."""
+    """Capture smoke regression (torch process-group mode): with the RCCL process group's watchdog thread
+    tracking earlier collectives, a capture in torch's default (global) mode aborted the process when the
+    watchdog queried an event mid-capture ("operation not permitted when stream is capturing"). Engine and
+    autotuner capture thread-locally. One member: the captured in-place all-reduce is empty (HIP warns
+    "The CUDA Graph is empty"); the test is about the watchdog, not the collective."""
     import os
 
     import torch.distributed as dist

@@ -163,3 +163,38 @@ def test_scheduler_on_tokens_batched():
     b = S.schedule()
     S.on_tokens(b.ids, np.zeros(2, dtype=bool))  # third token: max_new reached -> finished
     assert not S.has_work()
+
+
+def _drive(s, max_steps=500):
+    """Run the scheduler to completion as the engine would; every step must do work."""
+    steps = preempted = 0
+    while s.has_work():
+        b = s.schedule()
+        assert b.kind != 0, "idle step with work left (livelock)"
+        preempted += len(b.preempted)
+        for i, smp in zip(b.ids.tolist(), b.sample.tolist()):
+            if smp:
+                s.on_token(i, False)
+        steps += 1
+        assert steps < max_steps
+    return steps, preempted
+
+
+@pytest.mark.parametrize("chunk", [8, 0])
+def test_scheduler_chunked_prefill_pool_exhaustion(native, chunk):
+    """concurrent chunked prompts that together hold the whole KV pool while nothing
+    decodes used to make every later schedule() idle forever. Now the newest is preempted."""
+    s = native.Scheduler(num_blocks=8, block_size=4, max_num_seqs=4, max_batched_tokens=16, max_model_len=64,
+                         prefill_chunk=chunk)
+    s.add(1, 20, 4)
+    s.add(2, 20, 4)
+    steps, preempted = _drive(s)
+    assert preempted >= 1 and s.num_free_blocks() == 8
+
+
+def test_scheduler_rejects_sequence_larger_than_pool(native):
+    s = native.Scheduler(num_blocks=4, block_size=4, max_num_seqs=4, max_batched_tokens=64, max_model_len=64)
+    with pytest.raises(ValueError):
+        s.add(1, 16, 4)  # 20 tokens need 5 blocks; the pool has 4
+    s.add(2, 12, 4)
+    assert _drive(s)[0] > 0
