@@ -60,12 +60,29 @@ def main():
     ap.add_argument("--sim-comm", default="",
                     help="with --simulate-tp: model each all-reduce / all-gather as LAT_US,GBPS (latency + bytes / "
                          "algorithmic bandwidth, a spin kernel on the collective's stream) to measure comm overlap")
+    ap.add_argument("--secondary-serve", default="grpc", choices=["grpc", "engine"],
+                    help="secondary config timed through the in-process gRPC Generate service with a separate "
+                         "client process (BASELINE config #2 'served over gRPC'; the engine-direct number is "
+                         "reported too), or engine-direct only")
     ap.add_argument("--timeout", type=float, default=float(os.environ.get("LLMSS_BENCH_TIMEOUT_S", "2400")),
                     help="launcher mode: kill every rank and exit 124 after this many seconds")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch(args))
+
+    # the gRPC clients run in their own process, started before this one touches the GPU (no fork of a
+    # GPU-initialised process); they learn the server port on stdin once the engine is up
+    client = None
+    if args.secondary not in ("", "none") and args.secondary != args.model and args.simulate_tp <= 1 \
+            and args.secondary_serve == "grpc":
+        from llmss_amd.models.config import get_preset
+
+        client = subprocess.Popen(
+            [sys.executable, "-m", "llmss_amd.serving.loadgen", "--batch", str(args.batch_per_gpu), "--prompt-len",
+             str(args.prompt_len), "--gen-len", str(args.gen_len), "--vocab", str(get_preset(args.secondary).vocab_size),
+             "--seed", str(4321 + int(os.environ.get("RANK", "0")))] + (["--greedy"] if args.greedy else []),
+            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, cwd=ROOT)
 
     from llmss_amd.parallel.dist import TPGroup, initialize_distributed
 
@@ -95,7 +112,12 @@ def main():
         # with N GPUs every rank serves its own TP=1 replica (data parallel) and the node total is reported
         if torch.cuda.is_available():
             torch.cuda.empty_cache()
-        res["secondary"] = run_config(args, args.secondary, tp, args.batch_per_gpu * world, progress, dp=True)
+        res["secondary"] = run_config(args, args.secondary, tp, args.batch_per_gpu * world, progress, dp=True,
+                                      client=client)
+    if client is not None and client.poll() is None:
+        client.stdin.write("quit\n")
+        client.stdin.flush()
+        client.wait(timeout=60)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if tp.is_real:
@@ -244,7 +266,48 @@ def _world_gather(obj):
     return out
 
 
-def run_config(args, model_name, tp, batch, progress, dp=False):
+def run_served(args, eng, client, progress, world, rank_sync):
+    """The same engine behind the in-process gRPC Generate service (EngineDriver thread + EngineServicer);
+    the client process sends each step's ``batch`` requests concurrently. Returns (seconds, tokens, client
+    step reports) over ``args.steps`` timed steps after ``args.warmup`` untimed ones."""
+    from llmss_amd.serving.driver import EngineDriver
+    from llmss_amd.serving.grpc_api import EngineServicer, serve
+    from llmss_amd.utils.tokenizer import load_tokenizer
+
+    drv = EngineDriver(eng).start()
+    server = serve(EngineServicer(drv, load_tokenizer(args.secondary, eng.cfg.vocab_size)), port=0, host="127.0.0.1")
+    client.stdin.write(f"{server.bound_port}\n")
+    client.stdin.flush()
+
+    def step():
+        client.stdin.write("step\n")
+        client.stdin.flush()
+        line = client.stdout.readline()
+        if not line:
+            raise RuntimeError(f"gRPC client process ended (exit code {client.poll()})")
+        return json.loads(line)
+
+    try:
+        for i in range(args.warmup):
+            r = step()
+            progress(f"grpc warmup {i}: {r['wall_s']:.3f}s")
+        rank_sync()
+        t0 = time.perf_counter()
+        reps = []
+        for i in range(args.steps):
+            reps.append(step())
+            progress(f"grpc step {i}: {reps[-1]['tokens']} tokens, {time.perf_counter() - t0:.3f}s elapsed")
+        rank_sync()
+        el = time.perf_counter() - t0
+    finally:
+        server.stop(0).wait()
+        drv.stop()
+    if drv.error is not None:
+        raise RuntimeError(f"engine driver failed: {drv.error}")
+    return el, sum(r["tokens"] for r in reps), reps
+
+
+def run_config(args, model_name, tp, batch, progress, dp=False, client=None):
     """Build ``model_name`` on ``tp`` (``dp``: an independent TP=1 replica per rank), warm up, time
     ``args.steps`` batched generations; returns the JSON dict."""
     from llmss_amd.engine import LLMEngine, SamplingParams, build_model
@@ -361,6 +424,31 @@ def run_config(args, model_name, tp, batch, progress, dp=False):
                    "engine_stats": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()},
                    **({"phase_ms": eng.phase_summary()} if eng.timer.enabled else {})},
     }
+    if client is not None:
+        def rank_sync():
+            sync()
+            barrier()
+            sync()
+
+        gel, gtot, reps = run_served(args, eng, client, progress, world, rank_sync)
+        grank = [gel]
+        if world > 1:
+            allv = _world_gather((gel, gtot))
+            grank = [v[0] for v in allv]
+            gel, gtot = max(grank), sum(v[1] for v in allv)
+        engine_direct = {k: out[k] for k in ("value", "ms_per_step", "p50_tpot_ms", "p50_ttft_ms",
+                                             "p50_request_latency_ms", "rank_elapsed_s")}
+        out.update(value=round(gtot / gel, 2), ms_per_step=round(gel / args.steps * 1e3, 3),
+                   p50_tpot_ms=round(float(np.median([r["p50_tpot_s"] for r in reps])) * 1e3, 3),
+                   p50_ttft_ms=round(float(np.median([r["p50_ttft_s"] for r in reps])) * 1e3, 3),
+                   p50_request_latency_ms=round(float(np.median([r["p50_latency_s"] for r in reps])) * 1e3, 3),
+                   rank_elapsed_s=[round(v, 4) for v in grank], engine_direct=engine_direct)
+        out["config"]["serving"] = (f"gRPC Generate (in-process server, {local_batch} concurrent requests per step "
+                                    f"from a separate client process); engine_direct = the same engine stepped "
+                                    f"directly")
+        out["served_over_engine"] = round(out["value"] / engine_direct["value"], 4)
+        progress(f"served over gRPC: {out['value']} tok/s = {out['served_over_engine']:.1%} of engine-direct "
+                 f"{engine_direct['value']}")
     del eng, model
     return out
 

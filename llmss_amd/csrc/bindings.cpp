@@ -71,6 +71,7 @@ void launch_add_norm_partial(const void* part, int S, int64_t slab, const void* 
 void launch_sample(const void* logits, int64_t ld, bool fp32_logits, int B, int V, const void* temperature,
                    const void* top_k, const void* top_p, const void* seeds, void* out, void* out2, hipStream_t st);
 void launch_quant_fp8_rows(const void* w, void* q, void* scale, int64_t N, int64_t K, hipStream_t st);
+void launch_quant_fp8_rows_ld(const void* x, int64_t ldx, void* q, void* scale, int64_t M, int64_t K, hipStream_t st);
 void launch_dequant_fp8_rows(const void* q, const void* scale, void* w, int64_t N, int64_t K, hipStream_t st);
 
 void register_runtime(py::module_& m);  // host-side C++ runtime (runtime.cpp)
@@ -189,6 +190,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("quant_fp8_rows", [](uintptr_t w, uintptr_t q, uintptr_t scale, int64_t N, int64_t K, uintptr_t st) {
     launch_quant_fp8_rows(CP(w), P(q), P(scale), N, K, S(st));
   });
+  m.def("quant_fp8_rows_ld", [](uintptr_t x, int64_t ldx, uintptr_t q, uintptr_t scale, int64_t M, int64_t K,
+                                uintptr_t st) { launch_quant_fp8_rows_ld(CP(x), ldx, P(q), P(scale), M, K, S(st)); });
   m.def("dequant_fp8_rows", [](uintptr_t q, uintptr_t scale, uintptr_t w, int64_t N, int64_t K, uintptr_t st) {
     launch_dequant_fp8_rows(CP(q), CP(scale), P(w), N, K, S(st));
   });

@@ -40,6 +40,62 @@ void launch_quant_fp8_rows(const void* w, void* q, void* scale, int64_t N, int64
   HIP_CHECK_LAUNCH();
 }
 
+// Per-token activation quantisation for W8A8 GEMMs (x rows with a leading dimension): one pass, the
+// row stays in registers between the absmax reduction and the conversion (K <= 8192; longer rows take
+// the two-pass kernel above). Writes q [M, K] (dense) and scale [M].
+template <int CH>
+__global__ __launch_bounds__(256) void quant_fp8_act_kernel(const bf16_t* __restrict__ x, int64_t ldx,
+                                                           unsigned char* __restrict__ q, float* __restrict__ scale,
+                                                           int K) {
+  __shared__ float red[16];
+  const int64_t r = blockIdx.x;
+  const bf16_t* xr = x + r * ldx;
+  u16x8 v[CH];
+  float amax = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int k = (c * 256 + threadIdx.x) * 8;
+    if (k < K) {
+      v[c] = *reinterpret_cast<const u16x8*>(xr + k);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(bf2f(v[c][j])));
+    }
+  }
+  amax = block_max(amax, red);
+  const float s = amax > 0.f ? amax / 448.f : 1.f;
+  const float inv = 1.f / s;
+  if (threadIdx.x == 0) scale[r] = s;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int k = (c * 256 + threadIdx.x) * 8;
+    if (k < K) {
+      float f[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = fminf(fmaxf(bf2f(v[c][j]) * inv, -448.f), 448.f);
+      unsigned lo = 0, hi = 0;
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], lo, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], hi, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
+      *reinterpret_cast<uint2*>(q + r * (int64_t)K + k) = make_uint2(lo, hi);
+    }
+  }
+}
+
+void launch_quant_fp8_rows_ld(const void* x, int64_t ldx, void* q, void* scale, int64_t M, int64_t K, hipStream_t st) {
+  if (K % 8 || ldx % 8) throw std::runtime_error("quant_fp8_rows_ld: K and the row stride must be multiples of 8");
+  if (M == 0) return;
+  auto X = (const bf16_t*)x;
+  auto Q = (unsigned char*)q;
+  auto S = (float*)scale;
+  if (K <= 2048) quant_fp8_act_kernel<1><<<(unsigned)M, 256, 0, st>>>(X, ldx, Q, S, (int)K);
+  else if (K <= 4096) quant_fp8_act_kernel<2><<<(unsigned)M, 256, 0, st>>>(X, ldx, Q, S, (int)K);
+  else if (K <= 8192) quant_fp8_act_kernel<4><<<(unsigned)M, 256, 0, st>>>(X, ldx, Q, S, (int)K);
+  else if (ldx == K) quant_fp8_rows_kernel<<<(unsigned)M, 256, 0, st>>>(X, Q, S, K);
+  else throw std::runtime_error("quant_fp8_rows_ld: rows longer than 8192 must be contiguous");
+  HIP_CHECK_LAUNCH();
+}
+
 // w[r, :] = q[r, :] * scale[r] -> bf16. Prefill with fp8 weights (M > 128) is compute-bound, so the
 // weight is expanded once per call into a bf16 scratch and the big-tile bf16 GEMM runs on it
 // (100 MB of fp8 -> ~40 us, vs ~0.75 ms for the GEMM it feeds at 8K tokens).

@@ -62,6 +62,14 @@ def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, 
     if fp8:  # tiled kernel with fp8 weight tiles (no stream-K / big-tile variants)
         if M > 16:
             out += [((t | d) << 8, s) for t, d in ((3, 16), (3, 32), (2, 16), (2, 32)) for s in splits]
+        if M >= 32:  # W8A8: per-token fp8 activations on the MX-fp8 matrix cores (ops/hip.py W8A8_FLAG)
+            from .hip import W8A8_FLAG
+
+            tiles = [3, 2] + ([1] if M > 64 else [])
+            out += [(W8A8_FLAG | (t << 8) | (d << 12), s) for t in tiles for d in (2, 3, 4) for s in splits
+                    if not (t == 1 and d > 3)]
+            if M >= 256 and K % 128 == 0:
+                out.append((W8A8_FLAG | (4 << 8), 1))
         return out
     # tiled: tile << 8 | depth code << 12   (tile 1: 128x128, 2: 64x128, 3: 64x64; depth 2/3/4/6)
     tiles = [(3, (0, 16, 32, 48)), (2, (0, 16, 32))]

@@ -365,7 +365,34 @@ class PartialSum:
         return True
 
 
-_FP8_PREFILL_M = 128  # above this, fp8 weights are expanded to bf16 and the compute-bound tile kernels run
+_FP8_PREFILL_M = 128  # untuned fp8 calls above this M run W8A8 (compute-bound); below, W8A16 weight streaming
+
+# nt_hint flag of a W8A8 plan (the tuned table's fp8 entries or an explicit hint): tile = (nt >> 8) & 15
+# (1 128x128, 2 64x128, 3 64x64, 4 256x256), ring depth = (nt >> 12) & 15, split-K = the plan's split
+W8A8_FLAG = 1 << 20
+
+
+class _QuantScratch:
+    """Per-token fp8 activations + scales for W8A8 calls: one buffer reused by every call on the stream (each
+    GEMM consumes it before the next quantisation), grown only outside graph capture, so a captured decode
+    step quantises into the same addresses on every replay."""
+
+    def __init__(self):
+        self.q = None
+        self.s = None
+
+    def get(self, M, K, device):
+        if self.q is None or self.q.numel() < M * K or self.s.numel() < M or self.q.device != device:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError(f"fp8 activation scratch for [{M}, {K}] must be allocated before graph capture")
+            nq = max(M * K, 0 if self.q is None else self.q.numel())
+            ns = max(M, 0 if self.s is None else self.s.numel())
+            self.q = torch.empty(nq, dtype=torch.uint8, device=device)
+            self.s = torch.empty(ns, dtype=torch.float32, device=device)
+        return self.q[:M * K].view(M, K), self.s[:M]
+
+
+_QSCRATCH = _QuantScratch()
 
 
 class _DequantScratch:
@@ -385,16 +412,19 @@ _W8A8 = os.environ.get("LLMSS_FP8_W8A8", "1") != "0"
 
 
 def linear_w8a8(x, wq, w_scale, bias=None, act="none", glu=False, out=None, tile=0, depth=0, split=0):
-    """Y = (fp8(x) . wq^T) * x_scale[m] * w_scale[n] on the MX-fp8 MFMA (2x the bf16 matrix rate)."""
+    """Y = (fp8(x) . wq^T) * x_scale[m] * w_scale[n] on the MX-fp8 MFMA (2x the bf16 matrix rate). The
+    activations are quantised per token into a reusable scratch (graph-capturable)."""
     M, K = x.shape
     N = wq.shape[0]
+    _bf16_rows(x, "x")
     _check(wq.dtype == torch.uint8 and wq.is_contiguous() and K % 16 == 0 and wq.shape[1] == K, "fp8 weight")
     _check(w_scale.dtype == torch.float32 and w_scale.numel() == N, "w_scale [N] fp32")
     if glu:
         _check(N % 32 == 0, "glu needs N % 32 == 0")
     if bias is not None:
         _check(bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.numel() == N, "bias [N] bf16")
-    xq, xs = quant_fp8_rows(x.contiguous())
+    xq, xs = _QSCRATCH.get(M, K, x.device)
+    lib().quant_fp8_rows_ld(x.data_ptr(), x.stride(0), xq.data_ptr(), xs.data_ptr(), M, K, _stream())
     nout = N // 2 if glu else N
     y = out if out is not None else torch.empty(M, nout, dtype=torch.bfloat16, device=x.device)
     _bf16_rows(y, "out", nout)
@@ -460,7 +490,12 @@ def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hi
         _check(w.dtype == torch.uint8 and w.is_contiguous() and w.is_cuda, "fp8 weight stored as uint8 [N, K]")
         _check(w_scale.dtype == torch.float32 and w_scale.numel() == w.shape[0], "w_scale [N] fp32")
         tuned = lib().gemm_tuned_get(M, w.shape[0], K, bool(glu), 1) if not nt_hint else None
-        if M > _FP8_PREFILL_M and not nt_hint and tuned is None and not torch.cuda.is_current_stream_capturing():
+        if tuned is not None and tuned[0] & W8A8_FLAG:  # the autotuner picked W8A8 for this M
+            nt_hint, split_hint = tuned
+        if nt_hint & W8A8_FLAG:
+            return linear_w8a8(x, w, w_scale, bias, act, glu, out, (nt_hint >> 8) & 15, (nt_hint >> 12) & 15,
+                               split_hint)
+        if M > _FP8_PREFILL_M and not nt_hint and tuned is None:
             if _W8A8:  # compute-bound: per-token fp8 activations on the MX-fp8 matrix cores
                 return linear_w8a8(x, w, w_scale, bias, act, glu, out)
             wd = _DEQ.get(w.numel(), x.device)[: w.numel()].view(w.shape)

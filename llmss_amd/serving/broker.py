@@ -48,6 +48,17 @@ class Broker:
         """Blocking right-pop; ``timeout`` seconds (0 = forever). Returns the value or None."""
         raise NotImplementedError
 
+    def brpoplpush(self, src: str, dst: str, timeout: float = 0) -> Optional[str]:
+        """Pop the tail of ``src`` and push it onto the head of ``dst`` in one step (Redis BRPOPLPUSH): a
+        consumer's in-flight request stays in its processing list until it is acknowledged with lrem."""
+        raise NotImplementedError
+
+    def lrem(self, key: str, count: int, value: str) -> int:
+        raise NotImplementedError
+
+    def lrange(self, key: str, start: int, stop: int) -> List[str]:
+        raise NotImplementedError
+
     def delete(self, key: str) -> int:
         raise NotImplementedError
 
@@ -114,6 +125,45 @@ class MemoryBroker(Broker):
     def delete(self, key):
         with self._cv:
             return 1 if self._lists.pop(key, None) is not None else 0
+
+    def brpoplpush(self, src, dst, timeout=0):
+        deadline = None if not timeout else time.monotonic() + timeout
+        with self._cv:
+            while True:
+                q = self._lists.get(src)
+                if q:
+                    v = q.pop()
+                    self._lists[dst].appendleft(v)
+                    self._cv.notify_all()
+                    return v
+                rem = None if deadline is None else deadline - time.monotonic()
+                if rem is not None and rem <= 0:
+                    return None
+                self._cv.wait(rem)
+
+    def lrem(self, key, count, value):
+        """Remove up to ``count`` occurrences of ``value`` (0 = all; < 0 = from the tail), like Redis."""
+        with self._cv:
+            q = self._lists.get(key)
+            if not q:
+                return 0
+            items = list(q)
+            idx = [i for i, v in enumerate(items) if v == value]
+            if count < 0:
+                idx = idx[::-1][:-count]
+            elif count > 0:
+                idx = idx[:count]
+            drop = set(idx)
+            self._lists[key] = deque(v for i, v in enumerate(items) if i not in drop)
+            return len(drop)
+
+    def lrange(self, key, start, stop):
+        with self._cv:
+            items = list(self._lists.get(key, ()))
+        n = len(items)
+        start = max(0, start + n if start < 0 else start)
+        stop = stop + n if stop < 0 else stop
+        return items[start:stop + 1]
 
 
 # ------------------------------------------------------------------------------- RESP client
@@ -221,6 +271,15 @@ class RedisBroker(Broker):
     def delete(self, key):
         return self.execute("DEL", key)
 
+    def brpoplpush(self, src, dst, timeout=0):
+        return self.execute("BRPOPLPUSH", src, dst, _fmt_timeout(timeout))
+
+    def lrem(self, key, count, value):
+        return self.execute("LREM", key, int(count), value)
+
+    def lrange(self, key, start, stop):
+        return self.execute("LRANGE", key, int(start), int(stop)) or []
+
     def close(self):
         c = getattr(self._local, "conn", None)
         if c is not None:
@@ -308,6 +367,20 @@ class MiniRedisServer:
                     return ("array", [keys[0], v])
         if op == "DEL":
             return sum(store.delete(k) for k in a)
+        if op == "BRPOPLPUSH":
+            t = float(a[2])
+            deadline = None if t == 0 else time.monotonic() + t
+            while True:  # bounded waits so a stopping server is not held by an idle client
+                rem = None if deadline is None else deadline - time.monotonic()
+                if rem is not None and rem <= 0:
+                    return ("bulk", None)
+                v = store.brpoplpush(a[0], a[1], min(rem, 0.05) if rem is not None else 0.05)
+                if v is not None:
+                    return ("bulk", v)
+        if op == "LREM":
+            return store.lrem(a[0], int(a[1]), a[2])
+        if op == "LRANGE":
+            return ("array", store.lrange(a[0], int(a[1]), int(a[2])))
         raise RuntimeError(f"ERR unknown command {op}")
 
     @staticmethod

@@ -2,17 +2,24 @@
 
 Reference: consumer_server.py - rank 0 ``RPOP pqueue`` when ``LLEN`` > 0, ``batch_size = 1``, a
 spinning ``broadcast_object_list`` every idle iteration, one request decoded to completion before
-the next is popped, reply ``LPUSH squeue``.
+the next is popped, reply ``LPUSH squeue``; a consumer that dies loses the request it popped
+(``consumer_server.py:79-80``).
 
-Here rank 0 runs an intake thread that blocks on ``BRPOP pqueue`` and submits every request to the
-:class:`EngineDriver` immediately, so concurrent requests share continuous-batching decode steps;
-each completion is pushed to ``squeue:<request_id>`` (or plain ``squeue`` when the request came
-from a reference producer without an id). All ranks run the driver loop; followers block on the
-CPU control group between bursts of work.
+Here rank 0 runs an intake thread that blocks on ``BRPOPLPUSH pqueue -> pqueue:processing:<id>`` and
+submits every request to the :class:`EngineDriver` immediately, so concurrent requests share
+continuous-batching decode steps; each completion is pushed to ``squeue:<request_id>`` (or plain
+``squeue`` when the request came from a reference producer without an id) and only then removed
+from the processing list (``LREM``). A consumer restarted under the same ``consumer_id`` first moves
+whatever its previous incarnation left in that list back onto ``pqueue`` - a crash no longer loses
+in-flight requests. Streaming requests (``"stream": true``) get one message per engine step with
+that step's tokens, then the final message. Replies are written by a publisher thread, so the
+engine loop never waits on the broker. All ranks run the driver loop; followers block on the CPU
+control group between bursts of work.
 """
 from __future__ import annotations
 
 import json
+import queue
 import threading
 from typing import Optional
 
@@ -25,31 +32,108 @@ from .protocol import dump_response, parse_request, to_sampling
 log = get_logger(__name__)
 
 
+def processing_key(consumer_id: str) -> str:
+    return f"{PQUEUE}:processing:{consumer_id}"
+
+
 class Consumer:
-    def __init__(self, driver: EngineDriver, tokenizer, broker: Optional[Broker] = None, poll_timeout: float = 1.0):
+    def __init__(self, driver: EngineDriver, tokenizer, broker: Optional[Broker] = None, poll_timeout: float = 1.0,
+                 consumer_id: str = "0", durable: bool = True):
         self.driver = driver
         self.tok = tokenizer
         self.broker = broker
         self.poll_timeout = poll_timeout
+        self.consumer_id = str(consumer_id)
+        self.durable = durable
         self._stop = threading.Event()
+        self._out: "queue.Queue" = queue.Queue()
         self.served = 0
+        self.requeued = 0
+
+    # ------------------------------------------------------------------ publisher thread
+    def _publish_loop(self):
+        """Drain everything queued, merge each streaming request's tokens into one message per drain (order
+        kept per request: its pending tokens go out before its final reply), publish."""
+        while True:
+            batch = [self._out.get()]
+            while True:
+                try:
+                    batch.append(self._out.get_nowait())
+                except queue.Empty:
+                    break
+            pending = {}  # id(req) -> (req, tokens)
+
+            def flush(key=None):
+                for k in ([key] if key is not None else list(pending)):
+                    if k in pending:
+                        req, toks = pending.pop(k)
+                        self.broker.lpush(reply_key(req.request_id),
+                                          json.dumps({"token_ids": toks, "text": self.tok.decode(toks)}))
+            try:
+                for item in batch:
+                    if item is None:
+                        flush()
+                        return
+                    kind = item[0]
+                    if kind == "tokens":
+                        _, req, toks = item
+                        pending.setdefault(id(req), (req, []))[1].extend(toks)
+                    elif kind == "done":
+                        _, req, h, raw = item
+                        flush(id(req))
+                        self._reply(req, h)
+                        if raw is not None and self.durable:
+                            self.broker.lrem(processing_key(self.consumer_id), 1, raw)  # acknowledged
+                    elif kind == "error":
+                        _, rid, err, raw = item
+                        self.broker.lpush(reply_key(rid), json.dumps({"prompt": "", "continuation": "", "error": err}))
+                        if raw is not None and self.durable:
+                            self.broker.lrem(processing_key(self.consumer_id), 1, raw)
+                flush()
+            except Exception:  # noqa: BLE001 - a broker hiccup must not kill the publisher
+                log.exception("consumer publish failed")
 
     def _reply(self, req, h: Handle):
         m = h.metrics or {}
         resp = {"prompt": req.prompt, "continuation": self.tok.decode(h.output_ids)}
         if req.request_id:
             resp.update(request_id=req.request_id, output_tokens=len(h.output_ids), token_ids=list(h.output_ids),
-                        finish_reason=h.finish_reason,
-                        ttft_s=m.get("ttft_s"), e2e_s=m.get("e2e_s"))
+                        finish_reason=h.finish_reason, ttft_s=m.get("ttft_s"), e2e_s=m.get("e2e_s"))
+            if req.stream:
+                resp.update(finished=True, text="")
+        if h.finish_reason == "error":
+            resp["error"] = h.error or "engine failure"
         self.broker.lpush(reply_key(req.request_id), dump_response(resp))
         self.served += 1
 
+    # ------------------------------------------------------------------ intake
+    def recover(self) -> int:
+        """Put back on pqueue what a previous consumer with this id left unacknowledged (it crashed or was
+        killed mid-request). RPUSH: the recovered requests are popped next (consumers pop the tail)."""
+        if not self.durable:
+            return 0
+        key = processing_key(self.consumer_id)
+        n = 0
+        for raw in reversed(self.broker.lrange(key, 0, -1)):  # oldest (tail) first back to the pop end
+            self.broker.rpush(PQUEUE, raw)
+            n += 1
+        self.broker.delete(key)
+        if n:
+            log.warning("consumer %s: re-queued %d unacknowledged request(s)", self.consumer_id, n)
+        self.requeued += n
+        return n
+
     def intake_loop(self):
         """Rank 0: broker -> engine (non-spinning blocking pop)."""
+        pk = processing_key(self.consumer_id)
         while not self._stop.is_set():
-            msg = self.broker.brpop(PQUEUE, timeout=self.poll_timeout)
+            if self.durable:
+                msg = self.broker.brpoplpush(PQUEUE, pk, timeout=self.poll_timeout)
+            else:
+                msg = self.broker.brpop(PQUEUE, timeout=self.poll_timeout)
             if msg is None:
                 continue
+            raw = msg if self.durable else None
             try:
                 req = parse_request(msg)
                 params = to_sampling(req)
@@ -59,16 +143,26 @@ class Consumer:
                     rid = json.loads(msg).get("request_id")
                 except Exception:  # noqa: BLE001
                     rid = None
-                self.broker.lpush(reply_key(rid), json.dumps({"prompt": "", "continuation": "", "error": str(e)}))
+                self._out.put(("error", rid, str(e), raw))
                 continue
-            ids = encode(self.tok, req.prompt)
-            self.driver.submit(ids, params, on_done=lambda h, req=req: self._reply(req, h))
+            ids = list(req.prompt_token_ids) if req.prompt_token_ids else encode(self.tok, req.prompt)
+            on_token = None
+            if req.stream and req.request_id:
+                def on_token(h, t, req=req):
+                    self._out.put(("tokens", req, [int(t)]))
+            self.driver.submit(ids, params, on_done=lambda h, req=req, raw=raw: self._out.put(("done", req, h, raw)),
+                               on_token=on_token)
 
     def start(self):
         if self.driver.leader:
+            self.recover()
+            self._pub = threading.Thread(target=self._publish_loop, daemon=True, name="broker-publish")
+            self._pub.start()
             self._intake = threading.Thread(target=self.intake_loop, daemon=True, name="broker-intake")
             self._intake.start()
         return self
 
     def stop(self):
         self._stop.set()
+        if self.driver.leader:
+            self._out.put(None)

@@ -51,6 +51,10 @@ class Handle:
     finish_reason: str = ""
     metrics: Dict[str, float] = field(default_factory=dict)
     on_done: Optional[Callable[["Handle"], None]] = None
+    # streaming consumers only: tokens are queued for stream() (gRPC GenerateStream) and/or handed to
+    # on_token; a unary request just accumulates output_ids (no per-token queue hop)
+    stream: bool = False
+    on_token: Optional[Callable[["Handle", int], None]] = None
     t_submit: float = field(default_factory=time.perf_counter)
     deadline: Optional[float] = None  # perf_counter time after which the request is aborted
     error: str = ""
@@ -58,7 +62,10 @@ class Handle:
     def wait(self, timeout: Optional[float] = None) -> bool:
         return self.done.wait(timeout)
 
-    def stream(self):
+    def iter_tokens(self):
+        """Tokens as they are sampled (submit(..., stream=True)); ends when the request finishes."""
+        if not self.stream:
+            raise RuntimeError("iter_tokens() needs a handle submitted with stream=True")
         while True:
             t = self.tokens.get()
             if t is None:
@@ -100,6 +107,10 @@ class EngineDriver:
         self._thread: Optional[threading.Thread] = None
         self._lock = threading.Lock()
         self.idle_wait_s = 0.05
+        # admission window: an idle leader that wakes on a request keeps collecting arrivals until none
+        # came for `batch_window_s` (at most 10 windows), so a burst of concurrent clients is admitted in
+        # one prefill step instead of trickling in one by one
+        self.batch_window_s = float(os.environ.get("LLMSS_ADMIT_WINDOW_S", "0.002"))
         self.fault = fault if fault is not None else FaultSpec.from_env()
         self.error: Optional[BaseException] = None
         self._last_bcast = time.perf_counter()
@@ -114,14 +125,15 @@ class EngineDriver:
 
     # --------------------------------------------------------------------- leader API
     def submit(self, prompt_ids: List[int], params: SamplingParams,
-               on_done: Optional[Callable[[Handle], None]] = None, deadline_s: Optional[float] = None) -> Handle:
+               on_done: Optional[Callable[[Handle], None]] = None, deadline_s: Optional[float] = None,
+               stream: bool = False, on_token: Optional[Callable[[Handle, int], None]] = None) -> Handle:
         if not self.leader:
             raise RuntimeError("submit() is only valid on rank 0")
         params.resolved_seed()  # fix the seed on the leader so every rank uses the same one
         with self._lock:
             rid = self._next
             self._next += self._rid_stride
-        h = Handle(rid, list(prompt_ids), params, on_done=on_done)
+        h = Handle(rid, list(prompt_ids), params, on_done=on_done, stream=stream, on_token=on_token)
         if deadline_s is not None:
             h.deadline = h.t_submit + deadline_s
         if self.error is not None:  # the driver already failed: refuse instead of queueing forever
@@ -181,6 +193,7 @@ class EngineDriver:
         new, aborts, stop = [], [], False
         try:
             item = self.inbox.get(timeout=self.idle_wait_s) if block else self.inbox.get_nowait()
+            t_end = time.perf_counter() + 10 * self.batch_window_s
             while True:
                 kind, v = item
                 if kind == "new":
@@ -189,7 +202,12 @@ class EngineDriver:
                     aborts.append(v)
                 elif kind == "stop":
                     stop = True
-                item = self.inbox.get_nowait()
+                try:
+                    item = self.inbox.get_nowait()
+                except queue.Empty:
+                    if not (block and self.batch_window_s > 0 and new and not stop) or time.perf_counter() > t_end:
+                        raise
+                    item = self.inbox.get(timeout=self.batch_window_s)
         except queue.Empty:
             pass
         now = time.perf_counter()
@@ -258,7 +276,10 @@ class EngineDriver:
                     if h is None:
                         continue
                     h.output_ids.append(ev.token)
-                    h.tokens.put(ev.token)
+                    if h.stream:
+                        h.tokens.put(ev.token)
+                    if h.on_token is not None:
+                        h.on_token(h, ev.token)
                     if ev.finished:
                         self._complete(h, ev.finish_reason)
             for r in eng.pop_finished():
@@ -269,7 +290,8 @@ class EngineDriver:
         h.finish_reason = reason
         if req is not None:
             h.metrics = req.metrics()
-        h.tokens.put(None)
+        if h.stream:
+            h.tokens.put(None)
         h.done.set()
         self.handles.pop(h.rid, None)
         if h.on_done is not None:

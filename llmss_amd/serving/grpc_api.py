@@ -37,7 +37,7 @@ def _build_pool():
     S, I32, I64, B, FL = _F.TYPE_STRING, _F.TYPE_INT32, _F.TYPE_INT64, _F.TYPE_BOOL, _F.TYPE_FLOAT
     msg("GenerateRequest", [("prompt", S, 0), ("max_new_tokens", I32, 0), ("is_greedy", B, 0), ("temperature", FL, 0),
                             ("top_p", FL, 0), ("top_k", I32, 0), ("request_id", S, 0), ("seed", I64, 0),
-                            ("prompt_token_ids", I32, 1)])
+                            ("prompt_token_ids", I32, 1), ("ignore_eos", B, 0)])
     msg("GenerateResponse", [("prompt", S, 0), ("continuation", S, 0), ("request_id", S, 0), ("token_ids", I32, 1),
                              ("finish_reason", S, 0), ("ttft_s", FL, 0), ("e2e_s", FL, 0)])
     msg("Token", [("token_id", I32, 0), ("text", S, 0), ("finished", B, 0), ("finish_reason", S, 0)])
@@ -70,7 +70,7 @@ def _params(req):
     # (0 is invalid for them) and "disabled" for top_k (as in the reference CLI, generate.py:30).
     return SamplingParams(max_new_tokens=req.max_new_tokens or 20, is_greedy=req.is_greedy,
                           temperature=req.temperature or 1.0, top_p=req.top_p or 0.95, top_k=req.top_k,
-                          seed=req.seed or None).validate()
+                          seed=req.seed or None, ignore_eos=req.ignore_eos).validate()
 
 
 def add_servicer(server: grpc.Server, servicer) -> None:
@@ -148,12 +148,12 @@ class EngineServicer:
             params = _params(req)
         except ValueError as e:
             ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
-        h = self.driver.submit(self._prompt_ids(req), params, deadline_s=ctx.time_remaining())
+        h = self.driver.submit(self._prompt_ids(req), params, deadline_s=ctx.time_remaining(), stream=True)
         ctx.add_callback(lambda: (not h.done.is_set()) and self.driver.abort(h.rid))
         from ..utils.tokenizer import StreamDecoder
 
         dec = StreamDecoder(self.tok)  # one short-window decode per token, not the whole prefix again
-        for t in h.stream():
+        for t in h.iter_tokens():
             yield Token(token_id=t, text=dec.push(t), finished=False)
         yield Token(token_id=-1, text=dec.flush(), finished=True, finish_reason=h.finish_reason)
 
@@ -173,16 +173,23 @@ class BrokerServicer:
         self.timeout = default_timeout
         self.stats = {"requests": 0, "timeouts": 0}
 
+    @staticmethod
+    def _body(req, rid, stream=False):
+        from .protocol import Request
+
+        return Request(prompt=req.prompt, max_new_tokens=req.max_new_tokens or 20, is_greedy=req.is_greedy,
+                       temperature=req.temperature or 1.0, top_p=req.top_p or 0.95, top_k=req.top_k or 50,
+                       request_id=rid, seed=req.seed or None, ignore_eos=req.ignore_eos, stream=stream,
+                       prompt_token_ids=list(req.prompt_token_ids) or None)
+
     def Generate(self, req, ctx):
         from .broker import PQUEUE, reply_key
-        from .protocol import Request, new_request_id
+        from .protocol import new_request_id
 
         rid = req.request_id or new_request_id()
-        body = Request(prompt=req.prompt, max_new_tokens=req.max_new_tokens or 20, is_greedy=req.is_greedy,
-                       temperature=req.temperature or 1.0, top_p=req.top_p or 0.95, top_k=req.top_k or 50,
-                       request_id=rid, seed=req.seed or None)
+        body = self._body(req, rid)
         t0 = time.perf_counter()
-        self.broker.lpush(PQUEUE, body.model_dump_json())
+        self.broker.lpush(PQUEUE, body.model_dump_json(exclude_none=True))
         self.stats["requests"] += 1
         remaining = ctx.time_remaining()
         msg = self.broker.brpop(reply_key(rid), timeout=remaining if remaining else self.timeout)
@@ -195,8 +202,31 @@ class BrokerServicer:
                                 e2e_s=float(time.perf_counter() - t0))
 
     def GenerateStream(self, req, ctx):
-        r = self.Generate(req, ctx)
-        yield Token(token_id=-1, text=r.continuation, finished=True, finish_reason=r.finish_reason)
+        """Streams through the broker: the consumer pushes the tokens of every engine step to the
+        request's reply list as they are sampled ({"token_ids": [...], "text": ...}), then a final
+        message with "finished"; each token becomes one Token message here."""
+        from .broker import PQUEUE, reply_key
+        from .protocol import new_request_id
+
+        rid = req.request_id or new_request_id()
+        self.broker.lpush(PQUEUE, self._body(req, rid, stream=True).model_dump_json(exclude_none=True))
+        self.stats["requests"] += 1
+        remaining = ctx.time_remaining()
+        deadline = time.monotonic() + (remaining if remaining else self.timeout)
+        while True:
+            msg = self.broker.brpop(reply_key(rid), timeout=max(0.001, deadline - time.monotonic()))
+            if msg is None:
+                self.stats["timeouts"] += 1
+                ctx.abort(grpc.StatusCode.DEADLINE_EXCEEDED, "no reply from consumer")
+            d = json.loads(msg)
+            if d.get("error"):
+                ctx.abort(grpc.StatusCode.UNAVAILABLE, d["error"])
+            if d.get("finished"):
+                yield Token(token_id=-1, text=d.get("text", ""), finished=True, finish_reason=d.get("finish_reason", ""))
+                return
+            ids = d.get("token_ids") or []
+            for j, t in enumerate(ids):
+                yield Token(token_id=int(t), text=d.get("text", "") if j == len(ids) - 1 else "", finished=False)
 
     def Stats(self, req, ctx):
         return StatsResponse(json=json.dumps(self.stats))

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import json
 import uuid
-from typing import Any, Dict, Optional
+from typing import Any, Dict, List, Optional
 
 from pydantic import BaseModel
 
@@ -26,6 +26,10 @@ class Request(BaseModel):
     top_k: int = 50
     request_id: Optional[str] = None
     seed: Optional[int] = None
+    # extensions (absent from reference requests; a reference consumer ignores them)
+    ignore_eos: bool = False
+    stream: bool = False  # reply per engine step on squeue:<request_id>, then a final "finished" message
+    prompt_token_ids: Optional[List[int]] = None  # pre-tokenized prompt (prompt text ignored)
 
 
 class Response(BaseModel):
@@ -50,7 +54,7 @@ def parse_request(msg: str) -> Request:
 
 def to_sampling(req: Request) -> SamplingParams:
     return SamplingParams(max_new_tokens=req.max_new_tokens, is_greedy=req.is_greedy, temperature=req.temperature,
-                          top_p=req.top_p, top_k=req.top_k, seed=req.seed).validate()
+                          top_p=req.top_p, top_k=req.top_k, seed=req.seed, ignore_eos=req.ignore_eos).validate()
 
 
 def dump_response(resp: Dict[str, Any]) -> str:

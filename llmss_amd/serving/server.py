@@ -57,7 +57,8 @@ def _serve_replicas(driver, tok, args):
         broker_srv._thread.start()
     dist.barrier()  # the broker is listening before replicas connect
     if driver.leader:
-        Consumer(driver, tok, RedisBroker("127.0.0.1", args.broker_port)).start()
+        # one processing list per replica (durable hand-off, consumer.py)
+        Consumer(driver, tok, RedisBroker("127.0.0.1", args.broker_port), consumer_id=f"replica{g.replica}").start()
     if g.global_rank == 0:
         server = serve(BrokerServicer(RedisBroker("127.0.0.1", args.broker_port)), args.grpc_port, args.grpc_host)
         print(f"llmss gRPC Generate on {args.grpc_host}:{server.bound_port}: {g.dp} replicas x tp={g.size}", flush=True)

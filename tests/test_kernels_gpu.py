@@ -584,3 +584,56 @@ def test_gemm_w8a8_mx_fp8(tile, depth, split, M, N, K):
     # and close to the bf16-activation result: per-token fp8 activation error only (~3% relative RMS)
     ya, yr = H.linear(x, q, b, w_scale=s).float(), R.linear(x.float(), q, b.float(), w_scale=s)
     assert ((ya - yr).norm() / yr.norm()).item() < 0.05
+
+
+@pytest.mark.parametrize("K", [1024, 4096, 8192, 11008])
+def test_quant_fp8_activation_rows(K):
+    """Per-token activation quantisation (strided rows, one pass) == the two-pass weight quantiser."""
+    torch.manual_seed(1)
+    xf = rnd(37, K + 64)
+    x = xf[:, 32:32 + K] if K <= 8192 else xf[:, :K].contiguous()  # strided rows (one-pass kernel) or long rows
+    q = torch.empty(37, K, dtype=torch.uint8, device=dev)
+    s = torch.empty(37, dtype=torch.float32, device=dev)
+    H.lib().quant_fp8_rows_ld(x.data_ptr(), x.stride(0), q.data_ptr(), s.data_ptr(), 37, K, H._stream())
+    q_ref, s_ref = H.quant_fp8_rows(x.contiguous())
+    assert torch.equal(q, q_ref) and torch.equal(s, s_ref)
+
+
+@pytest.mark.parametrize("M", [64, 256, 512])
+def test_w8a8_decode_plan_in_graph(M):
+    """a tuned W8A8 plan (fp8 activations quantised into the reusable scratch, MX-fp8
+    MFMA) runs inside a captured HIP graph and replays exactly the eager values; both match fp32 math on
+    the same fp8 operands. The plan goes through the tuned table exactly as a decode step consults it."""
+    from llmss_amd import _native
+
+    torch.manual_seed(2)
+    N, K = 1024, 4096
+    w = rnd(N, K, scale=K ** -0.5)
+    q, s = H.quant_fp8_rows(w)
+    b = rnd(N, scale=0.1)
+    x = rnd(M, K)
+    lib = _native()
+    nt = H.W8A8_FLAG | (3 << 8) | (3 << 12)
+    lib.gemm_tuned_set(M, N, K, False, 1, nt, 2)
+    try:
+        eager = H.linear(x, q, b, w_scale=s)
+        y = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        g = torch.cuda.CUDAGraph()
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            H.linear(x, q, b, w_scale=s, out=y)
+        torch.cuda.current_stream().wait_stream(st)
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            H.linear(x, q, b, w_scale=s, out=y)
+        x2 = rnd(M, K)
+        x.copy_(x2)
+        y.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+    finally:
+        lib.gemm_tuned_clear()
+    xq, xs = H.quant_fp8_rows(x2)
+    ref = R.linear(R.dequant_fp8(xq, xs), q, b.float(), w_scale=s)
+    close(y, ref, 2e-2)
+    assert not torch.equal(eager, y)  # the replay read the new activations
