@@ -202,6 +202,8 @@ class LLMEngine:
         self.buckets = [b for b in self.buckets if b <= max_num_seqs] or [max_num_seqs]
         if self.buckets[-1] < max_num_seqs:
             self.buckets.append(max_num_seqs)
+        self._tbo_cands = self._tbo_candidates()
+        self.tbo_choice: Dict[int, bool] = {}  # bucket -> two-micro-batch graph chosen by the capture-time A/B
         self.tp.check_consistent("LLMEngine", self.fingerprint())
         self.buf = _DecodeBuffers(self.buckets[-1], self.max_blocks, self.device) if self.is_gpu else None
         if self.is_gpu:
@@ -263,13 +265,34 @@ class LLMEngine:
 
     def decode_batch_sizes(self) -> List[int]:
         """Row counts the decode kernels run at: every bucket, plus both micro-batch halves of the
-        buckets that DecoderLM splits for all-reduce / compute overlap."""
+        buckets that DecoderLM splits for all-reduce / compute overlap (or that the capture-time A/B
+        may split, _tbo_candidates)."""
         out = set(self.buckets)
         for b in self.buckets:
-            h = self.model.overlap_split(b)
+            h = self.model.overlap_split(b) or self._tbo_half(b)
             if h:
                 out.update((h, b - h))
         return sorted(out)
+
+    def _tbo_candidates(self) -> List[int]:
+        """Decode buckets whose two-micro-batch schedule is timed against the single-batch one at capture
+        (LLMSS_TBO_AUTO, default on): only with a real multi-rank communicator - on one GPU there is nothing
+        to overlap - and for buckets of >= LLMSS_TBO_AUTO_MIN (128) sequences."""
+        if not (self.is_gpu and self.tp.is_real and not self.tp.host_staged and self.model.tbo_min <= 0
+                and os.environ.get("LLMSS_TBO_AUTO", "1") != "0"):
+            return []
+        lo = int(os.environ.get("LLMSS_TBO_AUTO_MIN", "128"))
+        return [b for b in self.buckets if b >= lo]
+
+    def _tbo_half(self, b: int) -> int:
+        if b not in getattr(self, "_tbo_cands", ()):
+            return 0
+        m = self.model
+        old, m.tbo_min = m.tbo_min, b
+        try:
+            return m.overlap_split(b)
+        finally:
+            m.tbo_min = old
 
     def _splits(self, b):
         return _hip_ops.decode_splits(b, self.model.plan.nkv_l, self.max_model_len, self.block_size)
@@ -641,8 +664,80 @@ class LLMEngine:
                     self._decode_forward(b, buf, dist=d)
                 self.graphs[(b, d)] = g
         torch.cuda.synchronize()
+        if self._tbo_cands:
+            self._tbo_ab(pool, modes)
         log.info("captured %d decode graphs: buckets %s, samplers %s", len(self.graphs), self.buckets,
                  ["candidates" if d else "gathered" for d in modes])
+
+    def _tbo_ab(self, pool, modes):
+        """Capture-time A/B of the two-micro-batch decode schedule (each half's all-reduces on the comm stream
+        while the other half computes, DecoderLM._hidden_states_overlap) against the single-batch graphs, on
+        the real communicator: per candidate bucket both graphs are replayed with a realistic context length
+        (the bench's 128 + 64 average), every rank's times are gathered and the max over ranks decides, so all
+        ranks keep the same graph. The split loses on one GPU (half-batch kernels are nearly as long as full
+        ones, profiles/r1_tbo) and can win only where collectives cost real time - hence measured, not assumed."""
+        buf, m = self.buf, self.model
+        ctx = int(os.environ.get("LLMSS_TBO_AUTO_CTX", "192"))
+        ctx = max(1, min(ctx, self.max_model_len - 1))
+        nblk = -(-ctx // self.block_size)
+        if nblk > self.num_blocks:
+            return
+        alt = {}
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):  # eager warm-up of the split schedule (comm stream, half-batch workspaces)
+            for b in reversed(self._tbo_cands):
+                old, m.tbo_min = m.tbo_min, b
+                try:
+                    self._decode_forward(b, buf, dist=modes[0])
+                finally:
+                    m.tbo_min = old
+        torch.cuda.current_stream().wait_stream(st)
+        torch.cuda.synchronize()
+        for b in reversed(self._tbo_cands):
+            for d in modes:
+                old, m.tbo_min = m.tbo_min, b
+                try:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
+                        self._decode_forward(b, buf, dist=d)
+                finally:
+                    m.tbo_min = old
+                alt[(b, d)] = g
+        torch.cuda.synchronize()
+        # realistic rows for timing: every row attends `ctx` cached positions (garbage K/V, no cache writes)
+        buf.ctx.fill_(ctx)
+        buf.bt.zero_()
+        buf.bt[:, :nblk] = torch.arange(nblk, dtype=torch.int32, device=buf.bt.device)
+        times = {}
+        for (b, d), g_alt in alt.items():
+            g_one = self.graphs[(b, d)]
+            for g in (g_one, g_alt):  # warm both
+                g.replay()
+            torch.cuda.synchronize()
+            res = []
+            for g in (g_one, g_alt, g_one, g_alt):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(3):
+                    g.replay()
+                e.record()
+                e.synchronize()
+                res.append(s.elapsed_time(e) / 3)
+            times[(b, d)] = (min(res[0], res[2]), min(res[1], res[3]))
+        allt = self.tp.all_gather_object(times)
+        for key in times:
+            one = max(t[key][0] for t in allt)
+            two = max(t[key][1] for t in allt)
+            if two < 0.97 * one:
+                self.graphs[key] = alt[key]
+            self.tbo_choice[key[0]] = self.tbo_choice.get(key[0], False) or two < 0.97 * one
+            self.stats.setdefault("tbo_ab_ms", {})[f"{key[0]}{'c' if key[1] else 'g'}"] = [round(one, 3), round(two, 3)]
+        buf.ctx.zero_()
+        buf.bt.zero_()
+        torch.cuda.synchronize()
+        log.info("decode micro-batch overlap A/B (max over ranks, ms one/two micro-batches): %s",
+                 self.stats.get("tbo_ab_ms"))
 
     # -------------------------------------------------------------------------- offline API
     def generate(self, prompts: Iterable[Sequence[int]], params=None) -> List[List[int]]:

@@ -105,3 +105,43 @@ def test_tp_engine_with_native_comm_in_graphs(comm):
     del e_graph
     e_eager = LLMEngine(m, max_num_seqs=4, block_size=16, use_graphs=False, autotune=False)
     assert e_eager.generate(prompts, sp) == out_g
+
+
+def test_decode_overlap_ab_at_capture(comm, monkeypatch):
+    """The capture-time A/B of the two-micro-batch decode schedule runs on a native-comm TP group, records
+    both timings, keeps one graph per bucket, and whatever it keeps decodes exactly like eager."""
+    from llmss_amd.engine import LLMEngine, SamplingParams
+    from llmss_amd.models.config import get_preset
+    from llmss_amd.models.decoder import DecoderLM
+    from llmss_amd.models.weights import random_weights
+    from llmss_amd.parallel.dist import TPGroup
+
+    class OneRankNative(TPGroup):
+        def all_gather_last_dim(self, t):
+            t = t.contiguous()
+            out = torch.empty_like(t)
+            self.comm.all_gather(t.data_ptr(), out.data_ptr(), t.numel(), self._code(t), _st())
+            return torch.cat([out, out], -1)
+
+        def all_reduce_int(self, v, op="min"):
+            return int(v)
+
+        def check_consistent(self, what, fp):
+            pass
+
+        def all_gather_object(self, obj):
+            return [obj, obj]
+
+    monkeypatch.setenv("LLMSS_TBO_AUTO_MIN", "16")
+    tp = OneRankNative(0, 2, comm=comm)
+    cfg = get_preset("tiny-llama", hidden_size=256, num_heads=4, num_kv_heads=2, head_dim=64, rotary_dim=64,
+                     intermediate_size=512, max_position_embeddings=256)
+    m = DecoderLM(cfg, random_weights(cfg, 2, 0, device="cuda", dtype=torch.bfloat16, seed=5, std=0.05), tp)
+    prompts = [[int(x) for x in torch.randint(0, cfg.vocab_size, (n,))] for n in range(3, 23)]
+    sp = SamplingParams(max_new_tokens=10, is_greedy=True, ignore_eos=True)
+    e = LLMEngine(m, max_num_seqs=24, block_size=16, use_graphs=True, autotune=False, graph_buckets=[1, 8, 16, 24])
+    assert e._tbo_cands == [16, 24] and set(e.stats["tbo_ab_ms"]) >= {"16c", "24c"}
+    out_g = e.generate(prompts, sp)
+    del e
+    e2 = LLMEngine(m, max_num_seqs=24, block_size=16, use_graphs=False, autotune=False)
+    assert e2.generate(prompts, sp) == out_g

@@ -54,8 +54,7 @@ def test_forward_matches_reference(name):
     out = m_gpu(StepInput("prefill", ids.cuda(), pos.cuda(), slots.cuda(), cu_seqlens=cu.cuda(), max_seqlen=25,
                           last_idx=last.cuda()), kv_g)
     V = cfg.vocab_size
-    err = (out[:, :V].float().cpu() - ref[:, :V]).abs().max().item()
-    assert err < 0.05 * max(1.0, ref.abs().max().item()), err
+    _assert_logits_close(out[:, :V].float().cpu(), ref[:, :V])
     # single-sequence decode step after a prefill of 25 tokens
     dec_ids = torch.randint(0, V, (1,))
     kv_c = m_cpu.allocate_kv_cache(16, 16)
@@ -72,8 +71,25 @@ def test_forward_matches_reference(name):
     ref = m_cpu(StepInput(**d_in), kv_c)
     d_g = {k: (v.cuda() if torch.is_tensor(v) else v) for k, v in d_in.items()}
     out = m_gpu(StepInput(**d_g), kv_g)
-    err = (out[:, :V].float().cpu() - ref[:, :V]).abs().max().item()
-    assert err < 0.05 * max(1.0, ref.abs().max().item()), err
+    _assert_logits_close(out[:, :V].float().cpu(), ref[:, :V])
+
+
+def _assert_logits_close(got, ref):
+    """bf16 kernels vs the fp32 reference: per-row cosine > 0.999 and relative L2 error < 2%."""
+    cos = torch.nn.functional.cosine_similarity(got, ref.float(), dim=-1).min().item()
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert cos > 0.999 and rel < 0.02, (cos, rel)
+
+
+def _near_tie(m, ids, tol):
+    """Top-2 logit margin of the next token after ``ids`` (one prefill on the GPU model) is below ``tol``."""
+    T = len(ids)
+    x = torch.tensor(ids, device="cuda")
+    lg = m(StepInput("prefill", x, torch.arange(T, device="cuda"), torch.full((T,), -1, device="cuda"),
+                     cu_seqlens=torch.tensor([0, T], dtype=torch.int32, device="cuda"), max_seqlen=T,
+                     last_idx=torch.tensor([T - 1], device="cuda")), m.allocate_kv_cache(8, 16))
+    top2 = lg[0, :m.cfg.vocab_size].float().topk(2).values
+    return (top2[0] - top2[1]).item() < tol
 
 
 def test_engine_graph_vs_eager_and_batching():
@@ -89,11 +105,14 @@ def test_engine_graph_vs_eager_and_batching():
     e_eager = LLMEngine(m, max_num_seqs=8, block_size=16, use_graphs=False)
     out_e = e_eager.generate(prompts, sp)
     assert out_g == out_e
-    # one-at-a-time == batched (continuous batching must not change greedy results)
-    # (prefill may use a different GEMM kernel for a lone prompt, so allow rare bf16 argmax flips)
+    # one-at-a-time == batched (continuous batching must not change greedy results); a lone prompt may run a
+    # different GEMM kernel, so a flip is allowed only where the top-2 logit margin is within bf16 noise, and
+    # that sequence is compared no further
     singles = [e_eager.generate([p], sp)[0] for p in prompts]
-    agree = sum(a == b for s1, s2 in zip(singles, out_e) for a, b in zip(s1, s2)) / sum(len(s) for s in out_e)
-    assert agree > 0.8, agree
+    for p, s1, s2 in zip(prompts, singles, out_e):
+        k = next((i for i, (a, b) in enumerate(zip(s1, s2)) if a != b), None)
+        if k is not None:
+            assert _near_tie(m, p + s2[:k], 0.05), ("batched and single greedy runs differ at a clear margin", k)
     # sampled decoding is reproducible with fixed seeds
     sps = [SamplingParams(max_new_tokens=16, temperature=0.8, top_k=20, top_p=0.9, seed=11 + i, ignore_eos=True)
            for i in range(len(prompts))]

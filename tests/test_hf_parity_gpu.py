@@ -68,15 +68,26 @@ def test_native_bf16_matches_hf(tmp_path, name):
     # greedy continuations through the engine (paged decode, HIP graphs) vs HF generate
     eng = LLMEngine(m, max_num_seqs=4, block_size=16, autotune=False)
     out = eng.generate(ps, SamplingParams(max_new_tokens=10, is_greedy=True, ignore_eos=True))
-    agree = tot = 0
+    # margin-aware greedy agreement: every token must match HF's greedy token, except at a position where HF's
+    # own top-2 logit margin is within bf16 noise (a few times the measured prefill error): there a flip is a
+    # tie-break, and the rest of that sequence is conditioned on a different token, so comparison stops
+    noise = max(4 * float(err) * float(scale), 1e-3)
+    compared = ties = 0
     for p, o in zip(ps, out):
         with torch.no_grad():
             r = hf.generate(torch.tensor([p]), max_new_tokens=10, do_sample=False, min_new_tokens=10,
                             pad_token_id=0)[0, len(p):].tolist()
-        k = next((i for i, (a, b) in enumerate(zip(o, r)) if a != b), len(r))
-        agree += k
-        tot += len(r)
-    assert agree / tot >= 0.7, (name, out)
+            lg = hf(torch.tensor([p + r])).logits[0, len(p) - 1:len(p) + len(r) - 1]
+        top2 = lg.topk(2, dim=-1).values
+        margin = (top2[:, 0] - top2[:, 1]).tolist()
+        for i, (a, b) in enumerate(zip(o, r)):
+            if a == b:
+                compared += 1
+                continue
+            assert margin[i] < noise, (name, "greedy token differs at a clear margin", i, margin[i], noise, o, r)
+            ties += 1
+            break
+    assert compared >= 0.75 * 10 * len(ps), (name, compared, ties, out)
 
 
 def test_fp8_llama_end_to_end_vs_bf16(tmp_path):
