@@ -219,6 +219,8 @@ class LLMEngine:
             from ..ops.autotune import tune_model
 
             self.tuned = tune_model(model, self.decode_batch_sizes())
+        if self.is_gpu and autotune:
+            self._tune_gqa_attention()
         if self.use_graphs and os.environ.get("LLMSS_GRAPHS", "1") == "0":
             self.use_graphs = False
         if self.use_graphs:
@@ -273,6 +275,57 @@ class LLMEngine:
             if h:
                 out.update((h, b - h))
         return sorted(out)
+
+    def _tune_gqa_attention(self):
+        """For grouped-query models (>= 4 query heads per kv head, e.g. Llama-2-70B's 8, MQA's all) time the VALU
+        split-K decode kernel against the MFMA extend kernel per decode bucket on a synthetic cache (context
+        LLMSS_TBO_AUTO_CTX, default 192) and route the buckets where MFMA wins (DecoderLM.gqa_mfma). Every rank
+        sees the same shapes; the decision is agreed through all_reduce_int so the ranks run the same kernels."""
+        m, p, cfg = self.model, self.model.plan, self.cfg
+        if p.nh_l // max(1, p.nkv_l) < 4 or os.environ.get("LLMSS_GQA_MFMA", "auto") == "0":
+            return
+        if os.environ.get("LLMSS_GQA_MFMA") == "1":
+            m.gqa_mfma = set(self.decode_batch_sizes())
+            return
+        from ..ops.autotune import _time
+
+        D, dev = cfg.head_dim, self.device
+        ctx = max(1, min(int(os.environ.get("LLMSS_TBO_AUTO_CTX", "192")), self.max_model_len - 1))
+        nblk = -(-ctx // self.block_size)
+        res = {}
+        for b in self.decode_batch_sizes():
+            if b < 8:
+                continue
+            nb = b * nblk
+            kc = torch.randn(nb, p.nkv_l, self.block_size, D, device=dev).to(m.dtype) if not m.kv_fp8 else None
+            if kc is None:
+                return
+            vc = torch.randn_like(kc)
+            qkv = torch.randn(b, (p.nh_l + 2 * p.nkv_l) * D, device=dev).to(m.dtype)
+            bt = torch.arange(nb, dtype=torch.int32, device=dev).view(b, nblk)
+            bt = torch.nn.functional.pad(bt, (0, self.max_blocks - nblk))
+            cl = torch.full((b,), ctx, dtype=torch.int32, device=dev)
+            out = torch.empty(b, p.nh_l * D, dtype=m.dtype, device=dev)
+            cu = m.decode_cu(b, dev)
+            sp = self._splits(b)
+
+            def valu(i):
+                ops.attn_decode(qkv, kc, vc, bt, cl, p.nh_l, p.nkv_l, D, m.scale, self.max_model_len, splits=sp,
+                                out=out)
+
+            def mfma(i):
+                ops.attn_extend(qkv, kc, vc, bt, cu, cl, 1, p.nh_l, p.nkv_l, D, m.scale, out=out)
+            valu(0)
+            mfma(0)
+            torch.cuda.synchronize()
+            tv, tm = _time(valu, 8), _time(mfma, 8)
+            win = self.tp.all_reduce_int(int(tm < 0.97 * tv), "min")
+            if win:
+                m.gqa_mfma.add(b)
+            res[b] = (round(tv, 1), round(tm, 1))
+            del kc, vc
+        self.stats["gqa_attn_us"] = {str(b): v for b, v in res.items()}
+        log.info("GQA decode attention (us VALU split-K / MFMA extend): %s; MFMA for %s", res, sorted(m.gqa_mfma))
 
     def _tbo_candidates(self) -> List[int]:
         """Decode buckets whose two-micro-batch schedule is timed against the single-batch one at capture

@@ -106,6 +106,11 @@ class DecoderLM:
         # QKV GEMM epilogue with RoPE + paged KV write (one launch instead of two) wherever the autotuner
         # installed a faster plan for it (LLMSS_QKV_EPI=0: always GEMM + rope_cache)
         self.qkv_epi = os.environ.get("LLMSS_QKV_EPI", "1") != "0"
+        # decode batch sizes whose GQA attention runs on the MFMA extend kernel (one workgroup per kv head
+        # serving its whole query-head group: K/V staged once, QK^T and PV on the matrix cores) instead of
+        # the VALU split-K decode kernel; filled by LLMEngine's capture-time timing for G >= 4 groups
+        self.gqa_mfma: set = set()
+        self._cu_decode = {}
         self._comm_stream = None
 
     @property
@@ -163,6 +168,10 @@ class DecoderLM:
                 inp.block_tables, inp.ctx_lens, p.nh_l, p.nkv_l, D, cfg.rotary_dim, cfg.rope_style, self.scale,
                 inp.max_ctx, do_rope=do_rope, splits=inp.decode_splits)
         qkv = self._qkv_rope_cache(L, y, inp, kc, vc)
+        if inp.kind == "decode" and qkv.is_cuda and qkv.shape[0] in self.gqa_mfma:
+            B = qkv.shape[0]
+            return ops.attn_extend(qkv, kc, vc, inp.block_tables, self.decode_cu(B, qkv.device), inp.ctx_lens, 1,
+                                   p.nh_l, p.nkv_l, D, self.scale)
         if inp.kind == "prefill":
             return ops.attn_prefill(qkv, inp.cu_seqlens, inp.max_seqlen, p.nh_l, p.nkv_l, D, self.scale)
         if inp.kind == "extend":
@@ -187,6 +196,14 @@ class DecoderLM:
                 ops.attn_prefill(qkv[nd:], inp.cu_seqlens, inp.max_seqlen, p.nh_l, p.nkv_l, D, self.scale,
                                  out=out[nd:])
         return out
+
+    def decode_cu(self, B: int, device) -> torch.Tensor:
+        """[0, 1, .., B] int32: a decode step as B one-token 'chunks' (the extend kernel's cu_q); made once per B
+        outside graph capture (the engine's eager warm-up runs every bucket first)."""
+        cu = self._cu_decode.get((B, str(device)))
+        if cu is None:
+            cu = self._cu_decode[(B, str(device))] = torch.arange(B + 1, dtype=torch.int32, device=device)
+        return cu
 
     def bucket_rows(self, M: int) -> int:
         """Rows per all-reduce bucket of an M-row row-parallel output (>= M: one all-reduce)."""

@@ -368,3 +368,33 @@ def test_async_decode_matches_sync():
     b = _async_engine_run(m, prompts, sps, True, abort_after=4)
     assert a[0][1] == b[0][1] == "abort"
     assert a[1:] == b[1:] == ref[1:]
+
+
+@pytest.mark.parametrize("kv_heads", [1, 2])
+def test_gqa_decode_on_mfma_extend_kernel(kv_heads):
+    """GQA / MQA decode attention routed through the MFMA extend kernel (DecoderLM.gqa_mfma) == the VALU
+    split-K decode kernel, on a decode step after a prefill; and the engine's timed choice decodes the same
+    greedy tokens as the eager VALU path up to near-ties."""
+    cfg = get_preset("tiny-llama", hidden_size=512, num_heads=8, num_kv_heads=kv_heads, head_dim=64, rotary_dim=64,
+                     intermediate_size=512, max_position_embeddings=512)
+    m = DecoderLM(cfg, random_weights(cfg, device="cuda", dtype=torch.bfloat16, seed=9, std=0.05))
+    B, T0 = 6, 37
+    kv = m.allocate_kv_cache(64, 16)
+    ids = torch.randint(0, cfg.vocab_size, (B * T0,), device="cuda")
+    pos = torch.arange(T0, device="cuda").repeat(B)
+    slots = torch.cat([torch.arange(T0, device="cuda") + 16 * 4 * i for i in range(B)])
+    cu = torch.arange(0, B * T0 + 1, T0, dtype=torch.int32, device="cuda")
+    m(StepInput("prefill", ids, pos, slots, cu_seqlens=cu, max_seqlen=T0, last_idx=cu[1:].long() - 1), kv)
+    bt = torch.stack([torch.arange(4 * i, 4 * i + 4, dtype=torch.int32) for i in range(B)]).cuda()
+    dec = dict(kind="decode", input_ids=torch.randint(0, cfg.vocab_size, (B,), device="cuda"),
+               positions=torch.full((B,), T0, device="cuda"), slots=torch.tensor([64 * i + T0 for i in range(B)],
+                                                                                 device="cuda"),
+               block_tables=bt, ctx_lens=torch.full((B,), T0 + 1, dtype=torch.int32, device="cuda"), max_ctx=64)
+    m.gqa_mfma = set()
+    ref = m(StepInput(**dec), kv).float()
+    m.gqa_mfma = {B}
+    got = m(StepInput(**dec), kv).float()
+    m.gqa_mfma = set()
+    _assert_logits_close(got.cpu(), ref.cpu())
+    cos = torch.nn.functional.cosine_similarity(got, ref, dim=-1).min().item()
+    assert cos > 0.9999, cos
