@@ -548,6 +548,47 @@ __global__ __launch_bounds__(CAND_THREADS) void cand_topk_kernel(const bf16_t* _
     }
   }
   __syncthreads();
+  if (nout > KC) {
+    // more than KC keys tie at the boundary: the atomic slot order above kept an arbitrary subset
+    // of the ties, which could drop the lowest-index one that greedy / top-k tie-breaking needs. Rewrite the
+    // row deterministically: every key above the boundary (fewer than K <= KC of them), then the ties in
+    // ascending vocabulary index (a ballot rank per wave + wave offsets, in (e, t) = index order).
+    __shared__ int n_above, wtie[CAND_THREADS / 64], tie_base;
+    if (t == 0) { n_above = 0; tie_base = 0; }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      if (key[e] != 0u && key[e] > kth) {
+        const int s = atomicAdd(&n_above, 1);
+        ov[s] = x[e];
+        oi[s] = lo + t + e * CAND_THREADS;
+      }
+    }
+    __syncthreads();
+    const int room = KC - n_above;
+    const int lane = t & 63, wv = t >> 6;
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const bool tie = key[e] != 0u && key[e] == kth;
+      const unsigned long long bal = __ballot(tie);
+      if (lane == 0) wtie[wv] = __popcll(bal);
+      __syncthreads();
+      int off = tie_base;
+      for (int w2 = 0; w2 < wv; ++w2) off += wtie[w2];
+      const int rank = off + __popcll(bal & ((1ull << lane) - 1ull));
+      if (tie && rank < room) {
+        ov[n_above + rank] = x[e];
+        oi[n_above + rank] = lo + t + e * CAND_THREADS;
+      }
+      __syncthreads();
+      if (t == 0) {
+        int tot = 0;
+        for (int w2 = 0; w2 < CAND_THREADS / 64; ++w2) tot += wtie[w2];
+        tie_base += tot;
+      }
+      __syncthreads();
+    }
+  }
   for (int s = nout + t; s < KC; s += CAND_THREADS) {  // unused slots
     ov[s] = -INFINITY;
     oi[s] = 0x7fffffff;

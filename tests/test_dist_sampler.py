@@ -118,3 +118,30 @@ def test_gpu_engine_sharded_candidates_match_v3(monkeypatch):
         outs.append(eng.generate(prompts, sps))
         del eng
     assert outs[0] == outs[1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tp", [2, 8])
+def test_gpu_candidates_tie_mass_above_kc(tp):
+    """more than KC = 128 logits of a shard tie at the top-k boundary. The candidate kernel must
+    keep the lowest-index ties (deterministic), so greedy and top-k draws equal the full-row v3 sampler."""
+    from llmss_amd import ops
+    from llmss_amd.ops import hip as H
+
+    dev = torch.device("cuda")
+    B, V = 16, 4096 * tp
+    x = torch.randn(B, V, device=dev).to(torch.bfloat16) - 8.0
+    for b in range(B):  # 300 equal maxima per shard (plus a few above them on odd rows)
+        for r in range(tp):
+            idx = torch.randperm(4096, device=dev)[:300] + r * 4096
+            x[b, idx] = 5.0
+        if b % 2:
+            x[b, torch.randint(0, V, (3,), device=dev)] = 6.0
+    temp, topk, topp, seeds = (torch.from_numpy(a).to(dev) for a in _params(B, 11 + tp))
+    full = H.sample(x, temp, topk, topp, seeds, vocab=V)
+    vl = V // tp
+    packs = [H.cand_topk(x[:, r * vl:(r + 1) * vl].contiguous(), r * vl, V, temp, topk) for r in range(tp)]
+    again = [H.cand_topk(x[:, r * vl:(r + 1) * vl].contiguous(), r * vl, V, temp, topk) for r in range(tp)]
+    assert all(torch.equal(a, b) for a, b in zip(packs, again))  # deterministic packs
+    got = ops.sample_distributed(x[:, :vl].contiguous(), _FakeGather(packs), 0, V, temp, topk, topp, seeds)
+    assert got.tolist() == full.tolist()
