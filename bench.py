@@ -299,11 +299,13 @@ def run_served(args, eng, client, progress, world, rank_sync):
             progress(f"grpc step {i}: {reps[-1]['tokens']} tokens, {time.perf_counter() - t0:.3f}s elapsed")
         rank_sync()
         el = time.perf_counter() - t0
+        dstats = dict(drv.stats)
     finally:
         server.stop(0).wait()
         drv.stop()
     if drv.error is not None:
         raise RuntimeError(f"engine driver failed: {drv.error}")
+    reps[0]["driver_stats"] = dstats
     return el, sum(r["tokens"] for r in reps), reps
 
 
@@ -447,6 +449,8 @@ def run_config(args, model_name, tp, batch, progress, dp=False, client=None):
                                     f"from a separate client process); engine_direct = the same engine stepped "
                                     f"directly")
         out["served_over_engine"] = round(out["value"] / engine_direct["value"], 4)
+        out["config"]["driver_stats"] = {k: (round(v, 4) if isinstance(v, float) else v)
+                                         for k, v in reps[0].get("driver_stats", {}).items()}
         progress(f"served over gRPC: {out['value']} tok/s = {out['served_over_engine']:.1%} of engine-direct "
                  f"{engine_direct['value']}")
     del eng, model

@@ -1320,9 +1320,6 @@ int gemm_skinny_splitk(int M, int N, int K) {
   return s;
 }
 
-void launch_gemm_slice(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, const bf16_t* bias, bf16_t* Y,
-                       int64_t ldy, float* part, int M, int N, int K, int act, int nt, int split, hipStream_t st);
-
 int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const bf16_t* B, bf16_t* Y, int64_t ldy,
                  int M, int N, int K, int act, int g, int tsel, int split_hint, void* workspace, int64_t ws_bytes,
                  bool partial_out, hipStream_t st, const float* wscale = nullptr, const QkvEpi* qe = nullptr);
@@ -1404,11 +1401,7 @@ int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_f
     float* part = splitk > 1 ? (float*)workspace : nullptr;
     const int mt = (M + 15) / 16;
     const int act_k = splitk > 1 ? 0 : act, glu_k = splitk > 1 ? 0 : g;
-    if (variant == 3) {  // gemm_slice.hip: whole weight slice in flight per workgroup (M <= 64, bf16, no GLU)
-      if (w_fp8 || glu) throw std::runtime_error("gemm: the weight-slice kernel takes bf16 weights without GLU");
-      launch_gemm_slice(X, ldx, (const bf16_t*)w, ldw, B, Y, ldy, part, M, N, K, act_k, std::min(2, std::max(1, nt)),
-                        splitk, st);
-    } else if (w_fp8) launch_stream<true>(variant, mt, nt, X, ldx, w, ldw, WS, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
+    if (w_fp8) launch_stream<true>(variant, mt, nt, X, ldx, w, ldw, WS, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
     else launch_stream<false>(variant, mt, nt, X, ldx, w, ldw, nullptr, B, Y, ldy, part, M, N, K, act_k, glu_k, splitk, st);
     if (splitk > 1 && partial_out && !glu && act == 0) return splitk;
     if (splitk > 1) {

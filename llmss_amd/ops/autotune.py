@@ -59,10 +59,6 @@ def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, 
     splits = (1, 2, 4, 8)
     if fp8 or M <= 32:  # weight-streaming kernels: nt + 16 * variant
         out += [(nt + 16 * v, s) for v, nt, s in itertools.product((1, 2), (1, 2), splits)]
-    if not fp8 and not glu and M <= 64:  # weight-slice kernel (variant 3, csrc/gemm_slice.hip): slice fits LDS
-        nstg = -(-K // 64)
-        out += [(nt + 48, s) for nt in (1, 2) for s in (1, 2, 3, 4, 6, 8, 12, 16)
-                if s <= nstg and -(-nstg // s) * 16 * nt * 128 <= 160 * 1024]
     if fp8:  # tiled kernel with fp8 weight tiles (no stream-K / big-tile variants)
         if M > 16:
             out += [((t | d) << 8, s) for t, d in ((3, 16), (3, 32), (2, 16), (2, 32)) for s in splits]

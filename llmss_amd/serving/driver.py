@@ -110,11 +110,13 @@ class EngineDriver:
         # admission window: an idle leader that wakes on a request keeps collecting arrivals until none
         # came for `batch_window_s` (at most 10 windows), so a burst of concurrent clients is admitted in
         # one prefill step instead of trickling in one by one
-        self.batch_window_s = float(os.environ.get("LLMSS_ADMIT_WINDOW_S", "0.002"))
+        self.batch_window_s = float(os.environ.get("LLMSS_ADMIT_WINDOW_S", "0.001"))
+        self.batch_window_max = int(os.environ.get("LLMSS_ADMIT_WINDOW_MAX", "5"))
         self.fault = fault if fault is not None else FaultSpec.from_env()
         self.error: Optional[BaseException] = None
         self._last_bcast = time.perf_counter()
-        self.stats = {"ctrl_bcasts": 0, "ctrl_payloads": 0}
+        self.stats = {"ctrl_bcasts": 0, "ctrl_payloads": 0, "admit_windows": 0, "admit_window_s": 0.0,
+                      "admit_window_reqs": 0}
         self._rid_stride = 1
         # global rank of this replica's leader (broadcast src is a global rank in torch.distributed)
         self._src = dist.get_global_rank(self.cg, 0) if self.tp.is_real else 0
@@ -193,7 +195,8 @@ class EngineDriver:
         new, aborts, stop = [], [], False
         try:
             item = self.inbox.get(timeout=self.idle_wait_s) if block else self.inbox.get_nowait()
-            t_end = time.perf_counter() + 10 * self.batch_window_s
+            t_start = time.perf_counter()
+            t_end = t_start + self.batch_window_max * self.batch_window_s
             while True:
                 kind, v = item
                 if kind == "new":
@@ -210,6 +213,10 @@ class EngineDriver:
                     item = self.inbox.get(timeout=self.batch_window_s)
         except queue.Empty:
             pass
+        if block and new:
+            self.stats["admit_windows"] += 1
+            self.stats["admit_window_s"] += time.perf_counter() - t_start
+            self.stats["admit_window_reqs"] += len(new)
         now = time.perf_counter()
         for h in list(self.handles.values()):  # server-side deadlines
             if h.deadline is not None and now > h.deadline and h.rid not in aborts:

@@ -136,72 +136,3 @@ def test_packed_weight_layout(N, K):
     assert torch.allclose(R.linear(x, wp), R.linear(x, w))
     with pytest.raises(ValueError):
         R.pack_weight(torch.zeros(24, 64))
-
-
-def emulate_slice(X, W, NT, split):
-    """csrc/gemm_slice.hip gemm_slice_kernel, lane by lane: the LDS-DMA image of each workgroup's weight
-    slice (lane -> row rb*8 + lane>>3, global chunk (lane&7) ^ (row&7), LDS byte i*1024 + lane*16), the A
-    fragments read straight from X and the B fragment addresses; returns Y (split == 1) or the fp32 slabs."""
-    M, K = X.shape
-    N = W.shape[0]
-    ROWS, IPS = 16 * NT, 2 * NT
-    nstg_all = (K + 63) // 64
-    Wb = W.astype(np.float64)
-    out = np.zeros((split, M, N))
-    for bx in range((N + ROWS - 1) // ROWS):
-        n0 = bx * ROWS
-        for z in range(split):
-            s0, s1 = nstg_all * z // split, nstg_all * (z + 1) // split
-            nst, kb, ke = s1 - s0, s0 * 64, min(K, s1 * 64)
-            lds = np.full(nst * IPS * 512, np.nan)  # bf16 elements
-            for w in range(4):
-                for i in range(w, nst * IPS, 4):
-                    st, rb = divmod(i, IPS)
-                    for lane in range(64):
-                        row = rb * 8 + (lane >> 3)
-                        c = (lane & 7) ^ (row & 7)
-                        kc = min(kb + st * 64 + c * 8, K - 8)
-                        r = min(n0 + row, N - 1)
-                        assert 0 <= kc and kc + 8 <= K
-                        lds[i * 512 + lane * 8:i * 512 + lane * 8 + 8] = Wb[r, kc:kc + 8]
-            nk32 = (ke - kb + 31) // 32
-            for w in range(4):
-                if 16 * w >= M:
-                    continue
-                acc = [np.zeros((64, 4)) for _ in range(NT)]
-                for j in range(nk32):
-                    a = np.zeros((64, 8))
-                    bs = [np.zeros((64, 8)) for _ in range(NT)]
-                    for lane in range(64):
-                        li, g = lane & 15, lane >> 4
-                        k = kb + j * 32 + 8 * g
-                        m = min(16 * w + li, M - 1)
-                        if k < ke:
-                            a[lane] = X[m, min(k, K - 8):min(k, K - 8) + 8]
-                        st, c = j >> 1, 4 * (j & 1) + g
-                        for t in range(NT):
-                            row = t * 16 + li
-                            byte = (st * IPS + (row >> 3)) * 1024 + (row & 7) * 128 + ((c ^ (row & 7)) << 4)
-                            if k < ke:
-                                bs[t][lane] = lds[byte // 2:byte // 2 + 8]
-                    for t in range(NT):
-                        acc[t] = mfma_16x16x32(a, bs[t], acc[t])
-                for lane in range(64):
-                    li, g = lane & 15, lane >> 4
-                    for i in range(4):
-                        m = 16 * w + 4 * g + i
-                        for t in range(NT):
-                            n = n0 + t * 16 + li
-                            if m < M and n < N:
-                                out[z, m, n] = acc[t][lane, i]
-    return out
-
-
-@pytest.mark.parametrize("M,N,K,NT,split", [(64, 40, 200, 1, 1), (17, 70, 328, 2, 3), (33, 16, 136, 1, 2)])
-def test_slice_kernel_emulation(M, N, K, NT, split):
-    rng = np.random.default_rng(0)
-    X = rng.standard_normal((M, K))
-    W = rng.standard_normal((N, K))
-    slabs = emulate_slice(X, W, NT, split)
-    assert not np.isnan(slabs).any()
-    np.testing.assert_allclose(slabs.sum(0), X @ W.T, rtol=1e-9, atol=1e-9)

@@ -637,25 +637,3 @@ def test_w8a8_decode_plan_in_graph(M):
     ref = R.linear(R.dequant_fp8(xq, xs), q, b.float(), w_scale=s)
     close(y, ref, 2e-2)
     assert not torch.equal(eager, y)  # the replay read the new activations
-
-
-@pytest.mark.parametrize("nt", [1, 2])
-@pytest.mark.parametrize("split", [1, 2, 4])
-@pytest.mark.parametrize("M,N,K", [(64, 4800, 1600), (64, 1600, 6400), (33, 1000, 1616), (1, 96, 64), (48, 6400, 1600)])
-def test_gemm_weight_slice(nt, split, M, N, K):
-    """Weight-slice decode GEMM (csrc/gemm_slice.hip, stream variant 3): bias + GELU epilogue unsplit, fp32
-    slabs summed by the consumer when split."""
-    lds = -(-(-(-K // 64)) // split) * 16 * nt * 128
-    if lds > 160 * 1024:
-        pytest.skip("slice exceeds LDS at this split")
-    torch.manual_seed(3)
-    x, w, b = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
-    hint = nt + 48
-    if split == 1:
-        y = H.linear(x, w, b, act="gelu_tanh", nt_hint=hint, split_hint=1)
-        close(y, R.linear(x.float(), w.float(), b.float(), act="gelu_tanh"), 2e-2)
-    r = H.linear(x, w, b, nt_hint=hint, split_hint=split, partial_ok=True)
-    if isinstance(r, H.PartialSum):
-        assert r.S == split
-        r = r.buf[: r.S * M * N].view(r.S, M, N).sum(0) + b.float()
-    close(r, R.linear(x.float(), w.float(), b.float()), 2e-2)
