@@ -171,3 +171,18 @@ def test_tp_layer_library_tp2_matches_tp1(tmp_path):
     torch.testing.assert_close(got[1], ref[1], rtol=1e-5, atol=1e-5)  # column -> row + all-reduce (+ rank-0 bias)
     assert got[2][1] * 2 == ref[2][1]  # fused q|k|v column shard
     torch.testing.assert_close(got[3], ref[3], rtol=1e-5, atol=1e-5)  # vocab-parallel head, padded then trimmed
+
+
+def test_pool_exhaustion_leaves_pool_intact(tmp_path):
+    """a call that cannot get its KV blocks raises without leaking the blocks of earlier rows."""
+    d = str(tmp_path / "llama")
+    save_hf_model("llama", d)
+    model, _ = _load(d)
+    free0 = len(model._free)
+    ids = torch.randint(0, 100, (3, (free0 // 3 + 2) * model.block_size))  # needs more blocks than the pool has
+    with pytest.raises(RuntimeError, match="exhausted"):
+        model(ids, use_cache=True)
+    assert len(model._free) == free0
+    out = model(ids[:, :20], use_cache=True)  # the pool still serves a call that fits
+    model.release(out.past_key_values)
+    assert len(model._free) == free0
