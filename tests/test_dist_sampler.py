@@ -142,6 +142,9 @@ def test_gpu_candidates_tie_mass_above_kc(tp):
     vl = V // tp
     packs = [H.cand_topk(x[:, r * vl:(r + 1) * vl].contiguous(), r * vl, V, temp, topk) for r in range(tp)]
     again = [H.cand_topk(x[:, r * vl:(r + 1) * vl].contiguous(), r * vl, V, temp, topk) for r in range(tp)]
-    assert all(torch.equal(a, b) for a, b in zip(packs, again))  # deterministic packs
+    for a, b in zip(packs, again):  # the same candidate SET every run (slot order follows atomics; irrelevant)
+        ia = a[:, 128:].view(torch.int32).sort(-1).values
+        ib = b[:, 128:].view(torch.int32).sort(-1).values
+        assert torch.equal(ia, ib)
     got = ops.sample_distributed(x[:, :vl].contiguous(), _FakeGather(packs), 0, V, temp, topk, topp, seeds)
     assert got.tolist() == full.tolist()
