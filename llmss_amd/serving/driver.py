@@ -110,8 +110,8 @@ class EngineDriver:
         # admission window: an idle leader that wakes on a request keeps collecting arrivals until none
         # came for `batch_window_s` (at most 10 windows), so a burst of concurrent clients is admitted in
         # one prefill step instead of trickling in one by one
-        self.batch_window_s = float(os.environ.get("LLMSS_ADMIT_WINDOW_S", "0.001"))
-        self.batch_window_max = int(os.environ.get("LLMSS_ADMIT_WINDOW_MAX", "5"))
+        self.batch_window_s = float(os.environ.get("LLMSS_ADMIT_WINDOW_S", "0.003"))
+        self.batch_window_max = int(os.environ.get("LLMSS_ADMIT_WINDOW_MAX", "10"))
         self.fault = fault if fault is not None else FaultSpec.from_env()
         self.error: Optional[BaseException] = None
         self._last_bcast = time.perf_counter()
