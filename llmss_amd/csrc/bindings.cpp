@@ -11,7 +11,8 @@
 namespace py = pybind11;
 
 void launch_add_norm(const void* x, int64_t x_stride, const void* res_in, void* res_out, const void* w, const void* b,
-                     void* y, int64_t y_stride, int T, int H, float eps, bool rms, hipStream_t st);
+                     void* y, int64_t y_stride, int T, int H, float eps, bool rms, hipStream_t st, void* q8,
+                     void* s8);
 void launch_embed(const void* ids, const void* pos, const void* wte, const void* wpe, void* out, int T, int H,
                   int vocab, hipStream_t st);
 void launch_rope_cache(void* qkv, int64_t row_stride, const void* pos, const void* cos_t, const void* sin_t, void* kc,
@@ -56,7 +57,8 @@ void gemm_tuned_clear();
 void gemm_reserve_streamk(int n);
 int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq, int64_t ldw, const void* wsc,
                      const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, int tile,
-                     int depth, int split, void* workspace, int64_t ws_bytes, hipStream_t st);
+                     int depth, int split, void* workspace, int64_t ws_bytes, hipStream_t st, bool partial_out);
+int gemm_f8f8_partial_slabs(int M, int N, int K, bool glu, int act, int tile, int split, int64_t ws_bytes);
 int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int nt_hint, int split_hint,
                        int64_t ws_bytes);
 void attn_decode_set_unroll(int u);
@@ -67,7 +69,7 @@ int launch_gemm_packed(const void* x, int64_t ldx, const void* w, int64_t k64, c
                        int split_hint, bool partial_out, hipStream_t st);
 void launch_add_norm_partial(const void* part, int S, int64_t slab, const void* xbias, const void* res_in,
                              void* res_out, const void* w, const void* b, void* y, int64_t y_stride, int T, int H,
-                             float eps, bool rms, hipStream_t st);
+                             float eps, bool rms, hipStream_t st, void* q8, void* s8);
 void launch_sample(const void* logits, int64_t ld, bool fp32_logits, int B, int V, const void* temperature,
                    const void* top_k, const void* top_p, const void* seeds, void* out, void* out2, hipStream_t st);
 void launch_quant_fp8_rows(const void* w, void* q, void* scale, int64_t N, int64_t K, hipStream_t st);
@@ -84,9 +86,12 @@ void register_comm(py::module_& m);     // RCCL communicator (comm.cpp)
 PYBIND11_MODULE(_C, m) {
   m.doc() = "llmss_amd gfx950 HIP kernels + native runtime";
   m.def("add_norm", [](uintptr_t x, int64_t xs, uintptr_t ri, uintptr_t ro, uintptr_t w, uintptr_t b, uintptr_t y,
-                       int64_t ys, int T, int H, float eps, bool rms, uintptr_t st) {
-    launch_add_norm(CP(x), xs, CP(ri), P(ro), CP(w), CP(b), P(y), ys, T, H, eps, rms, S(st));
-  });
+                       int64_t ys, int T, int H, float eps, bool rms, uintptr_t st, uintptr_t q8, uintptr_t s8) {
+    launch_add_norm(CP(x), xs, CP(ri), P(ro), CP(w), CP(b), P(y), ys, T, H, eps, rms, S(st), P(q8), P(s8));
+  }, pybind11::arg("x"), pybind11::arg("xs"), pybind11::arg("ri"), pybind11::arg("ro"), pybind11::arg("w"),
+     pybind11::arg("b"), pybind11::arg("y"), pybind11::arg("ys"), pybind11::arg("T"), pybind11::arg("H"),
+     pybind11::arg("eps"), pybind11::arg("rms"), pybind11::arg("st"), pybind11::arg("q8") = 0,
+     pybind11::arg("s8") = 0);
   m.def("embed", [](uintptr_t ids, uintptr_t pos, uintptr_t wte, uintptr_t wpe, uintptr_t out, int T, int H, int V,
                     uintptr_t st) { launch_embed(CP(ids), CP(pos), CP(wte), CP(wpe), P(out), T, H, V, S(st)); });
   m.def("rope_cache", [](uintptr_t qkv, int64_t rs, uintptr_t pos, uintptr_t cos_t, uintptr_t sin_t, uintptr_t kc,
@@ -160,10 +165,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_reserve_streamk", &gemm_reserve_streamk);
   m.def("gemm_f8f8", [](uintptr_t xq, int64_t ldx, uintptr_t xs, uintptr_t wq, int64_t ldw, uintptr_t wsc,
                         uintptr_t bias, uintptr_t y, int64_t ldy, int M, int N, int K, int act, bool glu, int tile,
-                        int depth, int split, uintptr_t work, int64_t wbytes, uintptr_t st) {
+                        int depth, int split, uintptr_t work, int64_t wbytes, uintptr_t st, bool partial_out) {
     return launch_gemm_f8f8(CP(xq), ldx, CP(xs), CP(wq), ldw, CP(wsc), CP(bias), P(y), ldy, M, N, K, act, glu, tile,
-                            depth, split, P(work), wbytes, S(st));
-  });
+                            depth, split, P(work), wbytes, S(st), partial_out);
+  }, pybind11::arg("xq"), pybind11::arg("ldx"), pybind11::arg("xs"), pybind11::arg("wq"), pybind11::arg("ldw"),
+     pybind11::arg("wsc"), pybind11::arg("bias"), pybind11::arg("y"), pybind11::arg("ldy"), pybind11::arg("M"),
+     pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("act"), pybind11::arg("glu"), pybind11::arg("tile"),
+     pybind11::arg("depth"), pybind11::arg("split"), pybind11::arg("work"), pybind11::arg("wbytes"),
+     pybind11::arg("st"), pybind11::arg("partial_out") = false);
+  m.def("gemm_f8f8_partial_slabs", &gemm_f8f8_partial_slabs);
   m.def("gemm_partial_slabs", &gemm_partial_slabs);
   m.def("attn_decode_set_unroll", &attn_decode_set_unroll);
   m.def("gemm_tuned_get", [](int M, int N, int K, bool glu, int kind) -> py::object {
@@ -180,9 +190,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_packed_partial_slabs", &gemm_packed_partial_slabs);
   m.def("add_norm_partial", [](uintptr_t part, int S, int64_t slab, uintptr_t xbias, uintptr_t ri, uintptr_t ro,
                                uintptr_t w, uintptr_t b, uintptr_t y, int64_t ys, int T, int H, float eps, bool rms,
-                               uintptr_t st) {
-    launch_add_norm_partial(CP(part), S, slab, CP(xbias), CP(ri), P(ro), CP(w), CP(b), P(y), ys, T, H, eps, rms, S(st));
-  });
+                               uintptr_t st, uintptr_t q8, uintptr_t s8) {
+    launch_add_norm_partial(CP(part), S, slab, CP(xbias), CP(ri), P(ro), CP(w), CP(b), P(y), ys, T, H, eps, rms, S(st),
+                            P(q8), P(s8));
+  }, pybind11::arg("part"), pybind11::arg("S"), pybind11::arg("slab"), pybind11::arg("xbias"), pybind11::arg("ri"),
+     pybind11::arg("ro"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("y"), pybind11::arg("ys"),
+     pybind11::arg("T"), pybind11::arg("H"), pybind11::arg("eps"), pybind11::arg("rms"), pybind11::arg("st"),
+     pybind11::arg("q8") = 0, pybind11::arg("s8") = 0);
   m.def("sample", [](uintptr_t logits, int64_t ld, bool fp32, int B, int V, uintptr_t temp, uintptr_t topk,
                      uintptr_t topp, uintptr_t seeds, uintptr_t out, uintptr_t out2, uintptr_t st) {
     launch_sample(CP(logits), ld, fp32, B, V, CP(temp), CP(topk), CP(topp), CP(seeds), P(out), P(out2), S(st));

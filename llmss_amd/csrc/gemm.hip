@@ -1187,13 +1187,15 @@ __global__ __launch_bounds__(256) void gemm_f8f8_kernel(const unsigned char* __r
 }
 
 // tile: 1 = 128x128, 2 = 64x128, 3 = 64x64; ring depth 2-4; split-K over grid.y
+// partial_out: a split plan without activation / GLU leaves its fp32 slabs [split, M, N] (scales applied, no
+// bias) in `workspace` for the consumer (rope_cache / add_norm sum them) and returns the split; else 0.
 int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq, int64_t ldw, const void* wsc,
                      const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, int tile,
-                     int depth, int split, void* workspace, int64_t ws_bytes, hipStream_t st) {
+                     int depth, int split, void* workspace, int64_t ws_bytes, hipStream_t st, bool partial_out) {
   if (M == 0 || N == 0) return 0;
   if (K % 16) throw std::runtime_error("gemm_f8f8: K must be a multiple of 16");
   if (glu && (N % 32)) throw std::runtime_error("gemm_f8f8: glu needs N % 32 == 0");
-  if (!y) throw std::runtime_error("gemm_f8f8: output required");
+  if (!y && !partial_out) throw std::runtime_error("gemm_f8f8: output required");
   const int bm = tile == 1 ? 128 : 64, bn = tile == 3 ? 64 : 128;
   const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   const int nk = (K + TBK8 - 1) / TBK8;
@@ -1208,7 +1210,7 @@ int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq
   if (tile == 0) {  // auto: 128x128 when it fills the chip, else 64x128 / 64x64, split to >= ~256 WGs
     tile = ((M + 127) / 128) * ((N + 127) / 128) >= 240 ? 1 : (((M + 63) / 64) * ((N + 127) / 128) >= 240 ? 2 : 3);
     return launch_gemm_f8f8(xq, ldx, xs, wq, ldw, wsc, bias, y, ldy, M, N, K, act, glu, tile, depth, split, workspace,
-                            ws_bytes, st);
+                            ws_bytes, st, partial_out);
   }
   if (split <= 0) {
     split = 1;
@@ -1238,13 +1240,33 @@ int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq
   }
 #undef LF
   HIP_CHECK_LAUNCH();
+  if (split > 1 && partial_out && !glu && act == 0) return split;
   if (split > 1) {
+    if (!y) throw std::runtime_error("gemm_f8f8: output required");
     const int nout = glu ? N / 2 : N;
     dim3 rgrid(std::min((nout + 255) / 256, 64), M);
     splitk_reduce_kernel<<<rgrid, 256, 0, st>>>(part, split, M, N, Bi, Y, ldy, act, g);
     HIP_CHECK_LAUNCH();
   }
   return 0;
+}
+
+// the split a W8A8 call with these arguments leaves as slabs under partial_out (0 = finished output)
+int gemm_f8f8_partial_slabs(int M, int N, int K, bool glu, int act, int tile, int split, int64_t ws_bytes) {
+  if (M == 0 || N == 0 || glu || act != 0) return 0;
+  if (tile == 4 || (tile == 0 && K % 128 == 0 && ((M + 255) / 256) * ((N + 255) / 256) >= 192)) return 0;
+  if (tile == 0)
+    tile = ((M + 127) / 128) * ((N + 127) / 128) >= 240 ? 1 : (((M + 63) / 64) * ((N + 127) / 128) >= 240 ? 2 : 3);
+  const int bm = tile == 1 ? 128 : 64, bn = tile == 3 ? 64 : 128;
+  const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  const int nk = (K + TBK8 - 1) / TBK8;
+  if (split <= 0) {
+    split = 1;
+    while (tiles * split * 2 <= 512 && nk / (2 * split) >= 4 && split < 8) split *= 2;
+  }
+  split = std::max(1, std::min(split, nk));
+  if ((int64_t)split * M * N * 4 > ws_bytes) split = 1;
+  return split > 1 ? split : 0;
 }
 
 // -------------------------------------------------------------------------------------------

@@ -23,8 +23,10 @@ __global__ __launch_bounds__(256) void add_norm_kernel(const bf16_t* __restrict_
                                                        const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
                                                        bf16_t* __restrict__ y, int64_t y_stride, int H, float eps,
                                                        const float* __restrict__ part, int S, int64_t slab,
-                                                       const bf16_t* __restrict__ xbias) {
+                                                       const bf16_t* __restrict__ xbias, unsigned char* __restrict__ q8,
+                                                       float* __restrict__ s8) {
   __shared__ float red[32];
+  __shared__ float red2[32];
   const int row = blockIdx.x;
   const int nchunk = H >> 3;
   float v[MAXC][8];
@@ -113,6 +115,8 @@ __global__ __launch_bounds__(256) void add_norm_kernel(const bf16_t* __restrict_
     }
   }
   const float rstd = rsqrtf(var + eps);
+  u16x8 ov[MAXC];
+  float amax = 0.f;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int ch = threadIdx.x + c * blockDim.x;
@@ -123,8 +127,31 @@ __global__ __launch_bounds__(256) void add_norm_kernel(const bf16_t* __restrict_
         float t = (v[c][j] - mean) * rstd * bf2f(wv[c][j]);
         if constexpr (HAS_BIAS) t += bf2f(bv[c][j]);
         o[j] = f2bf(t);
+        amax = fmaxf(amax, fabsf(bf2f(o[j])));
       }
+      ov[c] = o;
       *reinterpret_cast<u16x8*>(y + row * y_stride + ch * 8) = o;
+    }
+  }
+  if (q8) {  // per-token fp8-e4m3 twin of the bf16 output for a W8A8 consumer (== quant_fp8_rows_ld of y)
+    amax = block_max(amax, red2);
+    const float sc = amax > 0.f ? amax / 448.f : 1.f;
+    const float inv = 1.f / sc;
+    if (threadIdx.x == 0) s8[row] = sc;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = threadIdx.x + c * blockDim.x;
+      if (ch < nchunk) {
+        float f[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fminf(fmaxf(bf2f(ov[c][j]) * inv, -448.f), 448.f);
+        unsigned lo = 0, hi = 0;
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], lo, false);
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], hi, false);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
+        *reinterpret_cast<uint2*>(q8 + (int64_t)row * H + ch * 8) = make_uint2(lo, hi);
+      }
     }
   }
 }
@@ -132,19 +159,20 @@ __global__ __launch_bounds__(256) void add_norm_kernel(const bf16_t* __restrict_
 template <bool RMS, bool HAS_RES, bool HAS_BIAS, int PART = 0>
 static void launch_norm_t(const bf16_t* x, int64_t xs, const bf16_t* ri, bf16_t* ro, const bf16_t* w,
                           const bf16_t* b, bf16_t* y, int64_t ys, int T, int H, float eps, hipStream_t st,
-                          const float* part = nullptr, int S = 0, int64_t slab = 0, const bf16_t* xbias = nullptr) {
+                          const float* part = nullptr, int S = 0, int64_t slab = 0, const bf16_t* xbias = nullptr,
+                          unsigned char* q8 = nullptr, float* s8 = nullptr) {
   const int nchunk = H / 8;
   int threads = nchunk <= 256 ? ((nchunk + 63) / 64) * 64 : 256;
   const int maxc = (nchunk + threads - 1) / threads;
   dim3 grid(T), block(threads);
   if (maxc == 1)
-    add_norm_kernel<1, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias);
+    add_norm_kernel<1, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias, q8, s8);
   else if (maxc == 2)
-    add_norm_kernel<2, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias);
+    add_norm_kernel<2, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias, q8, s8);
   else if (maxc <= 4)
-    add_norm_kernel<4, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias);
+    add_norm_kernel<4, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias, q8, s8);
   else if (maxc <= 8)
-    add_norm_kernel<8, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias);
+    add_norm_kernel<8, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias, q8, s8);
   else
     throw std::runtime_error("add_norm: hidden size too large (max 16384)");
   HIP_CHECK_LAUNCH();
@@ -152,7 +180,9 @@ static void launch_norm_t(const bf16_t* x, int64_t xs, const bf16_t* ri, bf16_t*
 
 void launch_add_norm(const void* x, int64_t x_stride, const void* res_in, void* res_out, const void* w,
                      const void* b, void* y, int64_t y_stride, int T, int H, float eps, bool rms,
-                     hipStream_t st) {
+                     hipStream_t st, void* q8v, void* s8v) {
+  auto Q8 = (unsigned char*)q8v;
+  auto S8 = (float*)s8v;
   if (H % 8 != 0) throw std::runtime_error("add_norm: hidden size must be a multiple of 8");
   if (T == 0) return;
   auto X = (const bf16_t*)x;
@@ -163,15 +193,15 @@ void launch_add_norm(const void* x, int64_t x_stride, const void* res_in, void* 
   auto Y = (bf16_t*)y;
   const bool has_res = res_in != nullptr, has_b = b != nullptr;
   if (rms) {
-    if (has_res) launch_norm_t<true, true, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st);
-    else launch_norm_t<true, false, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st);
+    if (has_res) launch_norm_t<true, true, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8);
+    else launch_norm_t<true, false, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8);
   } else {
     if (has_res) {
-      if (has_b) launch_norm_t<false, true, true>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st);
-      else launch_norm_t<false, true, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st);
+      if (has_b) launch_norm_t<false, true, true>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8);
+      else launch_norm_t<false, true, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8);
     } else {
-      if (has_b) launch_norm_t<false, false, true>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st);
-      else launch_norm_t<false, false, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st);
+      if (has_b) launch_norm_t<false, false, true>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8);
+      else launch_norm_t<false, false, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8);
     }
   }
 }
@@ -179,7 +209,9 @@ void launch_add_norm(const void* x, int64_t x_stride, const void* res_in, void* 
 // residual-add + norm whose input is the split-K partial sum of the preceding row-parallel GEMM
 void launch_add_norm_partial(const void* part, int S, int64_t slab, const void* xbias, const void* res_in,
                              void* res_out, const void* w, const void* b, void* y, int64_t y_stride, int T, int H,
-                             float eps, bool rms, hipStream_t st) {
+                             float eps, bool rms, hipStream_t st, void* q8v, void* s8v) {
+  auto Q8 = (unsigned char*)q8v;
+  auto S8 = (float*)s8v;
   if (H % 8 != 0) throw std::runtime_error("add_norm: hidden size must be a multiple of 8");
   if (!res_in) throw std::runtime_error("add_norm_partial: needs a residual");
   if (T == 0) return;
@@ -192,9 +224,9 @@ void launch_add_norm_partial(const void* part, int S, int64_t slab, const void* 
   auto Y = (bf16_t*)y;
 #define LNP(PS_)                                                                                                   \
   do {                                                                                                             \
-    if (rms) launch_norm_t<true, true, false, PS_>(nullptr, 0, RI, RO, W, B, Y, y_stride, T, H, eps, st, P, S, slab, XB); \
-    else if (b) launch_norm_t<false, true, true, PS_>(nullptr, 0, RI, RO, W, B, Y, y_stride, T, H, eps, st, P, S, slab, XB); \
-    else launch_norm_t<false, true, false, PS_>(nullptr, 0, RI, RO, W, B, Y, y_stride, T, H, eps, st, P, S, slab, XB); \
+    if (rms) launch_norm_t<true, true, false, PS_>(nullptr, 0, RI, RO, W, B, Y, y_stride, T, H, eps, st, P, S, slab, XB, Q8, S8); \
+    else if (b) launch_norm_t<false, true, true, PS_>(nullptr, 0, RI, RO, W, B, Y, y_stride, T, H, eps, st, P, S, slab, XB, Q8, S8); \
+    else launch_norm_t<false, true, false, PS_>(nullptr, 0, RI, RO, W, B, Y, y_stride, T, H, eps, st, P, S, slab, XB, Q8, S8); \
   } while (0)
   switch (S) {
     case 2: LNP(2); break;

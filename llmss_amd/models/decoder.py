@@ -110,6 +110,7 @@ class DecoderLM:
         # serving its whole query-head group: K/V staged once, QK^T and PV on the matrix cores) instead of
         # the VALU split-K decode kernel; filled by LLMEngine's capture-time timing for G >= 4 groups
         self.gqa_mfma: set = set()
+        self._norm_quant = os.environ.get("LLMSS_FP8_NORM_QUANT", "1") != "0"
         self._cu_decode = {}
         self._comm_stream = None
 
@@ -196,6 +197,13 @@ class DecoderLM:
                 ops.attn_prefill(qkv[nd:], inp.cu_seqlens, inp.max_seqlen, p.nh_l, p.nkv_l, D, self.scale,
                                  out=out[nd:])
         return out
+
+    def _fp8_in(self, lin, x) -> bool:
+        """The linear consuming add_norm's output runs W8A8 at this row count: have add_norm write the per-token
+        fp8 twin so the GEMM skips its quantisation launch (LLMSS_FP8_NORM_QUANT=0 disables)."""
+        if lin.w_scale is None or not x.is_cuda or lin.w.dim() != 2 or not self._norm_quant:
+            return False
+        return _hip_ops().w8a8_planned(x.shape[0], lin.N, lin.K, lin.glu)
 
     def decode_cu(self, B: int, device) -> torch.Tensor:
         """[0, 1, .., B] int32: a decode step as B one-token 'chunks' (the extend kernel's cu_q); made once per B
@@ -379,7 +387,7 @@ class DecoderLM:
         fuse = self.tp.size == 1  # split-K partials can skip their own reduce only without a TP all-reduce
         for i, L in enumerate(w.layers):
             kc, vc = kv_caches[i]
-            y, residual = ops.add_norm(delta, L.ln1_w, L.ln1_b, eps, rms, residual)
+            y, residual = ops.add_norm(delta, L.ln1_w, L.ln1_b, eps, rms, residual, fp8_out=self._fp8_in(L.qkv, delta))
             # column-parallel QKV: its split-K partials are summed inside the rope/cache kernel
             a = self._attention(L, y, inp, kc, vc)
             if cfg.parallel_block:  # GPT-J: one all-reduce for attention + MLP
@@ -387,11 +395,11 @@ class DecoderLM:
             elif fuse:
                 # TP=1: the split-K partials of o / down are reduced inside the next add_norm
                 o = L.o(a, partial_ok=True)
-                y2, residual = ops.add_norm(o, L.ln2_w, L.ln2_b, eps, rms, residual)
+                y2, residual = ops.add_norm(o, L.ln2_w, L.ln2_b, eps, rms, residual, fp8_out=self._fp8_in(L.up, a))
                 delta = L.down(L.up(y2, self.act), partial_ok=True)
             else:
                 o = self._reduce_rows(L.o, a)
-                y2, residual = ops.add_norm(o, L.ln2_w, L.ln2_b, eps, rms, residual)
+                y2, residual = ops.add_norm(o, L.ln2_w, L.ln2_b, eps, rms, residual, fp8_out=self._fp8_in(L.up, a))
                 delta = self._reduce_rows(lambda y_: L.down(L.up(y_, self.act)), y2)
         h, _ = ops.add_norm(delta, w.lnf_w, w.lnf_b, eps, rms, residual)
         return h

@@ -25,9 +25,10 @@ def _hip():
     return hip
 
 
-def add_norm(x, weight, bias, eps, rms, residual=None, out=None):
+def add_norm(x, weight, bias, eps, rms, residual=None, out=None, fp8_out=False):
+    """``fp8_out`` (GPU): also emit the output's per-token fp8 twin for a W8A8 consumer (ops/hip.py)."""
     if x.is_cuda:
-        return _hip().add_norm(x, weight, bias, eps, rms, residual, out=out)
+        return _hip().add_norm(x, weight, bias, eps, rms, residual, out=out, fp8_out=fp8_out)
     y, r = ref.add_norm(x, weight, bias, eps, rms, residual)
     if out is not None:
         out.copy_(y)

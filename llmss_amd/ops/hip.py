@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import math
 import os
+import weakref
 from typing import Optional
 
 import torch
@@ -62,9 +63,20 @@ def _bf16_rows(t: torch.Tensor, name: str, cols: Optional[int] = None):
 
 
 # ------------------------------------------------------------------------------------- norm
-def add_norm(x, weight, bias, eps, rms, residual=None, out=None, residual_out=None):
+def _fp8_twin(y):
+    """Scratch for the per-token fp8 twin of add_norm's output ``y`` [T, H], registered for its W8A8 consumer."""
+    T, H = y.shape
+    q, s = _PRESCRATCH.get(T, H, y.device)
+    _PREQ.clear()  # one live twin at a time: the previous one's consumer has run (same stream, program order)
+    _PREQ[id(y)] = (weakref.ref(y), q, s)
+    return q, s
+
+
+def add_norm(x, weight, bias, eps, rms, residual=None, out=None, residual_out=None, fp8_out=False):
+    """``fp8_out``: also write the per-token fp8-e4m3 twin of the output (== quant_fp8_rows of it) for the W8A8
+    GEMM that consumes it next, which then skips its own quantisation launch."""
     if isinstance(x, PartialSum):
-        return add_norm_partial(x, weight, bias, eps, rms, residual, out)
+        return add_norm_partial(x, weight, bias, eps, rms, residual, out, fp8_out=fp8_out)
     T, H = x.shape
     _bf16_rows(x, "x")
     _check(H % 8 == 0, "hidden must be a multiple of 8")
@@ -79,8 +91,9 @@ def add_norm(x, weight, bias, eps, rms, residual=None, out=None, residual_out=No
         _check(ro.is_contiguous() and ro.shape == (T, H), "residual_out")
     else:
         ro = None
+    q8, s8 = _fp8_twin(y) if fp8_out else (None, None)
     lib().add_norm(x.data_ptr(), x.stride(0), _ptr(residual), _ptr(ro), weight.data_ptr(), _ptr(bias),
-                   y.data_ptr(), y.stride(0), T, H, float(eps), bool(rms), _stream())
+                   y.data_ptr(), y.stride(0), T, H, float(eps), bool(rms), _stream(), _ptr(q8), _ptr(s8))
     return y, (ro if residual is not None else x)
 
 
@@ -411,9 +424,11 @@ _DEQ = _DequantScratch()
 _W8A8 = os.environ.get("LLMSS_FP8_W8A8", "1") != "0"
 
 
-def linear_w8a8(x, wq, w_scale, bias=None, act="none", glu=False, out=None, tile=0, depth=0, split=0):
+def linear_w8a8(x, wq, w_scale, bias=None, act="none", glu=False, out=None, tile=0, depth=0, split=0,
+                partial_ok=False):
     """Y = (fp8(x) . wq^T) * x_scale[m] * w_scale[n] on the MX-fp8 MFMA (2x the bf16 matrix rate). The
-    activations are quantised per token into a reusable scratch (graph-capturable)."""
+    activations are quantised per token into a reusable scratch (graph-capturable). ``partial_ok``: a split
+    plan may return its fp32 slabs as a :class:`PartialSum` for the consumer (rope_cache / add_norm)."""
     M, K = x.shape
     N = wq.shape[0]
     _bf16_rows(x, "x")
@@ -423,16 +438,59 @@ def linear_w8a8(x, wq, w_scale, bias=None, act="none", glu=False, out=None, tile
         _check(N % 32 == 0, "glu needs N % 32 == 0")
     if bias is not None:
         _check(bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.numel() == N, "bias [N] bf16")
-    xq, xs = _QSCRATCH.get(M, K, x.device)
-    lib().quant_fp8_rows_ld(x.data_ptr(), x.stride(0), xq.data_ptr(), xs.data_ptr(), M, K, _stream())
+    pre = _prequant_of(x)
+    if pre is not None:  # add_norm already wrote this tensor's per-token fp8 twin
+        xq, xs = pre
+    else:
+        xq, xs = _QSCRATCH.get(M, K, x.device)
+        lib().quant_fp8_rows_ld(x.data_ptr(), x.stride(0), xq.data_ptr(), xs.data_ptr(), M, K, _stream())
     nout = N // 2 if glu else N
-    y = out if out is not None else torch.empty(M, nout, dtype=torch.bfloat16, device=x.device)
-    _bf16_rows(y, "out", nout)
     ws = _GEMM_WS.get(64 << 20, x.device)
-    lib().gemm_f8f8(xq.data_ptr(), K, xs.data_ptr(), wq.data_ptr(), K, w_scale.data_ptr(), _ptr(bias), y.data_ptr(),
-                    y.stride(0), M, N, K, _ACT[act], bool(glu), int(tile), int(depth), int(split), ws.data_ptr(),
-                    ws.numel() * 4, _stream())
+    slabs = 0
+    if partial_ok and out is None and not glu and act in ("none", None):
+        slabs = lib().gemm_f8f8_partial_slabs(M, N, K, bool(glu), 0, int(tile), int(split), ws.numel() * 4)
+    y = None if slabs else (out if out is not None else torch.empty(M, nout, dtype=torch.bfloat16, device=x.device))
+    if y is not None:
+        _bf16_rows(y, "out", nout)
+    S = lib().gemm_f8f8(xq.data_ptr(), K, xs.data_ptr(), wq.data_ptr(), K, w_scale.data_ptr(), _ptr(bias), _ptr(y),
+                        y.stride(0) if y is not None else nout, M, N, K, _ACT[act], bool(glu), int(tile), int(depth),
+                        int(split), ws.data_ptr(), ws.numel() * 4, _stream(), y is None)
+    if y is None:
+        if S <= 1:
+            raise RuntimeError("internal: partial W8A8 GEMM did not produce partial slabs")
+        return PartialSum(ws, S, M, N, bias, x.device)
     return y
+
+
+# per-token fp8 twins written by add_norm(..., fp8_out=True) for the W8A8 GEMM that consumes the same tensor
+# next (its own quantisation launch is then skipped): id(tensor) -> (weakref, q, s). The weakref makes a
+# freed (and possibly address-reused) tensor miss; entries die with their tensor.
+_PREQ = {}
+
+
+class _PreQScratch:
+    """Separate from _QSCRATCH: between add_norm and its consumer another W8A8 call may quantise into that."""
+
+    def __init__(self):
+        self.q = self.s = None
+
+    def get(self, M, K, device):
+        if self.q is None or self.q.numel() < M * K or self.s.numel() < M or self.q.device != device:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError(f"fp8 norm-output scratch for [{M}, {K}] must be allocated before graph capture")
+            self.q = torch.empty(max(M * K, 0 if self.q is None else self.q.numel()), dtype=torch.uint8, device=device)
+            self.s = torch.empty(max(M, 0 if self.s is None else self.s.numel()), dtype=torch.float32, device=device)
+        return self.q[:M * K].view(M, K), self.s[:M]
+
+
+_PRESCRATCH = _PreQScratch()
+
+
+def _prequant_of(x):
+    e = _PREQ.get(id(x))
+    if e is None or e[0]() is not x:
+        return None
+    return e[1], e[2]
 
 
 def dequant_fp8_rows(q, scale, out=None):
@@ -494,10 +552,10 @@ def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hi
             nt_hint, split_hint = tuned
         if nt_hint & W8A8_FLAG:
             return linear_w8a8(x, w, w_scale, bias, act, glu, out, (nt_hint >> 8) & 15, (nt_hint >> 12) & 15,
-                               split_hint)
+                               split_hint, partial_ok=partial_ok)
         if M > _FP8_PREFILL_M and not nt_hint and tuned is None:
             if _W8A8:  # compute-bound: per-token fp8 activations on the MX-fp8 matrix cores
-                return linear_w8a8(x, w, w_scale, bias, act, glu, out)
+                return linear_w8a8(x, w, w_scale, bias, act, glu, out, partial_ok=partial_ok)
             wd = _DEQ.get(w.numel(), x.device)[: w.numel()].view(w.shape)
             dequant_fp8_rows(w, w_scale, out=wd)
             return linear(x, wd, bias, act, glu, None, out, 0, split_hint, partial_ok)
@@ -567,15 +625,25 @@ def linear_qkv(x, w, bias, positions, cos, sin, k_cache, v_cache, slots, nh, nkv
     return y if rc == 0 else None
 
 
-def add_norm_partial(p: PartialSum, weight, bias, eps, rms, residual, out=None):
+def add_norm_partial(p: PartialSum, weight, bias, eps, rms, residual, out=None, fp8_out=False):
     T, H = p.M, p.N
     _check(residual is not None and residual.is_contiguous() and residual.shape == (T, H), "residual [T, H]")
     _check(weight.numel() == H and weight.dtype == torch.bfloat16 and weight.is_contiguous(), "norm weight")
     y = out if out is not None else torch.empty(T, H, dtype=torch.bfloat16, device=residual.device)
+    q8, s8 = _fp8_twin(y) if fp8_out else (None, None)
     lib().add_norm_partial(p.buf.data_ptr(), p.S, T * H, _ptr(p.bias), residual.data_ptr(), residual.data_ptr(),
                            weight.data_ptr(), _ptr(bias), y.data_ptr(), y.stride(0), T, H, float(eps), bool(rms),
-                           _stream())
+                           _stream(), _ptr(q8), _ptr(s8))
     return y, residual
+
+
+def w8a8_planned(M: int, N: int, K: int, glu: bool) -> bool:
+    """Whether an fp8-weight linear of this shape runs W8A8 (per-token fp8 activations) at M rows: the tuned
+    table's plan, else the static rule (W8A8 above _FP8_PREFILL_M rows)."""
+    tuned = lib().gemm_tuned_get(M, N, K, bool(glu), 1)
+    if tuned is not None:
+        return bool(tuned[0] & W8A8_FLAG)
+    return _W8A8 and M > _FP8_PREFILL_M
 
 
 def quant_fp8_rows(w):

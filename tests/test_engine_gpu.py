@@ -398,3 +398,23 @@ def test_gqa_decode_on_mfma_extend_kernel(kv_heads):
     _assert_logits_close(got.cpu(), ref.cpu())
     cos = torch.nn.functional.cosine_similarity(got, ref, dim=-1).min().item()
     assert cos > 0.9999, cos
+
+
+def test_fp8_norm_twin_matches_separate_quantisation():
+    """add_norm's per-token fp8 twin (fp8_out) feeds the W8A8 GEMMs exactly what their own quantisation launch
+    would: a W8A8 prefill (M > 128 rows) gives bit-identical logits with and without the fused twin."""
+    from llmss_amd.engine import build_model
+
+    m = build_model("tiny-llama", None, "bf16", torch.device("cuda", 0), fp8=True, random_init=True)
+    assert m.w.layers[0].qkv.w_scale is not None
+    T = 200
+    ids = torch.randint(0, m.cfg.vocab_size, (T,), device="cuda")
+    inp = StepInput("prefill", ids, torch.arange(T, device="cuda"), torch.full((T,), -1, device="cuda"),
+                    cu_seqlens=torch.tensor([0, T], dtype=torch.int32, device="cuda"), max_seqlen=T,
+                    last_idx=torch.tensor([T - 1], device="cuda"))
+    kv = m.allocate_kv_cache(16, 16)
+    m._norm_quant = False
+    ref = m(inp, kv).float()
+    m._norm_quant = True
+    got = m(inp, kv).float()
+    assert torch.equal(got, ref)
