@@ -403,9 +403,9 @@ def test_gqa_decode_on_mfma_extend_kernel(kv_heads):
 def test_fp8_norm_twin_matches_separate_quantisation():
     """add_norm's per-token fp8 twin (fp8_out) feeds the W8A8 GEMMs exactly what their own quantisation launch
     would: a W8A8 prefill (M > 128 rows) gives bit-identical logits with and without the fused twin."""
-    from llmss_amd.engine import build_model
-
-    m = build_model("tiny-llama", None, "bf16", torch.device("cuda", 0), fp8=True, random_init=True)
+    cfg = get_preset("tiny-llama", hidden_size=512, num_heads=8, num_kv_heads=2, head_dim=64, rotary_dim=64,
+                     intermediate_size=1024, max_position_embeddings=512)
+    m = DecoderLM(cfg, random_weights(cfg, device="cuda", dtype=torch.bfloat16, seed=4, std=0.05, fp8=True))
     assert m.w.layers[0].qkv.w_scale is not None
     T = 200
     ids = torch.randint(0, m.cfg.vocab_size, (T,), device="cuda")
