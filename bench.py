@@ -319,10 +319,14 @@ def run_config(args, model_name, tp, batch, progress, dp=False, client=None):
     # of the multi-rank bench (tests/test_bench_dist.py), not a performance number
     dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
     local_batch = batch // world if dp else batch
+    t_setup = time.perf_counter()
     model = build_model(model_name, tp if not dp else None, "bf16", dev, fp8=args.fp8, random_init=True)
+    t_model = time.perf_counter() - t_setup
     max_len = min(model.cfg.max_position_embeddings, max(256, args.prompt_len + args.gen_len))
     eng = LLMEngine(model, max_num_seqs=local_batch, max_batched_tokens=max(8192, local_batch * args.prompt_len),
                     block_size=16, max_model_len=max_len, use_graphs=not args.no_graphs, kv_dtype=args.kv_dtype)
+    # engine init = KV pool + GEMM autotune + attention routing + decode-graph capture (and its TBO A/B)
+    setup_s = {"model": round(t_model, 2), "engine": round(time.perf_counter() - t_setup - t_model, 2)}
     rng = np.random.default_rng(1234 + (tp.rank if dp else 0))
     V = model.cfg.vocab_size
 
@@ -364,7 +368,7 @@ def run_config(args, model_name, tp, batch, progress, dp=False, client=None):
             torch.distributed.barrier()  # CPU (gloo) group with the native RCCL data plane
 
     progress(f"engine ready: {model.cfg.model_type} {'dp' if dp else 'tp'}={world} batch={batch} "
-             f"kv_blocks={eng.num_blocks} graphs={sorted({b for b, _ in eng.graphs})}")
+             f"kv_blocks={eng.num_blocks} graphs={sorted({b for b, _ in eng.graphs})} setup_s={setup_s}")
     if eng.tuned:
         mx = max(m for _, m in eng.tuned)
         progress("autotuned GEMMs at M=%d: " % mx + ", ".join(
@@ -416,6 +420,7 @@ def run_config(args, model_name, tp, batch, progress, dp=False, client=None):
         "rccl_world_size": (torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1),
         "comm_backend": tp.backend if not dp else "none (independent replicas)",
         "rank_elapsed_s": [round(v, 4) for v in rank_el],
+        "setup_s": setup_s,
         "p50_tpot_ms": round(float(tpot), 3),
         "p50_ttft_ms": round(float(ttft), 3),
         "p50_request_latency_ms": round(float(e2e), 3),
