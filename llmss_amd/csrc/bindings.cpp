@@ -78,6 +78,7 @@ void launch_dequant_fp8_rows(const void* q, const void* scale, void* w, int64_t 
 
 void register_runtime(py::module_& m);  // host-side C++ runtime (runtime.cpp)
 void register_comm(py::module_& m);     // RCCL communicator (comm.cpp)
+void register_ctrl(py::module_& m);     // shared-memory control ring (ctrl.cpp)
 
 #define P(x) reinterpret_cast<void*>(static_cast<uintptr_t>(x))
 #define CP(x) reinterpret_cast<const void*>(static_cast<uintptr_t>(x))
@@ -211,4 +212,5 @@ PYBIND11_MODULE(_C, m) {
   });
   register_runtime(m);
   register_comm(m);
+  register_ctrl(m);
 }

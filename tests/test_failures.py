@@ -45,9 +45,9 @@ def test_deadline_aborts_request(ckpt):
         drv.stop()
 
 
-def _worker(rank, world, port, ckpt, role, q):
+def _worker(rank, world, port, ckpt, role, q, ctrl="shm"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+                      LOCAL_RANK=str(rank), LLMSS_CTRL=ctrl)
     torch.set_num_threads(1)
     from llmss_amd.engine import LLMEngine, SamplingParams, build_model
     from llmss_amd.parallel.dist import initialize_distributed
@@ -76,17 +76,17 @@ def _worker(rank, world, port, ckpt, role, q):
             os._exit(0)  # leader vanishes without a word
         t0 = time.time()
         drv._thread.join(60)
-        q.put(("follower", drv.error is not None, time.time() - t0, str(drv.error)[:200]))
+        q.put(("follower", drv.error is not None, time.time() - t0, str(drv.error)[:200], drv.ctrl))
         q.close()
         q.join_thread()
         os._exit(0)
 
 
-def _spawn(world, ckpt, role):
+def _spawn(world, ckpt, role, ctrl="shm"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, ckpt, role, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, ckpt, role, q, ctrl)) for r in range(world)]
     for p in procs:
         p.start()
     return procs, q
@@ -102,8 +102,9 @@ def _drain(q, n, timeout):
     return out
 
 
-def test_follower_crash_fails_inflight_requests(ckpt):
-    procs, q = _spawn(2, ckpt, "follower_crash")
+@pytest.mark.parametrize("ctrl", ["shm", "gloo"])
+def test_follower_crash_fails_inflight_requests(ckpt, ctrl):
+    procs, q = _spawn(2, ckpt, "follower_crash", ctrl)
     try:
         res = {r[0]: r for r in _drain(q, 2, 150)}
         assert "leader" in res, res
@@ -118,13 +119,19 @@ def test_follower_crash_fails_inflight_requests(ckpt):
     assert procs[1].exitcode == 17  # the injected exit
 
 
-def test_leader_loss_detected_by_follower(ckpt):
-    procs, q = _spawn(2, ckpt, "leader_loss")
+@pytest.mark.parametrize("ctrl", ["shm", "gloo"])
+def test_leader_loss_detected_by_follower(ckpt, ctrl):
+    """gloo: the heartbeat timeout (leader_timeout_s = 5 s) ends the follower. shm ring: the follower sees
+    the leader's process gone while it waits for the next record (no timeout needed)."""
+    procs, q = _spawn(2, ckpt, "leader_loss", ctrl)
     try:
         res = _drain(q, 1, 120)
         assert res and res[0][0] == "follower", res
-        _, errored, waited, msg = res[0]
+        _, errored, waited, msg, mode = res[0]
         assert errored and waited < 60, res
+        assert mode == ("shm-ring" if ctrl == "shm" else "gloo"), res
+        if ctrl == "shm":
+            assert "producer process died" in msg, res
     finally:
         for p in procs:
             p.join(30)
