@@ -299,7 +299,7 @@ def run_served(args, eng, client, progress, world, rank_sync):
             progress(f"grpc step {i}: {reps[-1]['tokens']} tokens, {time.perf_counter() - t0:.3f}s elapsed")
         rank_sync()
         el = time.perf_counter() - t0
-        dstats = dict(drv.stats)
+        dstats = dict(drv.stats, ctrl=drv.ctrl)
     finally:
         server.stop(0).wait()
         drv.stop()
