@@ -149,29 +149,54 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const bf16_t* __restr
 // blocks are dispatched last-first so the long causal rows start early.
 // LDS rows are unpadded (DMA writes 1 KiB per wave-instruction linearly) with the 16-B chunk index
 // XOR-swizzled by the row: chunk' = chunk ^ (row & (SW-1)), applied on the source side of the DMA.
-template <int D, int QB>
-__global__ __launch_bounds__(256, 2) void attn_prefill_v2_kernel(const bf16_t* __restrict__ qkv, int64_t row_stride,
+// FAST (v3): the same structure with a lighter softmax - the v2 loop issues ~2x more VALU than its 64
+// MFMAs per tile can cover (MI355X_MICROARCH "vector-instruction ISSUE cost": 2 fillers per 16x16x32 gap):
+//   * the causal / length mask only on tiles that cross the wave's diagonal or the sequence end;
+//   * the row max on raw scores and the scale folded into the exponent (one fma per score);
+//   * v_exp_f32 directly (no denormal range fix-ups: p < 2^-126 flushes to 0);
+//   * deferred rescale (guide T13): the running max moves only when a row's max grows by more than 8
+//     (log2 units), so p <= 2^8 and the O *= alpha sweep runs only when some row of the wave moved -
+//     every l-side and o-side factor of a tile uses the same per-row alpha;
+//   * the row sum accumulates the fp32 probabilities (v2 summed the bf16-rounded ones).
+// NW: waves per workgroup (4: two workgroups per CU; 8: one 512-thread workgroup per CU whose K/V tile
+// feeds twice the query rows, halving the LDS-DMA traffic per FLOP).
+template <int D, int QB, bool FAST, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 2) void attn_prefill_v2_kernel(const bf16_t* __restrict__ qkv, int64_t row_stride,
                                                                  int T, const int* __restrict__ cu_seqlens,
                                                                  bf16_t* __restrict__ out, int64_t out_stride, int nh,
                                                                  int nkv, int GH, int k_off, int v_off,
-                                                                 float scale_log2) {
+                                                                 float scale_log2, int nqb, int nseq) {
   constexpr int BKV = 64;
   constexpr int CH = D / 8;                    // 16-B chunks per row
   constexpr int SW = CH < 16 ? CH : 16;        // swizzle span (conflict-free b128 reads of 16 rows)
   constexpr int TILE = BKV * D * 2;            // bytes of one K (or V) tile
   constexpr int RPI = 64 / CH;                 // rows per 1-KiB DMA wave-instruction
-  constexpr int LPW = BKV / RPI / 4;           // DMA instructions per wave per tile (K and V each)
+  constexpr int LPW = BKV / RPI / NW;          // DMA instructions per wave per tile (K and V each)
   static_assert(LPW >= 1, "tile / wave split");
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE];  // [slot][K, V]
 
   const int G = nh / nkv;
-  const int WPH = 4 / GH;                      // waves per query head
+  const int WPH = NW / GH;                     // waves per query head
   const int BQ = WPH * 16 * QB;
-  const int nqb = gridDim.x;
-  const int qb = nqb - 1 - (int)blockIdx.x;    // heavy (late) query blocks first
-  const int b = blockIdx.z;
+  // 1-D grid over (sequence, head group, query block). Workgroups are dealt round-robin to the 8 XCDs,
+  // so consecutive ids share no L2: when the (sequence, head group) pairs split evenly over the XCDs,
+  // every query block of one pair is sent to the same XCD (ids of one XCD = one residue mod 8) and
+  // that pair's K/V is fetched into one L2 instead of eight. Within an XCD: heavy (late) blocks first.
   const int ngrp = G / GH;
-  const int kvh = blockIdx.y / ngrp, grp = blockIdx.y % ngrp;
+  const int npair = nkv * ngrp * nseq;
+  const int L = (int)blockIdx.x;
+  int pair, qi_;
+  if ((npair & 7) == 0) {
+    const int slot = L >> 3;
+    pair = (L & 7) + 8 * (slot / nqb);
+    qi_ = slot % nqb;
+  } else {
+    pair = L / nqb;
+    qi_ = L % nqb;
+  }
+  const int qb = nqb - 1 - qi_;
+  const int b = pair / (nkv * ngrp);
+  const int kvh = (pair % (nkv * ngrp)) / ngrp, grp = pair % ngrp;
   const int tok0 = cu_seqlens[b];
   const int len = cu_seqlens[b + 1] - tok0;
   const int q0 = qb * BQ;
@@ -191,7 +216,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_v2_kernel(const bf16_t* _
   uint32_t voff[LPW];                          // per-lane (row, source-swizzled chunk) of each instruction
 #pragma unroll
   for (int i = 0; i < LPW; ++i) {
-    const int r = (i * 4 + w) * RPI + lane / CH, c = lane % CH;
+    const int r = (i * NW + w) * RPI + lane / CH, c = lane % CH;
     voff[i] = (uint32_t)(r * row_stride * 2 + ((c ^ (r & (SW - 1))) << 4));
   }
   // k position folded into the voffset (the range check covers voffset), soffset 0
@@ -200,9 +225,9 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_v2_kernel(const bf16_t* _
     char* sk_ = smem + ((J_) & 1) * 2 * TILE;                                                                  \
     const uint32_t kb_ = (uint32_t)((J_) * BKV) * (uint32_t)row_stride * 2u;                                   \
     _Pragma("unroll") for (int i_ = 0; i_ < LPW; ++i_) {                                                       \
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (LDS_AS void*)(sk_ + (i_ * 4 + w) * 1024), 16,              \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (LDS_AS void*)(sk_ + (i_ * NW + w) * 1024), 16,             \
                                                (uint32_t)(voff[i_] + kb_), (uint32_t)0, 0, 0);                 \
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (LDS_AS void*)(sk_ + TILE + (i_ * 4 + w) * 1024), 16,       \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (LDS_AS void*)(sk_ + TILE + (i_ * NW + w) * 1024), 16,      \
                                                (uint32_t)(voff[i_] + kb_), (uint32_t)0, 0, 0);                 \
     }                                                                                                          \
   } while (0)
@@ -257,6 +282,50 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_v2_kernel(const bf16_t* _
     }
     // ---- mask + online softmax per row block (lane owns query row wrow + 16 qi + li) -------------
     s16x8 pf[QB][2];
+    if constexpr (FAST) {
+      const bool need_mask = (kv0 + BKV - 1 > wrow) || (kv0 + BKV > len);  // wave-uniform
+#pragma unroll
+      for (int qi = 0; qi < QB; ++qi) {
+        const int qrow = wrow + qi * 16 + li;
+        float mx = -1.0e30f;
+        if (need_mask) {
+#pragma unroll
+          for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int key = kv0 + kt * 16 + 4 * g + i;
+              const float v = (key <= qrow && key < len) ? s[qi][kt][i] : -1.0e30f;
+              s[qi][kt][i] = v;
+              mx = fmaxf(mx, v);
+            }
+        } else {
+#pragma unroll
+          for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s[qi][kt][i]);
+        }
+        mx = xor32_max(xor16_max(mx)) * scale_log2;
+        const bool resc = mx > m[qi] + 8.f;
+        const float alpha = resc ? __builtin_amdgcn_exp2f(m[qi] - mx) : 1.f;
+        if (resc) m[qi] = mx;
+        const float nm = -m[qi];
+        float ps = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[qi][kt][i], scale_log2, nm));
+            ps += p;
+            pf[qi][kt >> 1][(kt & 1) * 4 + i] = (short)f2bf(p);
+          }
+        ps = xor32_sum(xor16_sum(ps));
+        lsum[qi] = lsum[qi] * alpha + ps;
+        if (__ballot(resc)) {
+#pragma unroll
+          for (int i = 0; i < D / 16; ++i) o[qi][i] *= alpha;
+        }
+      }
+    } else {
 #pragma unroll
     for (int qi = 0; qi < QB; ++qi) {
       const int qrow = wrow + qi * 16 + li;
@@ -287,6 +356,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_v2_kernel(const bf16_t* _
       lsum[qi] = lsum[qi] * alpha + ps;
 #pragma unroll
       for (int i = 0; i < D / 16; ++i) o[qi][i] *= alpha;
+    }
     }
     // ---- O^T += V^T P^T (V^T by transpose reads of the swizzled V tile), each V fragment feeds QB MFMAs
 #pragma unroll
@@ -322,8 +392,11 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_v2_kernel(const bf16_t* _
   }
 }
 
-static int g_prefill_version = 2;
-void attn_prefill_set_version(int v) { g_prefill_version = v == 1 ? 1 : 2; }
+// version 3 (default): v2 with the light softmax; waves per workgroup 0 = auto (8 for D = 256, else 4)
+static int g_prefill_version = 3;
+static int g_prefill_nw = 0;
+void attn_prefill_set_waves(int nw) { g_prefill_nw = (nw == 4 || nw == 8) ? nw : 0; }
+void attn_prefill_set_version(int v) { g_prefill_version = (v >= 1 && v <= 3) ? v : 3; }
 
 void launch_attn_prefill(const void* qkv, int64_t row_stride, int T, const void* cu_seqlens, void* out,
                          int64_t out_stride, int B, int max_seqlen, int nh, int nkv, int D, int k_off, int v_off,
@@ -334,20 +407,30 @@ void launch_attn_prefill(const void* qkv, int64_t row_stride, int T, const void*
   auto CU = (const int*)cu_seqlens;
   auto O = (bf16_t*)out;
   const float sl = scale * kLog2eP;
-  // v2 except where v1 measured faster (bench/attn_prefill_bench.py, profiles/r2_prefill_attn): D = 256
-  // (GPT-J: one row block per wave fits the registers) and D = 64 beyond 2K-token sequences
-  if (g_prefill_version == 2 && D != 256 && !(D == 64 && max_seqlen > 2048)) {
+  // v3 by default (profiles/r3_prefill_attn, bench/attn_prefill_bench.py: faster than v1 and v2 on every
+  // measured config); v2 keeps round 2's dispatch (v1 for D = 256 and D = 64 beyond 2K tokens)
+  const bool fast = g_prefill_version == 3;
+  if (fast || (g_prefill_version == 2 && D != 256 && !(D == 64 && max_seqlen > 2048))) {
     if (row_stride % 8 || k_off % 8 || v_off % 8)
       throw std::runtime_error("attn_prefill: 16-B aligned rows and k/v offsets required");
     if ((uint64_t)64 * row_stride * 2 >= (1ull << 31)) throw std::runtime_error("attn_prefill: row stride too large");
     const int G = nh / nkv;
-    const int GH = G % 4 == 0 ? 4 : (G % 2 == 0 ? 2 : 1);
-    const int QB = 2;
-    const int BQ = (4 / GH) * 16 * QB;
-    dim3 grid((max_seqlen + BQ - 1) / BQ, nkv * (G / GH), B);
-    switch (D) {
-      case 64: attn_prefill_v2_kernel<64, 2><<<grid, 256, 0, st>>>(Q, row_stride, T, CU, O, out_stride, nh, nkv, GH, k_off, v_off, sl); break;
-      case 128: attn_prefill_v2_kernel<128, 2><<<grid, 256, 0, st>>>(Q, row_stride, T, CU, O, out_stride, nh, nkv, GH, k_off, v_off, sl); break;
+    const int NW = !fast ? 4 : (g_prefill_nw ? g_prefill_nw : (D == 256 ? 8 : 4));
+    const int GH = (NW == 8 && G % 8 == 0) ? 8 : (G % 4 == 0 ? 4 : (G % 2 == 0 ? 2 : 1));
+    const int QB = D == 256 ? 1 : 2;  // D = 256: one row block per wave keeps O + Q in the register budget
+    const int BQ = (NW / GH) * 16 * QB;
+    const int nqb = (max_seqlen + BQ - 1) / BQ;
+    dim3 grid(nqb * nkv * (G / GH) * B);
+    const int key = (D * 2 + (fast ? 1 : 0)) * 16 + NW;
+    switch (key) {
+      case 128 * 16 + 4: attn_prefill_v2_kernel<64, 2, false><<<grid, 256, 0, st>>>(Q, row_stride, T, CU, O, out_stride, nh, nkv, GH, k_off, v_off, sl, nqb, B); break;
+      case 129 * 16 + 4: attn_prefill_v2_kernel<64, 2, true><<<grid, 256, 0, st>>>(Q, row_stride, T, CU, O, out_stride, nh, nkv, GH, k_off, v_off, sl, nqb, B); break;
+      case 129 * 16 + 8: attn_prefill_v2_kernel<64, 2, true, 8><<<grid, 512, 0, st>>>(Q, row_stride, T, CU, O, out_stride, nh, nkv, GH, k_off, v_off, sl, nqb, B); break;
+      case 256 * 16 + 4: attn_prefill_v2_kernel<128, 2, false><<<grid, 256, 0, st>>>(Q, row_stride, T, CU, O, out_stride, nh, nkv, GH, k_off, v_off, sl, nqb, B); break;
+      case 257 * 16 + 4: attn_prefill_v2_kernel<128, 2, true><<<grid, 256, 0, st>>>(Q, row_stride, T, CU, O, out_stride, nh, nkv, GH, k_off, v_off, sl, nqb, B); break;
+      case 257 * 16 + 8: attn_prefill_v2_kernel<128, 2, true, 8><<<grid, 512, 0, st>>>(Q, row_stride, T, CU, O, out_stride, nh, nkv, GH, k_off, v_off, sl, nqb, B); break;
+      case 513 * 16 + 4: attn_prefill_v2_kernel<256, 1, true><<<grid, 256, 0, st>>>(Q, row_stride, T, CU, O, out_stride, nh, nkv, GH, k_off, v_off, sl, nqb, B); break;
+      case 513 * 16 + 8: attn_prefill_v2_kernel<256, 1, true, 8><<<grid, 512, 0, st>>>(Q, row_stride, T, CU, O, out_stride, nh, nkv, GH, k_off, v_off, sl, nqb, B); break;
       default: throw std::runtime_error("attn_prefill: head_dim must be 64, 128 or 256");
     }
     HIP_CHECK_LAUNCH();

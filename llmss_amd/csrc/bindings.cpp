@@ -27,6 +27,7 @@ void launch_attn_prefill(const void* qkv, int64_t row_stride, int T, const void*
                          int64_t out_stride, int B, int max_seqlen, int nh, int nkv, int D, int k_off, int v_off,
                          float scale, hipStream_t st);
 void attn_prefill_set_version(int v);
+void attn_prefill_set_waves(int nw);
 void gemm_big_set_group(int g);
 void launch_cand_topk(const void* logits, int64_t ld, int B, int vl, int lo, int V, const void* temperature,
                       const void* top_k, int K, int KC, void* pack, int64_t ldp, hipStream_t st, int shards);
@@ -122,6 +123,7 @@ PYBIND11_MODULE(_C, m) {
     launch_attn_prefill(CP(qkv), rs, T, CP(cu), P(out), os, B, maxlen, nh, nkv, D, k_off, v_off, scale, S(st));
   });
   m.def("attn_prefill_set_version", &attn_prefill_set_version);
+  m.def("attn_prefill_set_waves", &attn_prefill_set_waves);
   m.def("gemm_big_set_group", &gemm_big_set_group);
   m.def("cand_topk", [](uintptr_t lg, int64_t ld, int B, int vl, int lo, int V, uintptr_t temp, uintptr_t topk, int K,
                         int KC, uintptr_t pack, int64_t ldp, uintptr_t st, int shards) {

@@ -141,25 +141,30 @@ def test_qkv_gemm_rope_cache_epilogue(style, D, rot, nh, nkv, bias, tile, split,
         close(a.nan_to_num(0), r.nan_to_num(0), 1e-2)
 
 
-@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("version,waves", [(1, 0), (2, 0), (3, 4), (3, 8)])
 @pytest.mark.parametrize("D,nh,nkv", [(64, 4, 4), (128, 8, 2), (128, 16, 1), (256, 4, 4), (128, 12, 4), (128, 16, 2),
                                       (64, 6, 3), (256, 8, 2)])
-def test_attn_prefill(D, nh, nkv, version):
-    """v1 (register-staged tiles) and v2 (LDS-DMA two-slot ring, 2 row blocks per wave, GQA heads
-    sharing a K/V tile) against the fp32 oracle; qkv as a row-strided view, NaN-filled output."""
+@pytest.mark.parametrize("lens", [(1, 70, 129, 5, 300), (1, 70, 129, 5, 300, 64, 17, 200)])
+def test_attn_prefill(D, nh, nkv, version, waves, lens):
+    """v1 (register-staged tiles), v2 (LDS-DMA two-slot ring, 2 row blocks per wave, GQA heads sharing a
+    K/V tile) and v3 (v2 + light softmax, 4 or 8 waves per workgroup) against the fp32 oracle; qkv as a
+    row-strided view, NaN-filled output. Eight sequences make the (sequence, head group) pairs a multiple
+    of 8, i.e. the XCD-grouped block order of v2/v3; five do not (plain order)."""
     torch.manual_seed(0)
-    lens = [1, 70, 129, 5, 300]
+    lens = list(lens)
     T = sum(lens)
     W = (nh + 2 * nkv) * D
     qkv = rnd(T, W + 64)[:, :W]  # row stride > width (as a fused-QKV view would have)
     cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=dev)
     sc = 1 / math.sqrt(D)
     H.lib().attn_prefill_set_version(version)
+    H.lib().attn_prefill_set_waves(waves)
     try:
         out = torch.full((T, nh * D), float("nan"), dtype=torch.bfloat16, device=dev)
         H.attn_prefill(qkv, cu, max(lens), nh, nkv, D, sc, out=out)
     finally:
-        H.lib().attn_prefill_set_version(2)
+        H.lib().attn_prefill_set_version(3)
+        H.lib().attn_prefill_set_waves(0)
     ref = R.attn_prefill(qkv.float(), cu.cpu(), nh, nkv, D, sc)
     close(out, ref, 2e-2)
 
