@@ -151,6 +151,22 @@ def test_gpu_chunked_engine_matches_whole_prompt(tmp_path, name):
     eng = _engine(d, 8, dev, "bf16", use_graphs=False, autotune=False)
     got = eng.generate(_prompts(), sp)
     assert eng.stats["mixed_decode_tokens"] > 0
-    # bf16: the chunked path adds the same terms in another order; rare argmax flips are tolerated
-    agree = sum(a == b for x, y in zip(got, ref) for a, b in zip(x, y)) / sum(len(x) for x in ref)
-    assert agree >= 0.9, (got, ref)
+    # bf16: the chunked path adds the same terms in another order, so a greedy pick may flip where the
+    # fp32 model itself has a near tie (the top-2 margin under 0.1 on these ~3-logit tiny models; a
+    # measured case: 3.204 vs 3.157). Every token must match up to such a tie; after a tie the
+    # sequences are conditioned on different tokens and comparison stops.
+    from transformers import AutoModelForCausalLM
+
+    hf = AutoModelForCausalLM.from_pretrained(d).float().eval()
+    compared = 0
+    for p, g, r in zip(_prompts(), got, ref):
+        for k, (a, b) in enumerate(zip(g, r)):
+            if a == b:
+                compared += 1
+                continue
+            with torch.no_grad():
+                top2 = hf(torch.tensor([p + r[:k]])).logits[0, -1].topk(2).values
+            assert float(top2[0] - top2[1]) < 0.1, ("chunked and whole-prompt runs differ at a clear margin",
+                                                    name, k, top2.tolist(), got, ref)
+            break
+    assert compared >= 0.6 * sum(len(x) for x in ref), (compared, got, ref)
