@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--S", default="128,2048,4096,8192")
     ap.add_argument("--heads", default="32:32:128,32:8:128,64:8:128,16:16:256,25:25:64")
     ap.add_argument("--tokens", type=int, default=16384)
+    ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--versions", default="1,2,3:4,3:8", help="kernel version[:waves per workgroup]")
     a = ap.parse_args()
     dev = torch.device("cuda")
@@ -40,7 +41,7 @@ def main():
                 for _ in range(3):
                     H.attn_prefill(qkv, cu, S, nh, nkv, D, D ** -0.5, out=out)
                 torch.cuda.synchronize()
-                it = 10
+                it = a.iters
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
                 for _ in range(it):
