@@ -1,6 +1,6 @@
 """Decode-attention micro-benchmark: paged KV read bandwidth per configuration.
 
-usage: python bench/attn_bench.py [--B 64] [--ctx 192,1024] [--heads 32:32,32:8]
+usage: python bench/attn_bench.py [--B 64] [--ctx 192,1024] [--heads 32:32,32:8] [--bs 16]
 """
 import argparse
 import os
@@ -21,8 +21,9 @@ def main():
     ap.add_argument("--random-pages", action="store_true", help="scatter pages (default: engine-like sequential)")
     ap.add_argument("--splits", default="", help="context splits to sweep (default: the engine's decode_splits)")
     ap.add_argument("--unrolls", default="1,2,4,11,12,14")
+    ap.add_argument("--bs", type=int, default=16, help="KV cache block (page) size in tokens")
     a = ap.parse_args()
-    dev, bs, D = "cuda", 16, a.D
+    dev, bs, D = "cuda", a.bs, a.D
     for hk in a.heads.split(","):
         nh, nkv = map(int, hk.split(":"))
         for ctx in map(int, a.ctx.split(",")):

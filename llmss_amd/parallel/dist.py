@@ -352,7 +352,26 @@ def initialize_distributed(timeout_s: Optional[int] = None, backend: Optional[st
             kwargs["pg_options"] = _pg_options(backend)
         dist.init_process_group(**kwargs)
     tp = world_size // dp
-    comm = _native_comm(rank, dp, tp) if native and tp > 1 else None
+    comm, err = None, ""
+    if native and tp > 1:
+        try:
+            comm = _native_comm(rank, dp, tp)
+        except Exception as e:  # noqa: BLE001 - decided collectively below
+            err = str(e)
+        ok = torch.tensor([0 if err else 1], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # CPU (gloo) world group: every rank takes the same path
+        if not int(ok[0]):
+            if comm is not None:
+                comm.abort()
+                comm = None
+            if dp != 1:
+                raise RuntimeError(f"rank {rank}: native RCCL communicator failed ({err or 'on a peer'})")
+            # one replica: fall back to torch's RCCL process group for the data plane (same library, c10d's
+            # bootstrap and stream handling) instead of failing the run
+            log.warning("rank %d: native RCCL communicator failed (%s); data plane on torch's nccl group",
+                        rank, err or "on a peer")
+            data = dist.new_group(list(range(world_size)), backend="nccl", pg_options=_pg_options("nccl"))
+            return TPGroup(rank, world_size, group=data), rank, world_size
     log.info("rank %d/%d initialised: process group %s, data plane %s", rank, world_size, backend,
              "native RCCL" if comm is not None else backend)
     if dp == 1:
