@@ -48,7 +48,12 @@ void launch_attn_decode_fused(const void* qkv, int64_t q_stride, const void* par
 int launch_gemm_qkv_args(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y, int64_t ldy,
                          int M, int N, int K, void* workspace, int64_t ws_bytes, int nt_hint, int split_hint,
                          const void* pos, const void* cos_t, const void* sin_t, void* kc, void* vc, const void* slot,
-                         int nh, int nkv, int D, int rot, int block_size, int style, bool do_rope, hipStream_t st);
+                         int nh, int nkv, int D, int rot, int block_size, int style, bool do_rope, hipStream_t st,
+                         const void* rstat, const void* c1, float inv_k, float eps);
+int launch_gemm_fold_args(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y,
+                          int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace, int64_t ws_bytes,
+                          int nt_hint, int split_hint, const void* rstat, const void* c1, float inv_k, float eps,
+                          void* wstat, hipStream_t st);
 int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_fp8, const void* w_scale,
                 const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace,
                 int64_t ws_bytes, int nt_hint, int split_hint, bool partial_out, hipStream_t st);
@@ -153,10 +158,24 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_qkv", [](uintptr_t x, int64_t ldx, uintptr_t w, int64_t ldw, uintptr_t bias, uintptr_t y, int64_t ldy,
                        int M, int N, int K, uintptr_t work, int64_t wbytes, int nt_hint, int split_hint, uintptr_t pos,
                        uintptr_t cos_t, uintptr_t sin_t, uintptr_t kc, uintptr_t vc, uintptr_t slot, int nh, int nkv,
-                       int D, int rot, int bs, int style, bool do_rope, uintptr_t st) {
+                       int D, int rot, int bs, int style, bool do_rope, uintptr_t st, uintptr_t rstat, uintptr_t c1,
+                       float inv_k, float eps) {
     return launch_gemm_qkv_args(CP(x), ldx, CP(w), ldw, CP(bias), P(y), ldy, M, N, K, P(work), wbytes, nt_hint,
                                 split_hint, CP(pos), CP(cos_t), CP(sin_t), P(kc), P(vc), CP(slot), nh, nkv, D, rot, bs,
-                                style, do_rope, S(st));
+                                style, do_rope, S(st), CP(rstat), CP(c1), inv_k, eps);
+  }, pybind11::arg("x"), pybind11::arg("ldx"), pybind11::arg("w"), pybind11::arg("ldw"), pybind11::arg("bias"),
+     pybind11::arg("y"), pybind11::arg("ldy"), pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"),
+     pybind11::arg("work"), pybind11::arg("wbytes"), pybind11::arg("nt_hint"), pybind11::arg("split_hint"),
+     pybind11::arg("pos"), pybind11::arg("cos_t"), pybind11::arg("sin_t"), pybind11::arg("kc"), pybind11::arg("vc"),
+     pybind11::arg("slot"), pybind11::arg("nh"), pybind11::arg("nkv"), pybind11::arg("D"), pybind11::arg("rot"),
+     pybind11::arg("bs"), pybind11::arg("style"), pybind11::arg("do_rope"), pybind11::arg("st"),
+     pybind11::arg("rstat") = 0, pybind11::arg("c1") = 0, pybind11::arg("inv_k") = 0.f, pybind11::arg("eps") = 0.f);
+  m.def("gemm_fold", [](uintptr_t x, int64_t ldx, uintptr_t w, int64_t ldw, uintptr_t bias, uintptr_t y, int64_t ldy,
+                        int M, int N, int K, int act, bool glu, uintptr_t work, int64_t wbytes, int nt_hint,
+                        int split_hint, uintptr_t rstat, uintptr_t c1, float inv_k, float eps, uintptr_t wstat,
+                        uintptr_t st) {
+    return launch_gemm_fold_args(CP(x), ldx, CP(w), ldw, CP(bias), P(y), ldy, M, N, K, act, glu, P(work), wbytes,
+                                 nt_hint, split_hint, CP(rstat), CP(c1), inv_k, eps, P(wstat), S(st));
   });
   m.def("gemm_plan", [](int M, int N, int K, bool fp8) {
     int nt, s;

@@ -588,8 +588,53 @@ def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hi
     return y
 
 
+def _fold_args(x, rstat, c1, eps, N):
+    """Validated (rstat ptr, c1 ptr, 1 / K, eps) of a norm-fold consumer (ops/reference.py linear_fold)."""
+    if rstat is None:
+        return 0, 0, 0.0, 0.0
+    M, K = x.shape
+    _check(rstat.dtype == torch.float32 and rstat.is_contiguous() and rstat.shape == (M, 2), "rstat [M, 2] fp32")
+    if c1 is not None:
+        _check(c1.dtype == torch.float32 and c1.is_contiguous() and c1.numel() == N, "c1 [N] fp32")
+    return rstat.data_ptr(), _ptr(c1), 1.0 / K, float(eps)
+
+
+def linear_fold(x, w, bias=None, act="none", glu=False, rstat=None, c1=None, eps=0.0, resid=None, wstat=None,
+                nt_hint=0, split_hint=0):
+    """Norm-fold GEMM (csrc/gemm.hip launch_gemm_epi; semantics: ops/reference.py linear_fold). Consumer:
+    ``rstat`` [M, 2] row statistics of ``x`` (the raw residual stream), ``c1`` the LayerNorm mean correction
+    (None for RMSNorm) -> new bf16 output. Producer: ``resid`` [M, N] updated in place (+= x @ w^T + bias) and
+    its new row statistics added into ``wstat`` [M, 2]. Tuned kinds 4 / 5 (ops/autotune.py tune_fold)."""
+    M, K = x.shape
+    _bf16_rows(x, "x")
+    _bf16_rows(w, "w")
+    _check(w.dim() == 2 and w.is_contiguous() and w.shape[1] == K, "fold weights are bf16 [N, K]")
+    N = w.shape[0]
+    _check(K % 16 == 0, "K must be a multiple of 16")
+    if bias is not None:
+        _check(bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.numel() == N, "bias [N] bf16")
+    ws = _GEMM_WS.get(64 << 20, x.device)
+    if resid is not None:
+        _check(rstat is None and not glu and act in ("none", None), "the producer takes no consumer epilogue")
+        _check(resid.dtype == torch.bfloat16 and resid.shape == (M, N) and resid.stride(1) == 1, "resid [M, N] bf16")
+        _check(wstat is not None and wstat.dtype == torch.float32 and wstat.is_contiguous()
+               and wstat.shape == (M, 2), "wstat [M, 2] fp32")
+        y, rs, c1p, inv_k, ep, wsp = resid, 0, 0, 0.0, 0.0, wstat.data_ptr()
+    else:
+        _check(rstat is not None, "fold consumer needs rstat")
+        if glu:
+            _check(N % 32 == 0, "glu needs N % 32 == 0")
+        y = torch.empty(M, N // 2 if glu else N, dtype=x.dtype, device=x.device)
+        rs, c1p, inv_k, ep = _fold_args(x, rstat, c1, eps, N)
+        wsp = 0
+    lib().gemm_fold(x.data_ptr(), x.stride(0), w.data_ptr(), K, _ptr(bias), y.data_ptr(), y.stride(0), M, N, K,
+                    _ACT[act], bool(glu), ws.data_ptr(), ws.numel() * 4, int(nt_hint), int(split_hint), rs, c1p,
+                    inv_k, ep, wsp, _stream())
+    return y
+
+
 def linear_qkv(x, w, bias, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, rot, style, do_rope=True,
-               nt_hint=0, split_hint=0):
+               nt_hint=0, split_hint=0, rstat=None, c1=None, eps=0.0):
     """QKV projection whose GEMM epilogue applies RoPE and writes k / v into the paged cache (one launch
     instead of GEMM + rope_cache; same values). Returns the bf16 [T, N] qkv tensor, or None when this
     weight / cache / plan cannot take the fused epilogue (packed or fp8 weights, fp8 KV rows, streaming or
@@ -609,6 +654,7 @@ def linear_qkv(x, w, bias, positions, cos, sin, k_cache, v_cache, slots, nh, nkv
     if do_rope:
         _check(cos.dtype == torch.float32 and cos.is_contiguous() and cos.shape[1] == rot // 2, "cos table")
         _check(sin.shape == cos.shape and sin.is_contiguous(), "sin table")
+    rs, c1p, inv_k, ep = _fold_args(x, rstat, c1, eps, N)
     bs = 1
     if k_cache is not None:
         _kv_cache_check(k_cache, v_cache, nkv, D)
@@ -621,7 +667,7 @@ def linear_qkv(x, w, bias, positions, cos, sin, k_cache, v_cache, slots, nh, nkv
                         ws.data_ptr(), ws.numel() * 4, int(nt_hint), int(split_hint), positions.data_ptr(),
                         _ptr(cos) if do_rope else 0, _ptr(sin) if do_rope else 0, _ptr(k_cache), _ptr(v_cache),
                         _ptr(slots) if k_cache is not None else 0, nh, nkv, D, rot, bs, 1 if style == "gptj" else 0,
-                        do_rope, _stream())
+                        do_rope, _stream(), rs, c1p, inv_k, ep)
     return y if rc == 0 else None
 
 

@@ -642,3 +642,87 @@ def test_w8a8_decode_plan_in_graph(M):
     ref = R.linear(R.dequant_fp8(xq, xs), q, b.float(), w_scale=s)
     close(y, ref, 2e-2)
     assert not torch.equal(eager, y)  # the replay read the new activations
+
+
+def _row_stats(h):
+    hf = h.float()
+    return torch.stack([hf.sum(1), hf.pow(2).sum(1)], 1).contiguous()
+
+
+@pytest.mark.parametrize("tile,split", [(0, 0), (3, 1), (3, 4), (2, 2), (11, 1), (11, 3), (10, 2), (1, 1), (8, 2),
+                                        (9, 1), (12, 2)])
+@pytest.mark.parametrize("M", [1, 37, 64, 200])
+@pytest.mark.parametrize("mode", ["rms", "ln_gelu", "rms_glu"])
+def test_gemm_norm_fold_consumer(tile, split, M, mode):
+    """Norm-fold consumer epilogue (rstd * acc - rstd * mean * c1, then bias / GELU / SwiGLU) on every tile and
+    split (a split runs as an in-launch combine) vs the fp32 oracle ops/reference.py linear_fold; the same value
+    as the unfolded add_norm + GEMM up to bf16 rounding."""
+    torch.manual_seed(0)
+    K, N = 1600, 1024
+    h = rnd(M, K, scale=2.0) + 0.3
+    w = rnd(N, K, scale=K ** -0.5)
+    b = rnd(N, scale=0.1) if mode != "rms" else None
+    ln = mode.startswith("ln")
+    glu = mode.endswith("glu")
+    act = "gelu_tanh" if mode == "ln_gelu" else "none"
+    c1 = w.float().sum(1).contiguous() if ln else None
+    rst = _row_stats(h)
+    d = 16 if tile not in (0, 1, 9) else 0
+    hint = (tile | d) << 8 if tile else 0
+    y = H.linear_fold(h, w, b, act, glu, rstat=rst, c1=c1, eps=1e-5, nt_hint=hint, split_hint=split)
+    y_ref = R.linear_fold(h, w, b, act, glu, rstat=rst, c1=c1, eps=1e-5)
+    close(y, y_ref, 2e-2)
+    # == explicit norm (no affine) + plain GEMM
+    xn, _ = R.add_norm(h, torch.ones(K, dtype=torch.bfloat16, device=dev),
+                       torch.zeros(K, dtype=torch.bfloat16, device=dev) if ln else None, 1e-5, not ln)
+    close(y, R.linear(xn, w, b, act, glu), 5e-2)
+
+
+@pytest.mark.parametrize("tile,split", [(0, 0), (3, 1), (3, 8), (2, 4), (11, 2), (10, 1), (1, 2), (8, 1), (12, 3)])
+@pytest.mark.parametrize("M,N", [(1, 4096), (64, 4096), (64, 1600), (130, 1000), (512, 4096)])
+def test_gemm_norm_fold_producer(tile, split, M, N):
+    """Norm-fold producer epilogue: h += x @ w^T + bias in place and the new rows' (sum, sum^2) added into
+    wstat by fp32 atomics (pre-filled wstat: accumulation, not overwrite)."""
+    torch.manual_seed(0)
+    K = 1024
+    x, w, b = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
+    h = rnd(M, N)
+    ws = torch.rand(M, 2, device=dev)
+    h_ref, ws_ref = h.clone(), ws.clone()
+    d = 16 if tile not in (0, 1, 9) else 0
+    hint = (tile | d) << 8 if tile else 0
+    H.linear_fold(x, w, b, resid=h, wstat=ws, nt_hint=hint, split_hint=split)
+    R.linear_fold(x, w, b, resid=h_ref, wstat=ws_ref)
+    close(h, h_ref, 2e-2)
+    # the sums are over the kernel's own bf16 outputs: compare with the stats of what it wrote
+    close(ws, ws_ref - _row_stats(h_ref) + _row_stats(h), 1e-3, 1e-4)
+    close(ws, ws_ref, 1e-1, 2e-2)
+
+
+@pytest.mark.parametrize("style,D,rot,nh,nkv", [("neox", 128, 128, 8, 2), ("none", 64, 0, 6, 6)])
+@pytest.mark.parametrize("ln", [False, True])
+@pytest.mark.parametrize("tile,split", [(3, 1), (11, 2), (2, 1)])
+def test_qkv_epilogue_with_norm_fold(style, D, rot, nh, nkv, ln, tile, split):
+    """QKV GEMM with RoPE + KV write AND the norm-fold consumer epilogue == norm (no affine) + QKV epilogue."""
+    torch.manual_seed(0)
+    K, T, bs, nb = 512, 40, 16, 8
+    N = (nh + 2 * nkv) * D
+    h, w = rnd(T, K, scale=1.5) + 0.2, rnd(N, K, scale=K ** -0.5)
+    b = rnd(N, scale=0.1) if ln else None
+    do_rope = style != "none"
+    pos = torch.randint(0, 120, (T,), device=dev)
+    cos, sin = R.rope_tables(128, rot if do_rope else 64, 10000.0, dev)
+    slots = torch.randperm(nb * bs, device=dev)[:T]
+    c1 = w.float().sum(1).contiguous() if ln else None
+    hint = (tile | 16) << 8
+    caches = [torch.zeros(nb, nkv, bs, D, dtype=torch.bfloat16, device=dev) for _ in range(4)]
+    y = H.linear_qkv(h, w, b, pos, cos, sin, caches[0], caches[1], slots, nh, nkv, D, rot, "neox", do_rope,
+                     nt_hint=hint, split_hint=split, rstat=_row_stats(h), c1=c1, eps=1e-5)
+    assert y is not None
+    xn, _ = R.add_norm(h, torch.ones(K, dtype=torch.bfloat16, device=dev),
+                       torch.zeros(K, dtype=torch.bfloat16, device=dev) if ln else None, 1e-5, not ln)
+    y2 = H.linear_qkv(xn, w, b, pos, cos, sin, caches[2], caches[3], slots, nh, nkv, D, rot, "neox", do_rope,
+                      nt_hint=hint, split_hint=split)
+    close(y, y2, 5e-2)
+    close(caches[0], caches[2], 5e-2)
+    close(caches[1], caches[3], 5e-2)
