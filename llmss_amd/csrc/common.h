@@ -378,43 +378,47 @@ __device__ __forceinline__ void tile_store_lds(const f32x4 (&acc)[MT][NT], char*
           for (int e = 0; e < 8 && ng + 16 + e < N; ++e) dst[e] = o[e];
       }
     } else if (qe.wstat) {  // norm-fold producer: h += acc + bias in place, row (sum, sum^2) of the new h
-      // VPR consecutive threads hold one row (NTHR % VPR == 0, rows * VPR a multiple of VPR): the
-      // whole group runs the same iterations, so its partial sums reduce by shuffles inside the group
+      // per-row partial sums gather in LDS (rowf, beside the image), then one global atomic pair per row
       constexpr int VPR = BN / 8;
-      static_assert(NTHR % VPR == 0 && VPR <= 64, "row groups must tile the workgroup");
+      for (int r = threadIdx.x; r < 2 * rows; r += NTHR) rowf[r] = 0.f;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
       for (int v = threadIdx.x; v < rows * VPR; v += NTHR) {
         const int r = v / VPR, c = (v - r * VPR) * 8;
         const int m = m0 + r0 + r, n = n0 + c;
+        if (m >= M || n >= N) continue;
         const bool full = n + 7 < N && (ldy & 7) == 0;
+        bf16_t* dst = Y + (int64_t)m * ldy + n;
+        u16x8 h;
+        if (full) h = *reinterpret_cast<const u16x8*>(dst);
+        else
+          for (int e = 0; e < 8; ++e) h[e] = n + e < N ? dst[e] : (bf16_t)0;
+        u16x8 o;
         float s1 = 0.f, s2 = 0.f;
-        if (m < M && n < N) {
-          bf16_t* dst = Y + (int64_t)m * ldy + n;
-          u16x8 h;
-          if (full) h = *reinterpret_cast<const u16x8*>(dst);
-          else
-            for (int e = 0; e < 8; ++e) h[e] = n + e < N ? dst[e] : (bf16_t)0;
-          u16x8 o;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            float x = ct[r * LDW + c + e] + bf2f(h[e]);
-            if (bias && n + e < N) x += bf2f(bias[n + e]);
-            o[e] = f2bf(x);
-            const float q = n + e < N ? bf2f(o[e]) : 0.f;
-            s1 += q;
-            s2 += q * q;
-          }
-          if (full) *reinterpret_cast<u16x8*>(dst) = o;
-          else
-            for (int e = 0; e < 8 && n + e < N; ++e) dst[e] = o[e];
+        for (int e = 0; e < 8; ++e) {
+          float x = ct[r * LDW + c + e] + bf2f(h[e]);
+          if (bias && n + e < N) x += bf2f(bias[n + e]);
+          o[e] = f2bf(x);
+          const float q = n + e < N ? bf2f(o[e]) : 0.f;
+          s1 += q;
+          s2 += q * q;
         }
-#pragma unroll
-        for (int o = VPR / 2; o > 0; o >>= 1) {
-          s1 += __shfl_xor(s1, o, VPR);
-          s2 += __shfl_xor(s2, o, VPR);
-        }
-        if ((threadIdx.x & (VPR - 1)) == 0 && m < M) {
-          atomicAdd(qe.wstat + 2 * m, s1);
-          atomicAdd(qe.wstat + 2 * m + 1, s2);
+        if (full) *reinterpret_cast<u16x8*>(dst) = o;
+        else
+          for (int e = 0; e < 8 && n + e < N; ++e) dst[e] = o[e];
+        atomicAdd(rowf + 2 * r, s1);
+        atomicAdd(rowf + 2 * r + 1, s2);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      for (int r = threadIdx.x; r < rows; r += NTHR) {
+        const int m = m0 + r0 + r;
+        if (m < M) {
+          atomicAdd(qe.wstat + 2 * m, rowf[2 * r]);
+          atomicAdd(qe.wstat + 2 * m + 1, rowf[2 * r + 1]);
         }
       }
     } else {  // bf16 rows: 8 values (16 B) per thread-step

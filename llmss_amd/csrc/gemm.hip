@@ -1615,7 +1615,7 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   float* part = s > 1 ? (float*)workspace : nullptr;
   const int act_k = s > 1 && !cnt ? 0 : act, glu_k = s > 1 && !cnt ? 0 : g;
   dim3 grid(nt, s);
-  if (tsel >= 8 && tsel <= 12) {
+  if (tsel >= 8 && tsel <= 13) {
     launch_gemm_mid(tsel, ns, wnt_ok(tsel_raw, M, tsel), X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, part, M, N, K,
                     act_k, glu_k, s, st, false, cnt, qe);
     if (cnt) return 0;

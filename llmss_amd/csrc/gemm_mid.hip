@@ -176,16 +176,24 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
                                                         act, glu, qe);
 }
 
-// tsel 8: 128x128 (2x2 waves), 9: 256x128 (4x2), 10: 64x256 (1x4), 11: 64x128 (1x4), 12: 128x256 (2x4)
-bool gemm_mid_dims(int tsel, int* bm, int* bn, int* threads) {
+// tsel 8: 128x128 (2x2 waves), 9: 256x128 (4x2), 10: 64x256 (1x4), 11: 64x128 (1x4), 12: 128x256 (2x4),
+// 13: 64x192 (2x2; a 12288-column QKV is 64 tiles, 4096 columns 22: one workgroup per CU without a K split)
+static bool mid_layout(int tsel, int* bm, int* bn, int* wm, int* wn) {
   switch (tsel) {
-    case 8: *bm = 128; *bn = 128; *threads = 256; return true;
-    case 9: *bm = 256; *bn = 128; *threads = 512; return true;
-    case 10: *bm = 64; *bn = 256; *threads = 256; return true;
-    case 11: *bm = 64; *bn = 128; *threads = 256; return true;
-    case 12: *bm = 128; *bn = 256; *threads = 512; return true;
+    case 8: *bm = 128; *bn = 128; *wm = 2; *wn = 2; return true;
+    case 9: *bm = 256; *bn = 128; *wm = 4; *wn = 2; return true;
+    case 10: *bm = 64; *bn = 256; *wm = 1; *wn = 4; return true;
+    case 11: *bm = 64; *bn = 128; *wm = 1; *wn = 4; return true;
+    case 12: *bm = 128; *bn = 256; *wm = 2; *wn = 4; return true;
+    case 13: *bm = 64; *bn = 192; *wm = 2; *wn = 2; return true;
     default: return false;
   }
+}
+bool gemm_mid_dims(int tsel, int* bm, int* bn, int* threads) {
+  int wm, wn;
+  if (!mid_layout(tsel, bm, bn, &wm, &wn)) return false;
+  *threads = 64 * wm * wn;
+  return true;
 }
 
 // largest ring depth <= want that fits the 160 KiB LDS
@@ -200,9 +208,9 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
                      int split, hipStream_t st, bool packed, int* cnt, const QkvEpi* qe) {
   const QkvEpi qv = qe ? *qe : QkvEpi{};
-  int bm, bn, thr;
-  if (!gemm_mid_dims(tsel, &bm, &bn, &thr)) throw std::runtime_error("gemm_mid: bad tile code");
-  if (glu && (bn / (thr / 64 / (bm == 256 ? 4 : (bm == 128 ? 2 : 1))) / 16) % 2)
+  int bm, bn, wm, wn;
+  if (!mid_layout(tsel, &bm, &bn, &wm, &wn)) throw std::runtime_error("gemm_mid: bad tile code");
+  if (glu && (bn / wn / 16) % 2)
     throw std::runtime_error("gemm_mid: SwiGLU needs an even number of 16-column tiles per wave");
   if ((uint64_t)bm * ldx * 2 >= (1ull << 31) || (uint64_t)bn * ldw * (packed ? 128 : 2) >= (1ull << 31))
     throw std::runtime_error("gemm_mid: row stride too large for 32-bit buffer offsets");
@@ -238,6 +246,8 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
              else MID(64, 256, 1, 4, 2); break;
     case 11: MID_NS(64, 128, 1, 4); break;
     case 12: if (ns >= 3) MID(128, 256, 2, 4, 3); else MID(128, 256, 2, 4, 2); break;
+    case 13: if (ns >= 5) MID(64, 192, 2, 2, 5); else if (ns == 4) MID(64, 192, 2, 2, 4);
+             else if (ns == 3) MID(64, 192, 2, 2, 3); else MID(64, 192, 2, 2, 2); break;
   }
 #undef MID_NS
 #undef MID

@@ -114,9 +114,12 @@ class DecoderLM:
         self._norm_quant = os.environ.get("LLMSS_FP8_NORM_QUANT", "1") != "0"
         self._cu_decode = {}
         self._comm_stream = None
-        # norm fold (TP = 1 decode): no add_norm launch inside the layer stack - see fold_norms
+        # norm fold (TP = 1 decode): no add_norm launch inside the layer stack - see fold_norms. Opt-in
+        # (LLMSS_NORM_FOLD=1): measured on MI355X it LOSES (profiles/r3_fold: Llama-2-7B 11.50 K vs 11.73 K
+        # tok/s, GPT-2-XL TPOT 3.66 vs 3.26 ms) - the o / down producers need finished sums, and the in-launch
+        # split-K combine behind them costs more (+5-7 us per GEMM) than the add_norm launches it removes
         if norm_fold is None:
-            norm_fold = os.environ.get("LLMSS_NORM_FOLD", "1") != "0" and weights.wte.is_cuda
+            norm_fold = os.environ.get("LLMSS_NORM_FOLD", "0") == "1" and weights.wte.is_cuda
         self.norm_fold = bool(norm_fold) and self.fold_norms()
 
     # ---------------------------------------------------------------------------- norm fold

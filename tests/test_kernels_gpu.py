@@ -210,8 +210,8 @@ def test_gemm(M, N, K):
 
 
 # 128x128, 64x128, 64x64, 256x256, 256x128 / 256x64 (8 waves); gemm_mid (buffer-descriptor staging):
-# 8 = 128x128, 9 = 256x128, 10 = 64x256, 11 = 64x128, 12 = 128x256
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12])
+# 8 = 128x128, 9 = 256x128, 10 = 64x256, 11 = 64x128, 12 = 128x256, 13 = 64x192
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13])
 @pytest.mark.parametrize("stages", [2, 3, 4, 6])
 @pytest.mark.parametrize("split", [1, 3, 8])
 @pytest.mark.parametrize("M,N,K", [(64, 1536, 4096), (200, 4800, 1600), (37, 256, 64 * 5 + 16), (700, 1312, 192)])
@@ -233,7 +233,7 @@ def test_gemm_tiled_variants(tile, stages, split, M, N, K):
           R.linear(x.float(), w.float(), None, glu=True), 2e-2)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 5, 6, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("tile", [1, 2, 3, 5, 6, 8, 9, 10, 11, 12, 13])
 @pytest.mark.parametrize("split", [2, 3, 8])
 @pytest.mark.parametrize("M,N,K", [(64, 1536, 4096), (200, 4800, 1600), (37, 256, 64 * 5 + 16), (512, 2752, 4096)])
 def test_gemm_splitk_combine_in_launch(tile, split, M, N, K):
@@ -650,7 +650,7 @@ def _row_stats(h):
 
 
 @pytest.mark.parametrize("tile,split", [(0, 0), (3, 1), (3, 4), (2, 2), (11, 1), (11, 3), (10, 2), (1, 1), (8, 2),
-                                        (9, 1), (12, 2)])
+                                        (9, 1), (12, 2), (13, 1), (13, 5)])
 @pytest.mark.parametrize("M", [1, 37, 64, 200])
 @pytest.mark.parametrize("mode", ["rms", "ln_gelu", "rms_glu"])
 def test_gemm_norm_fold_consumer(tile, split, M, mode):
@@ -678,7 +678,8 @@ def test_gemm_norm_fold_consumer(tile, split, M, mode):
     close(y, R.linear(xn, w, b, act, glu), 5e-2)
 
 
-@pytest.mark.parametrize("tile,split", [(0, 0), (3, 1), (3, 8), (2, 4), (11, 2), (10, 1), (1, 2), (8, 1), (12, 3)])
+@pytest.mark.parametrize("tile,split", [(0, 0), (3, 1), (3, 8), (2, 4), (11, 2), (10, 1), (1, 2), (8, 1), (12, 3),
+                                        (13, 1), (13, 3)])
 @pytest.mark.parametrize("M,N", [(1, 4096), (64, 4096), (64, 1600), (130, 1000), (512, 4096)])
 def test_gemm_norm_fold_producer(tile, split, M, N):
     """Norm-fold producer epilogue: h += x @ w^T + bias in place and the new rows' (sum, sum^2) added into
@@ -718,6 +719,9 @@ def test_qkv_epilogue_with_norm_fold(style, D, rot, nh, nkv, ln, tile, split):
     caches = [torch.zeros(nb, nkv, bs, D, dtype=torch.bfloat16, device=dev) for _ in range(4)]
     y = H.linear_qkv(h, w, b, pos, cos, sin, caches[0], caches[1], slots, nh, nkv, D, rot, "neox", do_rope,
                      nt_hint=hint, split_hint=split, rstat=_row_stats(h), c1=c1, eps=1e-5)
+    if do_rope and {3: 64, 11: 128, 2: 128}[tile] % D:  # neox partner columns must share the tile
+        assert y is None
+        return
     assert y is not None
     xn, _ = R.add_norm(h, torch.ones(K, dtype=torch.bfloat16, device=dev),
                        torch.zeros(K, dtype=torch.bfloat16, device=dev) if ln else None, 1e-5, not ln)
@@ -726,3 +730,20 @@ def test_qkv_epilogue_with_norm_fold(style, D, rot, nh, nkv, ln, tile, split):
     close(y, y2, 5e-2)
     close(caches[0], caches[2], 5e-2)
     close(caches[1], caches[3], 5e-2)
+
+
+@pytest.mark.parametrize("variant,nt", [(1, 1), (1, 2), (2, 1), (2, 2)])
+@pytest.mark.parametrize("split", [1, 4])
+@pytest.mark.parametrize("M", [17, 33, 64])
+def test_gemm_streaming_kernels_up_to_64_rows(variant, nt, split, M):
+    """The weight-streaming kernels (four 16-row MFMA tiles per wave at M = 49-64) are autotuner candidates
+    up to M = 64: explicit hints vs the fp32 oracle, with bias / GELU / SwiGLU epilogues and split-K."""
+    torch.manual_seed(0)
+    N, K = 2752, 4096
+    x, w, b = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
+    hint = nt + 16 * variant
+    close(H.linear(x, w, b, nt_hint=hint, split_hint=split), R.linear(x.float(), w.float(), b.float()), 2e-2)
+    close(H.linear(x, w, b, act="gelu_tanh", nt_hint=hint, split_hint=split),
+          R.linear(x.float(), w.float(), b.float(), act="gelu_tanh"), 2e-2)
+    close(H.linear(x, w, None, glu=True, nt_hint=hint, split_hint=split),
+          R.linear(x.float(), w.float(), None, glu=True), 2e-2)
