@@ -61,6 +61,7 @@ void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk);
 void gemm_tuned_set(int M, int N, int K, bool glu, int kind, int nt_hint, int split);
 void gemm_tuned_clear();
 void gemm_reserve_streamk(int n);
+void gemm_set_slot(int s);
 int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq, int64_t ldw, const void* wsc,
                      const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, int tile,
                      int depth, int split, void* workspace, int64_t ws_bytes, hipStream_t st, bool partial_out);
@@ -185,6 +186,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_tuned_set", &gemm_tuned_set);
   m.def("gemm_tuned_clear", &gemm_tuned_clear);
   m.def("gemm_reserve_streamk", &gemm_reserve_streamk);
+  m.def("gemm_set_slot", &gemm_set_slot);
   m.def("gemm_f8f8", [](uintptr_t xq, int64_t ldx, uintptr_t xs, uintptr_t wq, int64_t ldw, uintptr_t wsc,
                         uintptr_t bias, uintptr_t y, int64_t ldy, int M, int N, int K, int act, bool glu, int tile,
                         int depth, int split, uintptr_t work, int64_t wbytes, uintptr_t st, bool partial_out) {

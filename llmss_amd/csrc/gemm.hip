@@ -1518,22 +1518,29 @@ static std::mutex g_sk_mu;
 static int* g_sk_counters[64] = {};
 static int g_sk_capacity[64] = {};
 
+// workspace slot (gemm_set_slot): GEMM chains that may run concurrently on different streams (the two
+// half-batch decode chains, models/decoder.py) use disjoint counter ranges, as they use disjoint workspaces
+static constexpr int kSlots = 4;
+static thread_local int g_ws_slot = 0;
+void gemm_set_slot(int s) { g_ws_slot = s & (kSlots - 1); }
+
 static int* sk_counters(int n) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) throw std::runtime_error("gemm counters: bad device");
   std::lock_guard<std::mutex> lk(g_sk_mu);
-  if (n <= g_sk_capacity[dev]) return g_sk_counters[dev];
+  if (n <= g_sk_capacity[dev]) return g_sk_counters[dev] + (size_t)g_ws_slot * g_sk_capacity[dev];
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   (void)hipStreamIsCapturing(nullptr, &cs);
   if (cs != hipStreamCaptureStatusNone) throw std::runtime_error("gemm counters must be allocated before capture");
   int cap = std::max(n, 1 << 16);
   int* p = nullptr;
-  if (hipMalloc(&p, (size_t)cap * sizeof(int)) != hipSuccess) throw std::runtime_error("gemm counters: hipMalloc");
-  if (hipMemset(p, 0, (size_t)cap * sizeof(int)) != hipSuccess) throw std::runtime_error("gemm counters: memset");
+  const size_t bytes = (size_t)cap * kSlots * sizeof(int);
+  if (hipMalloc(&p, bytes) != hipSuccess) throw std::runtime_error("gemm counters: hipMalloc");
+  if (hipMemset(p, 0, bytes) != hipSuccess) throw std::runtime_error("gemm counters: memset");
   (void)hipDeviceSynchronize();
   g_sk_counters[dev] = p;  // the old (smaller) buffer is left to the process: launches may still reference it
   g_sk_capacity[dev] = cap;
-  return p;
+  return p + (size_t)g_ws_slot * cap;
 }
 
 void gemm_reserve_streamk(int n) { sk_counters(n); }

@@ -239,7 +239,41 @@ class DecodeWorkspace:
         return self.po, self.pml
 
 
-_DECODE_WS = DecodeWorkspace()
+class _Slotted:
+    """One instance of a scratch / workspace class per workspace slot (``workspace_slot``): kernels of chains
+    that may run concurrently on different streams never share a buffer."""
+
+    def __init__(self, cls):
+        self._items = [cls() for _ in range(4)]
+
+    def __getattr__(self, name):
+        return getattr(self._items[_SLOT[0]], name)
+
+
+_SLOT = [0]
+
+
+class workspace_slot:
+    """``with workspace_slot(k):`` ops issued inside use workspace slot k (GEMM workspace / combine counters,
+    decode-attention partials, fp8 scratch) - for a chain that runs concurrently with slot 0's on another
+    stream. Host-side state at launch (and capture) time."""
+
+    def __init__(self, k: int):
+        self.k = int(k) & 3
+
+    def __enter__(self):
+        self.prev = _SLOT[0]
+        _SLOT[0] = self.k
+        lib().gemm_set_slot(self.k)
+        return self
+
+    def __exit__(self, *exc):
+        _SLOT[0] = self.prev
+        lib().gemm_set_slot(self.prev)
+        return False
+
+
+_DECODE_WS = _Slotted(DecodeWorkspace)
 
 
 def decode_splits(B: int, nkv: int, max_ctx: int, block_size: int) -> tuple:
@@ -345,7 +379,7 @@ class GemmWorkspace:
         return self.buf
 
 
-_GEMM_WS = GemmWorkspace()
+_GEMM_WS = _Slotted(GemmWorkspace)
 
 
 def reserve_workspace(device, gemm_bytes: int = 64 << 20, decode_rows: int = 0, nh: int = 0, D: int = 128,
@@ -405,7 +439,7 @@ class _QuantScratch:
         return self.q[:M * K].view(M, K), self.s[:M]
 
 
-_QSCRATCH = _QuantScratch()
+_QSCRATCH = _Slotted(_QuantScratch)
 
 
 class _DequantScratch:
@@ -418,7 +452,7 @@ class _DequantScratch:
         return self.buf
 
 
-_DEQ = _DequantScratch()
+_DEQ = _Slotted(_DequantScratch)
 
 
 _W8A8 = os.environ.get("LLMSS_FP8_W8A8", "1") != "0"
@@ -483,7 +517,7 @@ class _PreQScratch:
         return self.q[:M * K].view(M, K), self.s[:M]
 
 
-_PRESCRATCH = _PreQScratch()
+_PRESCRATCH = _Slotted(_PreQScratch)
 
 
 def _prequant_of(x):

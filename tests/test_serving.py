@@ -228,7 +228,7 @@ def test_admission_window_batches_a_burst(driver):
         hs.append(drv.submit(encode(tok, f"burst {i}"), SamplingParams(max_new_tokens=3, is_greedy=True)))
 
     old = drv.batch_window_s
-    drv.batch_window_s = 0.02
+    drv.batch_window_s = 0.1  # generous: the suite runs under parallel load (pytest -n)
     try:
         with cf.ThreadPoolExecutor(6) as ex:
             list(ex.map(sub, range(6)))
