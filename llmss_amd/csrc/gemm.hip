@@ -1188,7 +1188,14 @@ __global__ __launch_bounds__(256) void gemm_f8f8_kernel(const unsigned char* __r
   }
 }
 
-// tile: 1 = 128x128, 2 = 64x128, 3 = 64x64; ring depth 2-4; split-K over grid.y
+bool gemm_mid_dims(int tsel, int* bm, int* bn, int* threads);
+void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
+                     const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
+                     int split, hipStream_t st, bool packed, int* cnt, const QkvEpi* qe, const float* xs,
+                     const float* wsc);
+
+// tile: 1 = 128x128, 2 = 64x128, 3 = 64x64; ring depth 2-4; split-K over grid.y; 8-13: the gemm_mid tiles
+// (buffer-descriptor staging, csrc/gemm_mid.hip, fp8 MFMA variant; K % 128 == 0)
 // partial_out: a split plan without activation / GLU leaves its fp32 slabs [split, M, N] (scales applied, no
 // bias) in `workspace` for the consumer (rope_cache / add_norm sum them) and returns the split; else 0.
 int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq, int64_t ldw, const void* wsc,
@@ -1198,7 +1205,12 @@ int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq
   if (K % 16) throw std::runtime_error("gemm_f8f8: K must be a multiple of 16");
   if (glu && (N % 32)) throw std::runtime_error("gemm_f8f8: glu needs N % 32 == 0");
   if (!y && !partial_out) throw std::runtime_error("gemm_f8f8: output required");
-  const int bm = tile == 1 ? 128 : 64, bn = tile == 3 ? 64 : 128;
+  int bm = tile == 1 ? 128 : 64, bn = tile == 3 ? 64 : 128, thr = 256;
+  const bool mid = tile >= 8 && tile <= 13;
+  if (mid) {
+    if (K % 128) throw std::runtime_error("gemm_f8f8: gemm_mid tiles need K % 128 == 0");
+    gemm_mid_dims(tile, &bm, &bn, &thr);
+  }
   const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   const int nk = (K + TBK8 - 1) / TBK8;
   if (tile == 4 || (tile == 0 && K % 128 == 0 && ((M + 255) / 256) * ((N + 255) / 256) >= 192)) {
@@ -1233,7 +1245,10 @@ int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq
   auto Y = (bf16_t*)y;
 #define LF(BM_, BN_, NS_) \
   gemm_f8f8_kernel<BM_, BN_, NS_><<<grid, 256, 0, st>>>(A, ldx, XS, Bw, ldw, WSc, Bi, Y, ldy, part, M, N, K, act_k, glu_k)
-  if (tile == 1) {
+  if (mid) {
+    launch_gemm_mid(tile, depth, M <= bm, (const bf16_t*)xq, ldx, (const bf16_t*)wq, ldw, Bi, Y, ldy, part, M, N, K,
+                    act_k, glu_k, split, st, false, nullptr, nullptr, XS, WSc);
+  } else if (tile == 1) {
     if (depth >= 3) LF(128, 128, 3); else LF(128, 128, 2);
   } else if (tile == 2) {
     if (depth >= 4) LF(64, 128, 4); else if (depth == 3) LF(64, 128, 3); else LF(64, 128, 2);
@@ -1259,7 +1274,8 @@ int gemm_f8f8_partial_slabs(int M, int N, int K, bool glu, int act, int tile, in
   if (tile == 4 || (tile == 0 && K % 128 == 0 && ((M + 255) / 256) * ((N + 255) / 256) >= 192)) return 0;
   if (tile == 0)
     tile = ((M + 127) / 128) * ((N + 127) / 128) >= 240 ? 1 : (((M + 63) / 64) * ((N + 127) / 128) >= 240 ? 2 : 3);
-  const int bm = tile == 1 ? 128 : 64, bn = tile == 3 ? 64 : 128;
+  int bm = tile == 1 ? 128 : 64, bn = tile == 3 ? 64 : 128, thr;
+  if (tile >= 8 && tile <= 13) gemm_mid_dims(tile, &bm, &bn, &thr);
   const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   const int nk = (K + TBK8 - 1) / TBK8;
   if (split <= 0) {
@@ -1452,7 +1468,7 @@ bool gemm_mid_dims(int tsel, int* bm, int* bn, int* threads);
 void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
                      int split, hipStream_t st, bool packed = false, int* cnt = nullptr,
-                     const QkvEpi* qe = nullptr);
+                     const QkvEpi* qe = nullptr, const float* xs = nullptr, const float* wsc = nullptr);
 
 // tsel 8-12: gemm_mid (gemm_mid.hip: buffer-descriptor staging, 128x128 / 256x128 / 64x256 / 64x128 / 128x256)
 static int tile_dims(int tsel, int* bm, int* bn) {

@@ -22,12 +22,21 @@
 // the buffer builtins is cast to uint32_t explicitly: otherwise the host compilation pass of this
 // template fails overload resolution quietly and hipcc drops the kernel's launch stub (undefined
 // __device_stub__ at link time, no diagnostic).
-template <int BM, int BN, int WM, int WN, int NS, bool WNT, bool PK>
+// F8 (W8A8, csrc/gemm.hip launch_gemm_f8f8 tiles 8-13): A and B are fp8-e4m3 bytes (lda / ldb / K in bytes, K %
+// 128 == 0). A 128-byte k-step of fp8 has the byte layout of the 64-element bf16 one, so the staging, ring and
+// LDS image are shared; each (m, n) tile takes one MX-fp8 16x16x128 MFMA per k-step (the lane's 16-B chunks 2g
+// and 2g+1), and the per-token x per-channel scales xs[m] * ws[n] are applied to the accumulators before the
+// epilogue (or the split-K slabs / combine, which are linear in them).
+template <int BM, int BN, int WM, int WN, int NS, bool WNT, bool PK, bool F8 = false>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                               const bf16_t* __restrict__ B, int64_t ldb,
                                                               const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
                                                               int64_t ldy, float* __restrict__ part, int M, int N, int K,
-                                                              int act, int glu, int* __restrict__ cnt, QkvEpi qe) {
+                                                              int act, int glu, int* __restrict__ cnt, QkvEpi qe,
+                                                              const float* __restrict__ xs,
+                                                              const float* __restrict__ wsc) {
+  constexpr int ES = F8 ? 1 : 2;  // operand bytes per element
+  static_assert(!(F8 && PK), "fp8 weights are row-major");
   constexpr int NW = WM * WN;
   constexpr int MT = BM / WM / 16, NT = BN / WN / 16;  // 16x16 accumulator tiles per wave
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
@@ -45,7 +54,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
   const TileWork tw = tile_work(ntm, ntn, BM, BN);
   const int m0 = tw.m0, n0 = tw.n0, zk = tw.z;
 
-  const int nk_all = (K + 63) / 64;
+  const int nk_all = (K * ES + 127) / 128;  // 128-byte k-steps
   const int per = (nk_all + gridDim.y - 1) / gridDim.y;
   const int t0 = zk * per, t1 = min(nk_all, t0 + per);
 
@@ -53,26 +62,27 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
   // PK: weights packed [N/16][K64][16][64] (ldb = K64, the 64-wide k blocks per row): a k-step of a
   // 16-row panel is one contiguous 2-KiB block, so a stage streams BN/16 such blocks instead of BN
   // strided 128-B row pieces (+18 % HBM read rate, bench/stream_ceiling.hip)
-  const uint64_t abytes = (uint64_t)(M - m0) * (uint64_t)lda * 2;
-  const uint64_t bbytes = PK ? (uint64_t)((N - n0) / 16) * (uint64_t)ldb * 2048 : (uint64_t)(N - n0) * (uint64_t)ldb * 2;
-  const int64_t boff = PK ? (int64_t)(n0 / 16) * ldb * 1024 : (int64_t)n0 * ldb;
-  const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(A + (int64_t)m0 * lda), (short)0,
-                                                    (int)(abytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)abytes),
-                                                    0x00020000);
-  const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(B + boff), (short)0,
+  const uint64_t abytes = (uint64_t)(M - m0) * (uint64_t)lda * ES;
+  const uint64_t bbytes = PK ? (uint64_t)((N - n0) / 16) * (uint64_t)ldb * 2048 : (uint64_t)(N - n0) * (uint64_t)ldb * ES;
+  const int64_t boff = PK ? (int64_t)(n0 / 16) * ldb * 2048 : (int64_t)n0 * ldb * ES;  // bytes
+  const auto ra = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<char*>(reinterpret_cast<const char*>(A) + (int64_t)m0 * lda * ES), (short)0,
+      (int)(abytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)abytes), 0x00020000);
+  const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(reinterpret_cast<const char*>(B) + boff),
+                                                    (short)0,
                                                     (int)(bbytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)bbytes),
                                                     0x00020000);
   uint32_t va[AL], vb[BL];  // per-lane byte offsets (row, source-swizzled chunk), fixed over k
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
     const int row = (i * NW + w) * 8 + (lane >> 3);
-    va[i] = (uint32_t)(row * lda * 2 + (((lane & 7) ^ (row & 7)) << 4));
+    va[i] = (uint32_t)(row * lda * ES + (((lane & 7) ^ (row & 7)) << 4));
   }
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
     const int row = (i * NW + w) * 8 + (lane >> 3);
     vb[i] = PK ? (uint32_t)((row >> 4) * ldb * 2048 + (row & 15) * 128 + (((lane & 7) ^ (row & 7)) << 4))
-               : (uint32_t)(row * ldb * 2 + (((lane & 7) ^ (row & 7)) << 4));
+               : (uint32_t)(row * ldb * ES + (((lane & 7) ^ (row & 7)) << 4));
   }
   // one ring stage (k-step T_) into LDS slot SA_: AL + BL wave-instructions of 1 KiB (8 rows x 128 B);
   // the k position is the scalar soffset, the per-lane voffsets never change
@@ -109,7 +119,31 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
 
   // ONE copy of the MFMA body (a second, masked copy made hipcc shuffle every accumulator between
   // AGPRs and VGPRs each k-step); the K tail is zeroed in LDS instead (below)
+  // fp8: the lane's two 16-B chunks 2g, 2g+1 of each fragment row (one 16x16x128 MFMA per tile pair)
+  const int y0 = ((2 * g) ^ (li & 7)) << 4, y1 = ((2 * g + 1) ^ (li & 7)) << 4;
   auto compute = [&](const char* st) {
+    if constexpr (F8) {
+      typedef int __attribute__((ext_vector_type(8))) i32x8_t;
+      i32x8_t a[MT], b[NT];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(st + arow * 128 + t * 2048 + y0);
+        const u32x4 hi = *reinterpret_cast<const u32x4*>(st + arow * 128 + t * 2048 + y1);
+        a[t] = i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(st + A_BYTES + brow * 128 + t * 2048 + y0);
+        const u32x4 hi = *reinterpret_cast<const u32x4*>(st + A_BYTES + brow * 128 + t * 2048 + y1);
+        b[t] = i32x8_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[mt], b[nt], acc[mt][nt], 0, 0, 0, 127, 0, 127);
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int ao = s ? aoff1 : aoff0, bo = s ? boff1 : boff0;
@@ -126,7 +160,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
     }
   };
 
-  const bool ktail = (K & 63) != 0;
+  const bool ktail = ((K * ES) & 127) != 0;  // bf16 only: fp8 calls have K % 128 == 0 (host-checked)
 #pragma unroll
   for (int j = 0; j < NS - 1; ++j)
     if (t0 + j < t1) MID_STAGE(t0 + j, smem + j * STAGE);
@@ -162,6 +196,23 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
   }
 
 #undef MID_STAGE
+  if constexpr (F8) {  // per-token x per-channel scales (C layout: row 4g + i of tile mt, column li of tile nt)
+    float wsv[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = n0 + wn * (NT * 16) + nt * 16 + li;
+      wsv[nt] = n < N ? wsc[n] : 0.f;
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm * (MT * 16) + mt * 16 + 4 * g + i;
+        const float sx = m < M ? xs[m] : 0.f;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt][i] *= sx * wsv[nt];
+      }
+  }
   if (cnt) {  // split-K slices combine in this launch; the tile's last arriver runs the epilogue
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!splitk_combine<MT, NT>(acc, part, cnt, (n0 / BN) * ntm + m0 / BM, gridDim.y, zk, w, NW, lane,
@@ -206,7 +257,10 @@ static int mid_depth(int bm, int bn, int want) {
 
 void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
-                     int split, hipStream_t st, bool packed, int* cnt, const QkvEpi* qe) {
+                     int split, hipStream_t st, bool packed, int* cnt, const QkvEpi* qe, const float* xs,
+                     const float* wsc) {
+  const bool f8 = xs != nullptr;
+  if (f8 && (packed || !wsc || K % 128)) throw std::runtime_error("gemm_mid fp8: row-major weights, K % 128 == 0");
   const QkvEpi qv = qe ? *qe : QkvEpi{};
   int bm, bn, wm, wn;
   if (!mid_layout(tsel, &bm, &bn, &wm, &wn)) throw std::runtime_error("gemm_mid: bad tile code");
@@ -221,10 +275,16 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
   dim3 grid(tiles, split);
 #define MID1(BM_, BN_, WM_, WN_, NS_, WNT_, PK_)                                                                   \
   gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, WNT_, PK_><<<grid, 64 * WM_ * WN_, 0, st>>>(X, ldx, W, ldw, bias, Y, ldy, \
-                                                                                      part, M, N, K, act, glu, cnt, qv)
+                                                                                      part, M, N, K, act, glu, cnt, qv, \
+                                                                                      nullptr, nullptr)
+#define MID1F8(BM_, BN_, WM_, WN_, NS_, WNT_)                                                                      \
+  gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, WNT_, false, true><<<grid, 64 * WM_ * WN_, 0, st>>>(                    \
+      X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, cnt, qv, xs, wsc)
 #define MID(BM_, BN_, WM_, WN_, NS_)                                                                             \
   do {                                                                                                         \
-    if (packed) {                                                                                              \
+    if (f8) {                                                                                                  \
+      if (wnt) MID1F8(BM_, BN_, WM_, WN_, NS_, true); else MID1F8(BM_, BN_, WM_, WN_, NS_, false);            \
+    } else if (packed) {                                                                                       \
       if (wnt) MID1(BM_, BN_, WM_, WN_, NS_, true, true); else MID1(BM_, BN_, WM_, WN_, NS_, false, true);     \
     } else {                                                                                                   \
       if (wnt) MID1(BM_, BN_, WM_, WN_, NS_, true, false); else MID1(BM_, BN_, WM_, WN_, NS_, false, false);   \
@@ -252,5 +312,6 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
 #undef MID_NS
 #undef MID
 #undef MID1
+#undef MID1F8
   HIP_CHECK_LAUNCH();
 }

@@ -68,6 +68,10 @@ def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, 
             tiles = [3, 2] + ([1] if M > 64 else [])
             out += [(W8A8_FLAG | (t << 8) | (d << 12), s) for t in tiles for d in (2, 3, 4) for s in splits
                     if not (t == 1 and d > 3)]
+            if K % 128 == 0:  # gemm_mid tiles with the fp8 MFMA (buffer-descriptor staging, csrc/gemm_mid.hip)
+                mt = [11, 10, 13] + ([8, 12] if M > 64 else []) + ([9] if M >= 256 else [])
+                out += [(W8A8_FLAG | (t << 8) | (d << 12), s) for t in mt for d in (3, 4)
+                        for s in (1, 2, 3, 4, 5, 6, 8)]
             if M >= 256 and K % 128 == 0:
                 out.append((W8A8_FLAG | (4 << 8), 1))
         return out

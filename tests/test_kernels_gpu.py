@@ -747,3 +747,27 @@ def test_gemm_streaming_kernels_up_to_64_rows(variant, nt, split, M):
           R.linear(x.float(), w.float(), b.float(), act="gelu_tanh"), 2e-2)
     close(H.linear(x, w, None, glu=True, nt_hint=hint, split_hint=split),
           R.linear(x.float(), w.float(), None, glu=True), 2e-2)
+
+
+@pytest.mark.parametrize("tile,depth", [(11, 3), (11, 4), (10, 3), (13, 4), (8, 3), (12, 3), (9, 3)])
+@pytest.mark.parametrize("split", [1, 3])
+@pytest.mark.parametrize("M,N,K", [(64, 1280, 2048), (37, 4096, 1024), (300, 544, 3072), (512, 2752, 4096)])
+def test_gemm_w8a8_mid_tiles(tile, depth, split, M, N, K):
+    """W8A8 through the gemm_mid kernels (fp8 MFMA on the buffer-descriptor ring, scales in registers before the
+    epilogue): exact vs fp32 math on the same fp8 operands; slabs left to a consumer carry the scales."""
+    torch.manual_seed(0)
+    x, w, b = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
+    q, s = H.quant_fp8_rows(w)
+    xq, xs = H.quant_fp8_rows(x)
+    xd = R.dequant_fp8(xq, xs)
+    y = H.linear_w8a8(x, q, s, b, act="gelu_tanh", tile=tile, depth=depth, split=split)
+    close(y, R.linear(xd, q, b.float(), act="gelu_tanh", w_scale=s), 2e-2)
+    yg = H.linear_w8a8(x, q, s, None, glu=True, tile=tile, depth=depth, split=split)
+    close(yg, R.linear(xd, q, None, glu=True, w_scale=s), 2e-2)
+    p = H.linear_w8a8(x, q, s, None, tile=tile, depth=depth, split=split, partial_ok=True)
+    if isinstance(p, H.PartialSum):
+        res = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+        _, r = H.add_norm_partial(p, torch.ones(N, dtype=torch.bfloat16, device=dev), None, 1e-5, True, res)
+        close(r, R.linear(xd, q, None, w_scale=s), 2e-2)
+    else:
+        close(p, R.linear(xd, q, None, w_scale=s), 2e-2)
