@@ -74,28 +74,89 @@ __global__ __launch_bounds__(256) void attn_extend_kernel(
   const bf16_t* __restrict__ vc = (const bf16_t*)vcv;
   const unsigned char* __restrict__ kc8 = (const unsigned char*)kcv;
   const unsigned char* __restrict__ vc8 = (const unsigned char*)vcv;
-  for (int kv0 = 0; kv0 < kv_end; kv0 += BKV) {
-    __syncthreads();
+  // page ids of keys [0, kv_end) staged in LDS once: a tile's K/V loads then wait for no dependent
+  // block-table load (an L2 round trip per tile)
+  constexpr int kMaxPages = 512;
+  __shared__ int s_pages[kMaxPages];
+  const int npg = (kv_end + bs - 1) / bs;
+  const bool lds_pages = npg <= kMaxPages;
+  if (lds_pages)
+    for (int i = threadIdx.x; i < npg; i += 256) s_pages[i] = bt[i];
+  __syncthreads();
+  // Software pipeline: tile t+1's K/V chunks are loaded into registers while tile t is computed from LDS
+  // (the register set is written to LDS after the next barrier), so each tile no longer waits a full
+  // HBM round trip behind the previous tile's compute.
+  static_assert((BKV * CH) % 256 == 0, "whole 16-B chunks per thread");
+  constexpr int NCH = BKV * CH / 256;  // 16-B chunks per thread per tile
+  u16x8 kr[NCH], vr[NCH];
+  u32x2 kr8[NCH], vr8[NCH];
+  float ksr[NCH], vsr[NCH];
+  auto load_tile = [&](int kv0) {
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int c = threadIdx.x + j * 256;
+      const int r = c / CH, ch = c % CH;
+      const int key = min(kv0 + r, kv_end - 1);
+      const int blk = lds_pages ? s_pages[key / bs] : bt[key / bs];
+      const int64_t rowoff = ((int64_t)blk * nkv + kvh) * head_stride + (int64_t)(key % bs) * RB;
+      if constexpr (KV8) {
+        kr8[j] = *reinterpret_cast<const u32x2*>(kc8 + rowoff + ch * 8);
+        vr8[j] = *reinterpret_cast<const u32x2*>(vc8 + rowoff + ch * 8);
+        ksr[j] = *reinterpret_cast<const float*>(kc8 + rowoff + D);
+        vsr[j] = *reinterpret_cast<const float*>(vc8 + rowoff + D);
+      } else {
+        kr[j] = *reinterpret_cast<const u16x8*>(kc + rowoff + ch * 8);
+        vr[j] = *reinterpret_cast<const u16x8*>(vc + rowoff + ch * 8);
+      }
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int c = threadIdx.x + j * 256;
+      const int r = c / CH, ch = c % CH;
+      if constexpr (KV8) {
+        u16x8 kb, vb;
+#pragma unroll
+        for (int hw = 0; hw < 2; ++hw) {
+          const f32x2 a = __builtin_amdgcn_cvt_pk_f32_fp8(kr8[j][hw], false), c2 = __builtin_amdgcn_cvt_pk_f32_fp8(kr8[j][hw], true);
+          const f32x2 x = __builtin_amdgcn_cvt_pk_f32_fp8(vr8[j][hw], false), y = __builtin_amdgcn_cvt_pk_f32_fp8(vr8[j][hw], true);
+          kb[4 * hw] = f2bf(a[0] * ksr[j]); kb[4 * hw + 1] = f2bf(a[1] * ksr[j]);
+          kb[4 * hw + 2] = f2bf(c2[0] * ksr[j]); kb[4 * hw + 3] = f2bf(c2[1] * ksr[j]);
+          vb[4 * hw] = f2bf(x[0] * vsr[j]); vb[4 * hw + 1] = f2bf(x[1] * vsr[j]);
+          vb[4 * hw + 2] = f2bf(y[0] * vsr[j]); vb[4 * hw + 3] = f2bf(y[1] * vsr[j]);
+        }
+        *reinterpret_cast<u16x8*>(&Ks[r * LD + ch * 8]) = kb;
+        *reinterpret_cast<u16x8*>(&Vs[r * LD + ch * 8]) = vb;
+      } else {
+        *reinterpret_cast<u16x8*>(&Ks[r * LD + ch * 8]) = kr[j];
+        *reinterpret_cast<u16x8*>(&Vs[r * LD + ch * 8]) = vr[j];
+      }
+    }
+  };
+  // D = 256: the register set would cost the kernel its occupancy - staged chunk by chunk instead
+  constexpr bool PIPE = D <= 128;
+  auto stage_direct = [&](int kv0) {
 #pragma unroll
     for (int c = threadIdx.x; c < BKV * CH; c += 256) {
       const int r = c / CH, ch = c % CH;
       const int key = min(kv0 + r, kv_end - 1);
-      const int blk = bt[key / bs];
+      const int blk = lds_pages ? s_pages[key / bs] : bt[key / bs];
       const int64_t rowoff = ((int64_t)blk * nkv + kvh) * head_stride + (int64_t)(key % bs) * RB;
       if constexpr (KV8) {
-        const u32x2 k8 = *reinterpret_cast<const u32x2*>(kc8 + rowoff + ch * 8);
-        const u32x2 v8 = *reinterpret_cast<const u32x2*>(vc8 + rowoff + ch * 8);
-        const float ks = *reinterpret_cast<const float*>(kc8 + rowoff + D);
-        const float vs = *reinterpret_cast<const float*>(vc8 + rowoff + D);
+        kr8[0] = *reinterpret_cast<const u32x2*>(kc8 + rowoff + ch * 8);
+        vr8[0] = *reinterpret_cast<const u32x2*>(vc8 + rowoff + ch * 8);
+        ksr[0] = *reinterpret_cast<const float*>(kc8 + rowoff + D);
+        vsr[0] = *reinterpret_cast<const float*>(vc8 + rowoff + D);
         u16x8 kb, vb;
 #pragma unroll
         for (int hw = 0; hw < 2; ++hw) {
-          const f32x2 a = __builtin_amdgcn_cvt_pk_f32_fp8(k8[hw], false), c = __builtin_amdgcn_cvt_pk_f32_fp8(k8[hw], true);
-          const f32x2 x = __builtin_amdgcn_cvt_pk_f32_fp8(v8[hw], false), y = __builtin_amdgcn_cvt_pk_f32_fp8(v8[hw], true);
-          kb[4 * hw] = f2bf(a[0] * ks); kb[4 * hw + 1] = f2bf(a[1] * ks);
-          kb[4 * hw + 2] = f2bf(c[0] * ks); kb[4 * hw + 3] = f2bf(c[1] * ks);
-          vb[4 * hw] = f2bf(x[0] * vs); vb[4 * hw + 1] = f2bf(x[1] * vs);
-          vb[4 * hw + 2] = f2bf(y[0] * vs); vb[4 * hw + 3] = f2bf(y[1] * vs);
+          const f32x2 a = __builtin_amdgcn_cvt_pk_f32_fp8(kr8[0][hw], false), c2 = __builtin_amdgcn_cvt_pk_f32_fp8(kr8[0][hw], true);
+          const f32x2 x = __builtin_amdgcn_cvt_pk_f32_fp8(vr8[0][hw], false), y = __builtin_amdgcn_cvt_pk_f32_fp8(vr8[0][hw], true);
+          kb[4 * hw] = f2bf(a[0] * ksr[0]); kb[4 * hw + 1] = f2bf(a[1] * ksr[0]);
+          kb[4 * hw + 2] = f2bf(c2[0] * ksr[0]); kb[4 * hw + 3] = f2bf(c2[1] * ksr[0]);
+          vb[4 * hw] = f2bf(x[0] * vsr[0]); vb[4 * hw + 1] = f2bf(x[1] * vsr[0]);
+          vb[4 * hw + 2] = f2bf(y[0] * vsr[0]); vb[4 * hw + 3] = f2bf(y[1] * vsr[0]);
         }
         *reinterpret_cast<u16x8*>(&Ks[r * LD + ch * 8]) = kb;
         *reinterpret_cast<u16x8*>(&Vs[r * LD + ch * 8]) = vb;
@@ -104,7 +165,18 @@ __global__ __launch_bounds__(256) void attn_extend_kernel(
         *reinterpret_cast<u16x8*>(&Vs[r * LD + ch * 8]) = *reinterpret_cast<const u16x8*>(vc + rowoff + ch * 8);
       }
     }
+  };
+  if constexpr (PIPE) {
+    if (kv_end > 0) load_tile(0);
+  }
+  for (int kv0 = 0; kv0 < kv_end; kv0 += BKV) {
+    __syncthreads();  // every wave is done reading the previous tile
+    if constexpr (PIPE) store_tile();
+    else stage_direct(kv0);
     __syncthreads();
+    if constexpr (PIPE) {
+      if (kv0 + BKV < kv_end) load_tile(kv0 + BKV);
+    }
     if (kv0 > wave_qhi) continue;  // whole tile in this wave's causal future (barriers stay uniform)
 
     f32x4 s[4];
