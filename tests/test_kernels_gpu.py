@@ -210,8 +210,8 @@ def test_gemm(M, N, K):
 
 
 # 128x128, 64x128, 64x64, 256x256, 256x128 / 256x64 (8 waves); gemm_mid (buffer-descriptor staging):
-# 8 = 128x128, 9 = 256x128, 10 = 64x256, 11 = 64x128, 12 = 128x256, 13 = 64x192, 14 = 64x32
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14])
+# 8 = 128x128, 9 = 256x128, 10 = 64x256, 11 = 64x128, 12 = 128x256, 13 = 64x192, 14 = 64x32, 15 = 64x96
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("stages", [2, 3, 4, 6])
 @pytest.mark.parametrize("split", [1, 3, 8])
 @pytest.mark.parametrize("M,N,K", [(64, 1536, 4096), (200, 4800, 1600), (37, 256, 64 * 5 + 16), (700, 1312, 192)])
@@ -233,7 +233,7 @@ def test_gemm_tiled_variants(tile, stages, split, M, N, K):
           R.linear(x.float(), w.float(), None, glu=True), 2e-2)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 5, 6, 8, 9, 10, 11, 12, 13, 14])
+@pytest.mark.parametrize("tile", [1, 2, 3, 5, 6, 8, 9, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("split", [2, 3, 8])
 @pytest.mark.parametrize("M,N,K", [(64, 1536, 4096), (200, 4800, 1600), (37, 256, 64 * 5 + 16), (512, 2752, 4096)])
 def test_gemm_splitk_combine_in_launch(tile, split, M, N, K):
@@ -650,7 +650,7 @@ def _row_stats(h):
 
 
 @pytest.mark.parametrize("tile,split", [(0, 0), (3, 1), (3, 4), (2, 2), (11, 1), (11, 3), (10, 2), (1, 1), (8, 2),
-                                        (9, 1), (12, 2), (13, 1), (13, 5), (14, 1), (14, 2)])
+                                        (9, 1), (12, 2), (13, 1), (13, 5), (14, 1), (14, 2), (15, 1)])
 @pytest.mark.parametrize("M", [1, 37, 64, 200])
 @pytest.mark.parametrize("mode", ["rms", "ln_gelu", "rms_glu"])
 def test_gemm_norm_fold_consumer(tile, split, M, mode):
@@ -679,7 +679,7 @@ def test_gemm_norm_fold_consumer(tile, split, M, mode):
 
 
 @pytest.mark.parametrize("tile,split", [(0, 0), (3, 1), (3, 8), (2, 4), (11, 2), (10, 1), (1, 2), (8, 1), (12, 3),
-                                        (13, 1), (13, 3), (14, 1)])
+                                        (13, 1), (13, 3), (14, 1), (15, 2)])
 @pytest.mark.parametrize("M,N", [(1, 4096), (64, 4096), (64, 1600), (130, 1000), (512, 4096)])
 def test_gemm_norm_fold_producer(tile, split, M, N):
     """Norm-fold producer epilogue: h += x @ w^T + bias in place and the new rows' (sum, sum^2) added into
@@ -749,7 +749,7 @@ def test_gemm_streaming_kernels_up_to_64_rows(variant, nt, split, M):
           R.linear(x.float(), w.float(), None, glu=True), 2e-2)
 
 
-@pytest.mark.parametrize("tile,depth", [(11, 3), (11, 4), (10, 3), (13, 4), (8, 3), (12, 3), (9, 3), (14, 4)])
+@pytest.mark.parametrize("tile,depth", [(11, 3), (11, 4), (10, 3), (13, 4), (8, 3), (12, 3), (9, 3), (14, 4), (15, 3)])
 @pytest.mark.parametrize("split", [1, 3])
 @pytest.mark.parametrize("M,N,K", [(64, 1280, 2048), (37, 4096, 1024), (300, 544, 3072), (512, 2752, 4096)])
 def test_gemm_w8a8_mid_tiles(tile, depth, split, M, N, K):
