@@ -1206,7 +1206,7 @@ int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq
   if (glu && (N % 32)) throw std::runtime_error("gemm_f8f8: glu needs N % 32 == 0");
   if (!y && !partial_out) throw std::runtime_error("gemm_f8f8: output required");
   int bm = tile == 1 ? 128 : 64, bn = tile == 3 ? 64 : 128, thr = 256;
-  const bool mid = tile >= 8 && tile <= 15;
+  const bool mid = tile >= 7 && tile <= 15;
   if (mid) {
     if (K % 128) throw std::runtime_error("gemm_f8f8: gemm_mid tiles need K % 128 == 0");
     gemm_mid_dims(tile, &bm, &bn, &thr);
@@ -1275,7 +1275,7 @@ int gemm_f8f8_partial_slabs(int M, int N, int K, bool glu, int act, int tile, in
   if (tile == 0)
     tile = ((M + 127) / 128) * ((N + 127) / 128) >= 240 ? 1 : (((M + 63) / 64) * ((N + 127) / 128) >= 240 ? 2 : 3);
   int bm = tile == 1 ? 128 : 64, bn = tile == 3 ? 64 : 128, thr;
-  if (tile >= 8 && tile <= 15) gemm_mid_dims(tile, &bm, &bn, &thr);
+  if (tile >= 7 && tile <= 15) gemm_mid_dims(tile, &bm, &bn, &thr);
   const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   const int nk = (K + TBK8 - 1) / TBK8;
   if (split <= 0) {
@@ -1638,7 +1638,7 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   float* part = s > 1 ? (float*)workspace : nullptr;
   const int act_k = s > 1 && !cnt ? 0 : act, glu_k = s > 1 && !cnt ? 0 : g;
   dim3 grid(nt, s);
-  if (tsel >= 8 && tsel <= 15) {
+  if (tsel >= 7 && tsel <= 15) {  // gemm_mid tiles (7, 8-15)
     launch_gemm_mid(tsel, ns, wnt_ok(tsel_raw, M, tsel), X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, part, M, N, K,
                     act_k, glu_k, s, st, false, cnt, qe);
     if (cnt) return 0;

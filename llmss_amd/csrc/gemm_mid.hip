@@ -230,7 +230,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
 // tsel 8: 128x128 (2x2 waves), 9: 256x128 (4x2), 10: 64x256 (1x4), 11: 64x128 (1x4), 12: 128x256 (2x4),
 // 13: 64x192 (2x2; a 12288-column QKV is 64 tiles, 4096 columns 22: one workgroup per CU without a K split),
 // 14: 64x32 (4x1; narrow projections without a K split: GPT-2-XL's 6400-column MLP up is 200 workgroups),
-// 15: 64x96 (4x1; Llama-2-7B's 22016-column gate/up is 230 workgroups: one wave of the chip, no K split)
+// 15: 64x96 (4x1; Llama-2-7B's 22016-column gate/up is 230 workgroups: one wave of the chip, no K split),
+// 7: 64x48 (2x1 waves: 48 rows do not split over 4 waves in 8-row staging pieces; a 12288-column QKV is
+//    exactly 256 workgroups without a K split)
 static bool mid_layout(int tsel, int* bm, int* bn, int* wm, int* wn) {
   switch (tsel) {
     case 8: *bm = 128; *bn = 128; *wm = 2; *wn = 2; return true;
@@ -241,6 +243,7 @@ static bool mid_layout(int tsel, int* bm, int* bn, int* wm, int* wn) {
     case 13: *bm = 64; *bn = 192; *wm = 2; *wn = 2; return true;
     case 14: *bm = 64; *bn = 32; *wm = 4; *wn = 1; return true;
     case 15: *bm = 64; *bn = 96; *wm = 4; *wn = 1; return true;
+    case 7: *bm = 64; *bn = 48; *wm = 2; *wn = 1; return true;
     default: return false;
   }
 }
@@ -313,6 +316,7 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
     case 13: if (ns >= 5) MID(64, 192, 2, 2, 5); else if (ns == 4) MID(64, 192, 2, 2, 4);
              else if (ns == 3) MID(64, 192, 2, 2, 3); else MID(64, 192, 2, 2, 2); break;
     case 14: MID_NS(64, 32, 4, 1); break;
+    case 7: MID_NS(64, 48, 2, 1); break;
     case 15: if (ns >= 5) MID(64, 96, 4, 1, 5); else if (ns == 4) MID(64, 96, 4, 1, 4);
              else if (ns == 3) MID(64, 96, 4, 1, 3); else MID(64, 96, 4, 1, 2); break;
   }

@@ -69,7 +69,7 @@ def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, 
             out += [(W8A8_FLAG | (t << 8) | (d << 12), s) for t in tiles for d in (2, 3, 4) for s in splits
                     if not (t == 1 and d > 3)]
             if K % 128 == 0:  # gemm_mid tiles with the fp8 MFMA (buffer-descriptor staging, csrc/gemm_mid.hip)
-                mt = [11, 10, 13, 15] + ([8, 12] if M > 64 else []) + ([9] if M >= 256 else [])
+                mt = [11, 10, 13, 15, 7] + ([8, 12] if M > 64 else []) + ([9] if M >= 256 else [])
                 out += [(W8A8_FLAG | (t << 8) | (d << 12), s) for t in mt for d in (3, 4)
                         for s in (1, 2, 3, 4, 5, 6, 8)]
             if M >= 256 and K % 128 == 0:
@@ -91,7 +91,7 @@ def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, 
         out += [((t | d) << 8, s) for t, d in ((5, 16), (6, 16), (6, 32)) for s in (2, 4, 8, 12, 16)]
     # gemm_mid (buffer-descriptor staging, csrc/gemm_mid.hip): 8 = 128x128, 9 = 256x128, 10 = 64x256,
     # 11 = 64x128, 12 = 128x256; depth code 16 / 32 = 3 / 4 stages (clamped to the LDS)
-    mids = [(10, 16), (11, 16), (11, 32), (13, 16), (13, 32), (14, 32), (14, 48), (15, 16), (15, 32)]
+    mids = [(10, 16), (11, 16), (11, 32), (13, 16), (13, 32), (14, 32), (14, 48), (15, 16), (15, 32), (7, 32), (7, 48)]
     if M > 64:
         mids += [(8, 16), (8, 32), (12, 16)]
     if M >= 256:
@@ -103,7 +103,7 @@ def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, 
     # split-K combined inside the launch (hint bit 256, csrc/common.h splitk_combine): finished bf16
     # output with no reduce launch - for SwiGLU / activation GEMMs and row-parallel outputs that an
     # all-reduce needs whole; odd splits too (grid just under a multiple of the CU count)
-    comb = [(3, 16), (2, 16), (11, 16), (10, 16), (13, 16), (14, 32), (15, 16)]
+    comb = [(3, 16), (2, 16), (11, 16), (10, 16), (13, 16), (14, 32), (15, 16), (7, 32)]
     if M > 64:
         comb += [(1, 0), (8, 16), (12, 16)]
     if M >= 256:
@@ -208,7 +208,7 @@ def model_shapes(model) -> Dict[str, GemmShape]:
 def qkv_epi_candidates(M: int, N: int, K: int, D: int, neox_rope: bool) -> List[Tuple[int, int]]:
     """(nt_hint, split) plans that can run the QKV RoPE + KV-write epilogue: tiled / gemm_mid tiles, unsplit
     or combined in-launch (a split plan runs as a combine); neox RoPE needs head-aligned tiles (BN % D)."""
-    tiles = [(3, 64, (16, 32)), (2, 128, (16, 32)), (11, 128, (16, 32)), (10, 256, (16,)), (13, 192, (16, 32)), (14, 32, (32, 48)), (15, 96, (16, 32))]
+    tiles = [(3, 64, (16, 32)), (2, 128, (16, 32)), (11, 128, (16, 32)), (10, 256, (16,)), (13, 192, (16, 32)), (14, 32, (32, 48)), (15, 96, (16, 32)), (7, 48, (32, 48))]
     if M > 64:
         tiles += [(1, 128, (0, 16)), (8, 128, (16,)), (12, 256, (16,))]
     if M >= 256:
@@ -310,7 +310,7 @@ def _reinstall_qkv(lib, model, results):
 def fold_candidates(M: int, N: int, K: int, glu: bool) -> List[Tuple[int, int]]:
     """(nt_hint, split) plans for the norm-fold epilogues (LDS-staged, finished sums): tiled / gemm_mid tiles,
     unsplit or split-K combined in-launch."""
-    tiles = [(3, (16, 32)), (2, (16, 32)), (11, (16, 32)), (10, (16,)), (13, (16, 32)), (14, (32,)), (15, (16,))]
+    tiles = [(3, (16, 32)), (2, (16, 32)), (11, (16, 32)), (10, (16,)), (13, (16, 32)), (14, (32,)), (15, (16,)), (7, (32,))]
     if M > 64:
         tiles += [(1, (0, 16)), (8, (16,)), (12, (16,))]
     if M >= 256:

@@ -10,6 +10,7 @@ from llmss_amd.ops import reference as R
 
 pytestmark = pytest.mark.gpu
 dev = "cuda"
+ODD_NT_TILES = (7,)  # gemm_mid 64x48: three 16-column tiles per wave (no SwiGLU epilogue)
 
 
 def rnd(*s, scale=1.0, dtype=torch.bfloat16):
@@ -210,8 +211,8 @@ def test_gemm(M, N, K):
 
 
 # 128x128, 64x128, 64x64, 256x256, 256x128 / 256x64 (8 waves); gemm_mid (buffer-descriptor staging):
-# 8 = 128x128, 9 = 256x128, 10 = 64x256, 11 = 64x128, 12 = 128x256, 13 = 64x192, 14 = 64x32, 15 = 64x96
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 15])
+# 8 = 128x128, 9 = 256x128, 10 = 64x256, 11 = 64x128, 12 = 128x256, 13 = 64x192, 14 = 64x32, 15 = 64x96, 7 = 64x48
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("stages", [2, 3, 4, 6])
 @pytest.mark.parametrize("split", [1, 3, 8])
 @pytest.mark.parametrize("M,N,K", [(64, 1536, 4096), (200, 4800, 1600), (37, 256, 64 * 5 + 16), (700, 1312, 192)])
@@ -229,11 +230,16 @@ def test_gemm_tiled_variants(tile, stages, split, M, N, K):
     y = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=x.device)
     close(H.linear(x, w, b, act="gelu_tanh", nt_hint=hint, split_hint=split, out=y), ref, 2e-2)
     y = torch.full((M, N // 2), float("nan"), dtype=torch.bfloat16, device=x.device)
+    if tile in ODD_NT_TILES and split == 1:  # an in-kernel SwiGLU pairs 16-column tiles in a wave: refused
+        with pytest.raises(RuntimeError):
+            H.linear(x, w, None, glu=True, nt_hint=hint, split_hint=split, out=y)
+        return
+    # (split plans apply SwiGLU in the reduce launch, so every tile takes them)
     close(H.linear(x, w, None, glu=True, nt_hint=hint, split_hint=split, out=y),
           R.linear(x.float(), w.float(), None, glu=True), 2e-2)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 5, 6, 8, 9, 10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("tile", [1, 2, 3, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("split", [2, 3, 8])
 @pytest.mark.parametrize("M,N,K", [(64, 1536, 4096), (200, 4800, 1600), (37, 256, 64 * 5 + 16), (512, 2752, 4096)])
 def test_gemm_splitk_combine_in_launch(tile, split, M, N, K):
@@ -248,6 +254,8 @@ def test_gemm_splitk_combine_in_launch(tile, split, M, N, K):
     hint, comb = (tile | d) << 8, (tile | d | 256) << 8
     H._GEMM_WS.get(64 << 20, x.device).fill_(float("nan"))
     for act, glu, bias in (("gelu_tanh", False, b), ("none", True, None), ("none", False, b)):
+        if glu and tile in ODD_NT_TILES:
+            continue
         nout = N // 2 if glu else N
         ref = H.linear(x, w, bias, act=act, glu=glu, nt_hint=hint, split_hint=split)
         for _ in range(3):
@@ -650,7 +658,7 @@ def _row_stats(h):
 
 
 @pytest.mark.parametrize("tile,split", [(0, 0), (3, 1), (3, 4), (2, 2), (11, 1), (11, 3), (10, 2), (1, 1), (8, 2),
-                                        (9, 1), (12, 2), (13, 1), (13, 5), (14, 1), (14, 2), (15, 1)])
+                                        (9, 1), (12, 2), (13, 1), (13, 5), (14, 1), (14, 2), (15, 1), (7, 1), (7, 3)])
 @pytest.mark.parametrize("M", [1, 37, 64, 200])
 @pytest.mark.parametrize("mode", ["rms", "ln_gelu", "rms_glu"])
 def test_gemm_norm_fold_consumer(tile, split, M, mode):
@@ -664,6 +672,8 @@ def test_gemm_norm_fold_consumer(tile, split, M, mode):
     b = rnd(N, scale=0.1) if mode != "rms" else None
     ln = mode.startswith("ln")
     glu = mode.endswith("glu")
+    if glu and tile in ODD_NT_TILES:
+        pytest.skip("SwiGLU needs an even number of 16-column tiles per wave")
     act = "gelu_tanh" if mode == "ln_gelu" else "none"
     c1 = w.float().sum(1).contiguous() if ln else None
     rst = _row_stats(h)
@@ -679,7 +689,7 @@ def test_gemm_norm_fold_consumer(tile, split, M, mode):
 
 
 @pytest.mark.parametrize("tile,split", [(0, 0), (3, 1), (3, 8), (2, 4), (11, 2), (10, 1), (1, 2), (8, 1), (12, 3),
-                                        (13, 1), (13, 3), (14, 1), (15, 2)])
+                                        (13, 1), (13, 3), (14, 1), (15, 2), (7, 1)])
 @pytest.mark.parametrize("M,N", [(1, 4096), (64, 4096), (64, 1600), (130, 1000), (512, 4096)])
 def test_gemm_norm_fold_producer(tile, split, M, N):
     """Norm-fold producer epilogue: h += x @ w^T + bias in place and the new rows' (sum, sum^2) added into
@@ -749,7 +759,7 @@ def test_gemm_streaming_kernels_up_to_64_rows(variant, nt, split, M):
           R.linear(x.float(), w.float(), None, glu=True), 2e-2)
 
 
-@pytest.mark.parametrize("tile,depth", [(11, 3), (11, 4), (10, 3), (13, 4), (8, 3), (12, 3), (9, 3), (14, 4), (15, 3)])
+@pytest.mark.parametrize("tile,depth", [(11, 3), (11, 4), (10, 3), (13, 4), (8, 3), (12, 3), (9, 3), (14, 4), (15, 3), (7, 4)])
 @pytest.mark.parametrize("split", [1, 3])
 @pytest.mark.parametrize("M,N,K", [(64, 1280, 2048), (37, 4096, 1024), (300, 544, 3072), (512, 2752, 4096)])
 def test_gemm_w8a8_mid_tiles(tile, depth, split, M, N, K):
@@ -762,8 +772,9 @@ def test_gemm_w8a8_mid_tiles(tile, depth, split, M, N, K):
     xd = R.dequant_fp8(xq, xs)
     y = H.linear_w8a8(x, q, s, b, act="gelu_tanh", tile=tile, depth=depth, split=split)
     close(y, R.linear(xd, q, b.float(), act="gelu_tanh", w_scale=s), 2e-2)
-    yg = H.linear_w8a8(x, q, s, None, glu=True, tile=tile, depth=depth, split=split)
-    close(yg, R.linear(xd, q, None, glu=True, w_scale=s), 2e-2)
+    if tile not in ODD_NT_TILES:
+        yg = H.linear_w8a8(x, q, s, None, glu=True, tile=tile, depth=depth, split=split)
+        close(yg, R.linear(xd, q, None, glu=True, w_scale=s), 2e-2)
     p = H.linear_w8a8(x, q, s, None, tile=tile, depth=depth, split=split, partial_ok=True)
     if isinstance(p, H.PartialSum):
         res = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
