@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import math
 import os
+import threading
 import weakref
 from typing import Optional
 
@@ -247,10 +248,10 @@ class _Slotted:
         self._items = [cls() for _ in range(4)]
 
     def __getattr__(self, name):
-        return getattr(self._items[_SLOT[0]], name)
+        return getattr(self._items[getattr(_SLOT, "k", 0)], name)
 
 
-_SLOT = [0]
+_SLOT = threading.local()  # per host thread, like the native slot (csrc/gemm.hip gemm_set_slot)
 
 
 class workspace_slot:
@@ -262,13 +263,13 @@ class workspace_slot:
         self.k = int(k) & 3
 
     def __enter__(self):
-        self.prev = _SLOT[0]
-        _SLOT[0] = self.k
+        self.prev = getattr(_SLOT, "k", 0)
+        _SLOT.k = self.k
         lib().gemm_set_slot(self.k)
         return self
 
     def __exit__(self, *exc):
-        _SLOT[0] = self.prev
+        _SLOT.k = self.prev
         lib().gemm_set_slot(self.prev)
         return False
 
