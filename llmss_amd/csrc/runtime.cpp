@@ -285,6 +285,15 @@ class Scheduler {
   int num_free_blocks() const { return alloc_.num_free(); }
   int max_blocks_per_seq() const { return max_blocks_per_seq_; }
   bool has_work() const { return !waiting_.empty() || !running_.empty(); }
+  // Blocks for `n_tokens` cached tokens of a running sequence ahead of its schedule() (the engine's pipelined
+  // decode launches the next step before the scheduler runs: a sequence entering a new KV block needs that
+  // block now). No preemption; returns the block holding token n_tokens - 1, or -1 when the pool is empty.
+  // schedule() later finds the block already there.
+  int reserve(int64_t id, int n_tokens) {
+    auto& s = get(id);
+    if (s.status != 1 || n_tokens <= 0 || blocks_for(n_tokens) > max_blocks_per_seq_ || !grow(s, n_tokens)) return -1;
+    return s.blocks[(n_tokens - 1) / bs_];
+  }
   int num_tokens(int64_t id) { return get(id).num_tokens; }
   int num_computed(int64_t id) { return get(id).num_computed; }
   std::vector<int> blocks(int64_t id) { return get(id).blocks; }
@@ -717,6 +726,7 @@ void register_runtime(py::module_& m) {
       .def("max_blocks_per_seq", &Scheduler::max_blocks_per_seq)
       .def("has_work", &Scheduler::has_work)
       .def("num_tokens", &Scheduler::num_tokens)
+      .def("reserve", &Scheduler::reserve)
       .def("blocks", &Scheduler::blocks)
       .def("contains", &Scheduler::contains);
 

@@ -620,13 +620,28 @@ class LLMEngine:
         if not alive.any():
             return
         nxt_pos = cur["pos"] + 1
-        if (nxt_pos[alive] % self.block_size == 0).any():  # a sequence enters a new KV block
-            return
+        slots = np.where(alive, cur["slots"] + 1, -1)
+        bt = cur["bt"]
+        cross = np.flatnonzero(alive & (nxt_pos % self.block_size == 0))
+        if cross.size:
+            # sequences entering a new KV block get it now (Scheduler.reserve; the next schedule() finds it
+            # allocated), so the pipeline does not drain every block_size steps; an empty pool leaves the step
+            # to the scheduler, which may preempt
+            bt = bt.copy()
+            bs = self.block_size
+            for i in cross:
+                blk = self.sched.reserve(int(cur["ids"][i]), int(nxt_pos[i]) + 1)
+                if blk < 0:
+                    return
+                bt[i, int(nxt_pos[i]) // bs] = blk
+                slots[i] = blk * bs
+            self.stats["spec_block_reserves"] = self.stats.get("spec_block_reserves", 0) + int(cross.size)
         dead = ~alive
-        rec = {k: cur[k] for k in ("ids", "reqs", "n", "temp", "topk", "topp", "seed", "maxnew", "bt", "dist")}
+        rec = {k: cur[k] for k in ("ids", "reqs", "n", "temp", "topk", "topp", "seed", "maxnew", "dist")}
+        rec["bt"] = bt
         rec["pos"] = nxt_pos
         rec["ctx"] = np.where(alive, cur["ctx"] + 1, 0).astype(np.int32)
-        rec["slots"] = np.where(alive, cur["slots"] + 1, -1)
+        rec["slots"] = slots
         rec["nout"] = cur["nout"] + 1
         rec["keep"] = alive
         if dead.any():

@@ -446,3 +446,22 @@ def test_norm_fold_decode_matches_reference(name):
     ref = m_cpu(StepInput(**d_in), kv_c)
     out = m_gpu(StepInput(**{k: (v.cuda() if torch.is_tensor(v) else v) for k, v in d_in.items()}), kv_g)
     _assert_logits_close(out[:, :V].float().cpu(), ref[:, :V])
+
+
+def test_pipelined_decode_across_kv_block_boundaries():
+    """The pipelined decode launches step t+1 before collecting step t, also when a sequence enters a new KV
+    block (the block is reserved ahead of the scheduler: Scheduler.reserve). Greedy tokens equal the
+    un-pipelined engine's, with 4-token pages so nearly every fourth step crosses a boundary."""
+    cfg = get_preset("tiny-llama", head_dim=64, hidden_size=256, num_heads=4, num_kv_heads=2, rotary_dim=64)
+    w = _to_gpu(random_weights(cfg, device="cpu", dtype=torch.float32, seed=3, std=0.05))
+    prompts = [[(5 * i + j) % cfg.vocab_size for j in range(3 + 2 * i)] for i in range(6)]
+    sp = SamplingParams(max_new_tokens=23, is_greedy=True, ignore_eos=True)
+    outs = []
+    for pipelined in (True, False):
+        eng = LLMEngine(DecoderLM(cfg, w), max_num_seqs=8, block_size=4, num_blocks=96, max_model_len=64,
+                        autotune=False)
+        eng.async_decode = pipelined
+        outs.append(eng.generate(prompts, sp))
+        if pipelined:
+            assert eng.stats.get("spec_block_reserves", 0) > 0
+    assert outs[0] == outs[1]

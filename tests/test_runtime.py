@@ -198,3 +198,24 @@ def test_scheduler_rejects_sequence_larger_than_pool(native):
         s.add(1, 16, 4)  # 20 tokens need 5 blocks; the pool has 4
     s.add(2, 12, 4)
     assert _drive(s)[0] > 0
+
+
+def test_scheduler_reserve_ahead_of_schedule(native):
+    """Scheduler.reserve: the pipelined decode takes the next KV block of a sequence before schedule() runs; the
+    scheduler's next decode step uses that same block (no second allocation), an empty pool refuses (-1), and the
+    reserved block is returned with the sequence."""
+    s = native.Scheduler(num_blocks=3, block_size=4, max_num_seqs=2, max_batched_tokens=16, max_model_len=16)
+    s.add(1, 4, 8)  # a full first block
+    b = s.schedule()
+    assert b.kind == 1 and s.num_free_blocks() == 2
+    s.on_token(1, False)
+    blk = s.reserve(1, 5)  # token 4 opens block 1
+    assert blk >= 0 and s.num_free_blocks() == 1 and s.blocks(1)[1] == blk
+    assert s.reserve(1, 5) == blk and s.num_free_blocks() == 1  # idempotent
+    b = s.schedule()
+    assert b.kind == 2 and b.slots.tolist() == [blk * 4] and s.num_free_blocks() == 1
+    assert s.reserve(1, 9) >= 0 and s.num_free_blocks() == 0
+    assert s.reserve(1, 13) == -1  # pool empty: no preemption here
+    assert s.reserve(1, 17) == -1  # past max_model_len
+    s.finish(1)
+    assert s.num_free_blocks() == 3
