@@ -604,10 +604,17 @@ class LLMEngine:
                      step_seeds(rec["seed"], rec["nout"]), rec["ctx"], rec["topk"], rec["bt"], rec["temp"],
                      rec["topp"])
             key = (b, bool(rec["dist"]))
+            if self._host_prof:
+                # was the GPU already idle (every earlier step done) when this step was launched?
+                idle = bool(self._pending) and self._pending[-1]["ev"].query()
+                self.stats["host_late_launches"] = self.stats.get("host_late_launches", 0) + int(idle)
+                t_r = time.perf_counter()
             if self.use_graphs and key in self.graphs:
                 self.graphs[key].replay()
             else:
                 self._decode_forward(b, buf, dist=key[1])
+            if self._host_prof:
+                self.stats["host_replay_s"] = self.stats.get("host_replay_s", 0.0) + time.perf_counter() - t_r
             buf.h_out[k][:n].copy_(buf.out[:n], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
