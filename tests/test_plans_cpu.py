@@ -1,0 +1,52 @@
+"""Host-side plan logic (no GPU): autotuner candidate lists for the decode GEMM tiles and the workspace slots
+that keep concurrently running kernel chains apart (ops/autotune.py, ops/hip.py)."""
+import pytest
+
+from llmss_amd.ops import autotune as A
+
+
+def _tiles(cands):
+    return {(nt >> 8) & 15 for nt, _ in cands if nt >> 8}
+
+
+@pytest.mark.parametrize("M,N,K,glu", [(64, 12288, 4096, False), (64, 22016, 4096, True), (64, 4096, 11008, False),
+                                       (512, 1536, 4096, False), (64, 6400, 1600, False)])
+def test_candidates_cover_the_round3_tiles(M, N, K, glu):
+    c = A.candidates(M, N, K, glu, False)
+    assert len(set(c)) == len(c), "duplicate candidates"
+    # the gemm_mid decode tiles: 64x192 (13), 64x32 (14), 64x96 (15), 64x48 (7), and the odd / large splits
+    assert {7, 13, 14, 15} <= _tiles(c)
+    nk = -(-K // 64)
+    for nt, s in c:
+        assert s >= 1 and (s == 1 or nk // s >= 1)
+    if nk // 11 >= 2:
+        assert any(s == 11 for _, s in c)
+
+
+def test_fold_and_qkv_epilogue_candidates_are_combined_or_unsplit():
+    for nt, s in A.fold_candidates(64, 4096, 4096, False) + A.qkv_epi_candidates(64, 12288, 4096, 128, False):
+        assert s == 1 or (nt >> 8) & 256, (hex(nt), s)  # a split plan must combine in-launch
+    # neox RoPE needs head-aligned tiles: no 64x48 / 64x96 / 64x192 plans for D = 128
+    neox = _tiles(A.qkv_epi_candidates(64, 12288, 4096, 128, True))
+    assert not ({7, 13, 14, 15} & neox)
+
+
+def test_w8a8_candidates_include_the_fp8_gemm_mid_tiles():
+    from llmss_amd.ops.hip import W8A8_FLAG
+
+    c = [nt for nt, _ in A.candidates(64, 10240, 8192, False, True) if nt & W8A8_FLAG]
+    tiles = {(nt >> 8) & 15 for nt in c}
+    assert {7, 10, 11, 13, 15} <= tiles
+    assert not [nt for nt, _ in A.candidates(64, 10240, 8200, False, True) if nt & W8A8_FLAG and (nt >> 8) & 15 >= 7]
+
+
+def test_workspace_slots_are_disjoint():
+    from llmss_amd.ops import hip as H
+
+    a0 = H._GEMM_WS._items[0]
+    with H.workspace_slot(1):
+        assert H._GEMM_WS._items[H._SLOT.k] is not a0
+        with H.workspace_slot(2):
+            assert H._SLOT.k == 2
+        assert H._SLOT.k == 1
+    assert getattr(H._SLOT, "k", 0) == 0
