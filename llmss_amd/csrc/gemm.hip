@@ -768,7 +768,9 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict
   int aoff[8][2], boff[4][2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const int c = F8 ? 2 * g + s : 4 * s + g;  // bf16: k-half s; fp8: the lane's two 16-B chunks
+    // bf16: k-half s; fp8: the lane's two 16-B chunks g, g + 4 (the same k permutation for A and B, the
+    // conflict-free bf16 read pattern; chunks 2g, 2g + 1 hit the same banks)
+    const int c = 4 * s + g;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int r = m * 16 + li;
@@ -1077,21 +1079,23 @@ __device__ __forceinline__ void f8_stage(const unsigned char* __restrict__ A, in
 template <int MTW, int NTW, bool MASK>
 __device__ __forceinline__ void f8_compute(const char* sA, const char* sB, f32x4 (&acc)[MTW][NTW], int wr, int wc,
                                            int li, int g, int k0, int K) {
-  const bool v0 = !MASK || (k0 + 32 * g < K), v1 = !MASK || (k0 + 32 * g + 16 < K);
+  // the lane's k-bytes: chunks g and g + 4 of the 128-byte step (one k permutation for A and B; the chunk
+  // pattern of the bf16 reads, free of bank conflicts on the swizzled image)
+  const bool v0 = !MASK || (k0 + 16 * g < K), v1 = !MASK || (k0 + 64 + 16 * g < K);
   i32x8 a[MTW], b[NTW];
 #pragma unroll
   for (int t = 0; t < MTW; ++t) {
     const int r = wr * (MTW * 16) + t * 16 + li;
-    const u32x4 lo = *reinterpret_cast<const u32x4*>(sA + r * 128 + (((2 * g) ^ (r & 7)) << 4));
-    const u32x4 hi = *reinterpret_cast<const u32x4*>(sA + r * 128 + (((2 * g + 1) ^ (r & 7)) << 4));
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(sA + r * 128 + ((g ^ (r & 7)) << 4));
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(sA + r * 128 + (((g + 4) ^ (r & 7)) << 4));
     a[t] = i32x8{(int)(v0 ? lo[0] : 0u), (int)(v0 ? lo[1] : 0u), (int)(v0 ? lo[2] : 0u), (int)(v0 ? lo[3] : 0u),
                  (int)(v1 ? hi[0] : 0u), (int)(v1 ? hi[1] : 0u), (int)(v1 ? hi[2] : 0u), (int)(v1 ? hi[3] : 0u)};
   }
 #pragma unroll
   for (int t = 0; t < NTW; ++t) {
     const int r = wc * (NTW * 16) + t * 16 + li;
-    const u32x4 lo = *reinterpret_cast<const u32x4*>(sB + r * 128 + (((2 * g) ^ (r & 7)) << 4));
-    const u32x4 hi = *reinterpret_cast<const u32x4*>(sB + r * 128 + (((2 * g + 1) ^ (r & 7)) << 4));
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(sB + r * 128 + ((g ^ (r & 7)) << 4));
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(sB + r * 128 + (((g + 4) ^ (r & 7)) << 4));
     b[t] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
   }
 #pragma unroll
