@@ -260,6 +260,26 @@ def comm_probe(tp, progress) -> dict:
     return {"backend": tp.backend, "ranks": tp.size, "all_reduce_bf16": out}
 
 
+def runtime_record(tp, eng, dp: bool) -> dict:
+    """What this rank's number depends on besides the code: data plane, RCCL library version, every NCCL_* /
+    RCCL_* / HSA_* variable in the environment, whether decode ran in HIP graphs (and which buckets), and the
+    capture-time micro-batch A/B's choice."""
+    rec = {"rank": tp.global_rank if tp.is_real else int(os.environ.get("RANK", "0")),
+           "data_plane": "none (independent replicas)" if dp else tp.backend,
+           "device": torch.cuda.get_device_name() if torch.cuda.is_available() else "cpu",
+           "use_graphs": bool(eng.use_graphs), "graph_buckets": sorted({b for b, _ in eng.graphs}),
+           "tbo_choice": {str(b): v for b, v in sorted(eng.tbo_choice.items())},
+           "env": {k: v for k, v in sorted(os.environ.items())
+                   if k.startswith(("NCCL_", "RCCL_", "HSA_", "LLMSS_", "TORCH_NCCL_", "GPU_MAX_HW_QUEUES"))}}
+    try:
+        from llmss_amd import _native
+
+        rec["rccl_version"] = _native().rccl_version()
+    except Exception as e:  # noqa: BLE001 - CPU rehearsal without the extension
+        rec["rccl_version"] = f"unavailable ({type(e).__name__})"
+    return rec
+
+
 def _world_gather(obj):
     out = [None] * torch.distributed.get_world_size()
     torch.distributed.all_gather_object(out, obj)
@@ -391,6 +411,9 @@ def run_config(args, model_name, tp, batch, progress, dp=False, client=None):
     barrier()
     el = time.perf_counter() - t0
     rank_el = [el]
+    rt = [runtime_record(tp, eng, dp)]
+    if world > 1 and args.simulate_tp <= 1:
+        rt = tp.all_gather_object(rt[0]) if not dp else _world_gather(rt[0])
     if world > 1 and args.simulate_tp <= 1:  # slowest rank's clock; node total of generated tokens
         allv = tp.all_gather_object((el, total)) if not dp else _world_gather((el, total))
         rank_el = [v[0] for v in allv]
@@ -421,6 +444,7 @@ def run_config(args, model_name, tp, batch, progress, dp=False, client=None):
         "comm_backend": tp.backend if not dp else "none (independent replicas)",
         "rank_elapsed_s": [round(v, 4) for v in rank_el],
         "setup_s": setup_s,
+        "runtime": rt,
         "p50_tpot_ms": round(float(tpot), 3),
         "p50_ttft_ms": round(float(ttft), 3),
         "p50_request_latency_ms": round(float(e2e), 3),

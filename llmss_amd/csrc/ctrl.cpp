@@ -195,10 +195,11 @@ class CtrlRing {
     } while (off < msg.size());
   }
 
-  // reader: next message; throws TimeoutError-mapped exception after timeout_s (< 0: forever)
+  // reader: next message; throws TimeoutError-mapped exception after timeout_s (< 0: forever). A message
+  // split into fragments is assembled in pend_, which survives a timeout between fragments: the next recv()
+  // resumes it instead of returning its tail as a message of its own.
   py::bytes recv(double timeout_s) {
     if (producer_) throw std::runtime_error("CtrlRing: recv() on the producer");
-    std::string out;
     for (;;) {
       uint32_t len = 0, flags = 0;
       {
@@ -206,7 +207,12 @@ class CtrlRing {
         Backoff b(timeout_s);
         unsigned polls = 0;
         while (h_->write_pos.v.load(std::memory_order_acquire) <= pos_) {
-          if (h_->closed.v.load(std::memory_order_acquire)) throw std::runtime_error("CtrlRing: producer closed");
+          // closed: records published before the close still drain (the close store follows them, so an
+          // acquire reload of write_pos after seeing it observes every one of them)
+          if (h_->closed.v.load(std::memory_order_acquire)) {
+            if (h_->write_pos.v.load(std::memory_order_acquire) > pos_) break;
+            throw std::runtime_error("CtrlRing: producer closed");
+          }
           if (!b.wait()) throw timeout_error();
           if (b.sleeping() && ++polls % 64 == 0 && !process_alive(h_->producer_pid))
             throw std::runtime_error("CtrlRing: producer process died");
@@ -215,15 +221,17 @@ class CtrlRing {
         copy_out(pos_, reinterpret_cast<char*>(hdr), 8);
         len = hdr[0];
         flags = hdr[1];
-        const size_t at = out.size();
-        out.resize(at + len);
-        copy_out(pos_ + 8, &out[at], len);
+        const size_t at = pend_.size();
+        pend_.resize(at + len);
+        copy_out(pos_ + 8, &pend_[at], len);
         pos_ += rec_bytes(len);
         h_->read_pos[reader_].v.store(pos_, std::memory_order_release);
       }
       if (!(flags & kMore)) break;
     }
-    return py::bytes(out);
+    py::bytes out(pend_);
+    pend_.clear();
+    return out;
   }
 
   // producer: orderly end (readers blocked in recv() raise instead of timing out)
@@ -299,6 +307,7 @@ class CtrlRing {
   size_t bytes_ = 0;
   uint64_t mask_ = 0;
   uint64_t pos_ = 0;  // reader position
+  std::string pend_;  // reader: fragments of a message not yet complete (kept across a recv() timeout)
 };
 
 }  // namespace

@@ -27,7 +27,9 @@
 // LDS image are shared; each (m, n) tile takes one MX-fp8 16x16x128 MFMA per k-step (the lane's 16-B chunks 2g
 // and 2g+1), and the per-token x per-channel scales xs[m] * ws[n] are applied to the accumulators before the
 // epilogue (or the split-K slabs / combine, which are linear in them).
-template <int BM, int BN, int WM, int WN, int NS, bool WNT, bool PK, bool F8 = false>
+// MODE (bench/proto/midm_probe.hip only; the library instantiates 0): 1 = loads without MFMAs, 2 = MFMAs on
+// whatever LDS holds without loads, 3 = no epilogue stores - to take a tile's time apart.
+template <int BM, int BN, int WM, int WN, int NS, bool WNT, bool PK, bool F8 = false, int MODE = 0>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                               const bf16_t* __restrict__ B, int64_t ldb,
                                                               const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
@@ -89,6 +91,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
 #define MID_STAGE(T_, SA_)                                                                                         \
   do {                                                                                                           \
     char* sA_ = (SA_);                                                                                           \
+    if (MODE == 2) break;                                                                                        \
     const int soff_ = (T_) * 128, sofb_ = (T_) * (PK ? 2048 : 128);                                             \
     if (!ktail || (T_) != nk_all - 1) {                                                                          \
       _Pragma("unroll") for (int i_ = 0; i_ < AL; ++i_)                                                           \
@@ -124,6 +127,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
   // LDS cycles were bank conflicts). A and B use the same k permutation, so the dot products are unchanged.
   const int y0 = x0, y1 = x1;
   auto compute = [&](const char* st) {
+    if constexpr (MODE == 1) return;
     if constexpr (F8) {
       typedef int __attribute__((ext_vector_type(8))) i32x8_t;
       i32x8_t a[MT], b[NT];
@@ -198,6 +202,15 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
   }
 
 #undef MID_STAGE
+  if constexpr (MODE == 3) {  // keep the accumulators live without storing them
+    float t = 0.f;
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int b = 0; b < NT; ++b) t += acc[a][b][0] + acc[a][b][3];
+    if (M < 0) part[threadIdx.x] = t;
+    return;
+  }
   if constexpr (F8) {  // per-token x per-channel scales (C layout: row 4g + i of tile mt, column li of tile nt)
     float wsv[NT];
 #pragma unroll

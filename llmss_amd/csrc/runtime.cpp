@@ -287,10 +287,13 @@ class Scheduler {
   bool has_work() const { return !waiting_.empty() || !running_.empty(); }
   // Blocks for `n_tokens` cached tokens of a running sequence ahead of its schedule() (the engine's pipelined
   // decode launches the next step before the scheduler runs: a sequence entering a new KV block needs that
-  // block now). No preemption; returns the block holding token n_tokens - 1, or -1 when the pool is empty.
+  // block now). No preemption; returns the block holding token n_tokens - 1, or -1 when the pool is empty
+  // or the sequence is gone (aborted while its step was in flight).
   // schedule() later finds the block already there.
   int reserve(int64_t id, int n_tokens) {
-    auto& s = get(id);
+    auto it = seqs_.find(id);
+    if (it == seqs_.end()) return -1;  // finished / aborted meanwhile: nothing to reserve for
+    auto& s = it->second;
     if (s.status != 1 || n_tokens <= 0 || blocks_for(n_tokens) > max_blocks_per_seq_ || !grow(s, n_tokens)) return -1;
     return s.blocks[(n_tokens - 1) / bs_];
   }

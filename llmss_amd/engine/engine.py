@@ -172,6 +172,7 @@ class LLMEngine:
         self._last_fins = None
         self._stage = 0  # pinned staging set of the next launch
         self._t_collect = 0.0  # when the last decode step was collected (non-overlapped decode_time_s)
+        self._aborted = set()  # ids aborted while a decode step holding them was in flight
         self.async_decode = os.environ.get("LLMSS_ASYNC_DECODE", "1") != "0"
         self._host_prof = os.environ.get("LLMSS_HOST_PROFILE") == "1"  # host-side time per engine phase
         self.check_tokens = check_tokens if check_tokens is not None else os.environ.get("LLMSS_CHECK_TOKENS") == "1"
@@ -223,14 +224,31 @@ class LLMEngine:
             self._tune_gqa_attention()
         if self.use_graphs and os.environ.get("LLMSS_GRAPHS", "1") == "0":
             self.use_graphs = False
+        self._capture_agreed()
+
+    def _capture_agreed(self):
+        """Capture the decode graphs, agreeing on the outcome across TP ranks: if capture fails on ANY rank
+        (e.g. a collective backend that refuses stream capture), every rank drops its graphs and decodes
+        eagerly - a rank deciding alone would replay graphs whose collectives its eager peer issues in a
+        different order, or wait in the A/B below for a rank that never comes. Then the capture-time A/B of
+        the two-micro-batch schedule (real communicator only), then a second consistency check whose
+        fingerprint holds the graph set and the A/B's choice."""
         if self.use_graphs:
-            try:
+            def capture():
+                if os.environ.get("LLMSS_FAULT_INJECT", "") == f"{self.tp.rank}:capture:raise":  # tests
+                    raise RuntimeError("injected decode graph capture failure")
                 self.capture_graphs()
-            except RuntimeError as e:  # e.g. a collective backend that refuses stream capture
-                log.warning("decode graph capture failed (%s): running decode eagerly", e)
-                torch.cuda.synchronize()
+            ok, err = self.tp.agree(capture)
+            if not ok:
+                log.warning("decode graph capture failed (%s): every rank decodes eagerly",
+                            err or "on a peer rank")
+                if self.is_gpu:
+                    torch.cuda.synchronize()
                 self.graphs.clear()
                 self.use_graphs = False
+            elif self._tbo_cands:
+                self._tbo_ab(self._graph_pool, self._graph_modes)
+        self.tp.check_consistent("LLMEngine (after graph capture)", self.fingerprint())
 
     # -------------------------------------------------------------------------- sizing
     def fingerprint(self) -> dict:
@@ -244,7 +262,8 @@ class LLMEngine:
                 "async_decode": self.async_decode, "eos": self.eos, "prefill_chunk": self.prefill_chunk,
                 "dist_sampling": self.dist_sampling, "kv_fp8": bool(self.model.kv_fp8),
                 "overlap_rows": self.model.overlap_rows, "bucket_bytes": self.model.bucket_bytes,
-                "tbo_min": self.model.tbo_min,
+                "tbo_min": self.model.tbo_min, "graph_keys": sorted(self.graphs),
+                "tbo_choice": sorted(self.tbo_choice.items()),
                 "fp8": any(L.qkv.w_scale is not None for L in self.model.w.layers[:1])}
 
     def _default_buckets(self):
@@ -365,8 +384,10 @@ class LLMEngine:
         rid = self._next_id if req_id is None else int(req_id)
         self._next_id = max(self._next_id, rid + 1)
         req = Request(rid, prompt, params, params.resolved_seed(), t_arrival=time.perf_counter())
-        self.requests[rid] = req
+        # the scheduler validates first (a sequence larger than the whole KV pool, a whole prompt over the token
+        # budget -> ValueError): a rejected request is never registered, so nothing is left behind
         self.sched.add(rid, len(prompt), max_new)
+        self.requests[rid] = req
         return rid
 
     def abort(self, rid: int):
@@ -374,6 +395,8 @@ class LLMEngine:
             self.sched.abort(rid)
             r = self.requests[rid]
             r.finished, r.finish_reason = True, "abort"
+            if self._pending:  # rows of in-flight decode steps: no speculative successor may touch it
+                self._aborted.add(rid)
 
     def has_unfinished(self) -> bool:
         return self.sched.has_work() or bool(self._pending)
@@ -382,6 +405,7 @@ class LLMEngine:
         done = [r for r in self.requests.values() if r.finished]
         for r in done:
             del self.requests[r.id]
+            self._aborted.discard(r.id)
         return done
 
     # -------------------------------------------------------------------------- step
@@ -624,6 +648,10 @@ class LLMEngine:
     def _speculate(self, cur: dict):
         """Launch the step after ``cur`` (still in flight) if it needs no scheduler decision."""
         alive = cur["keep"] & (cur["nout"] + 1 < cur["maxnew"])
+        if self._aborted:
+            # aborted while in flight: the scheduler has already released the sequence (no block to reserve,
+            # no on_tokens); the row rides along as padding and is dropped at collect time
+            alive &= ~np.isin(cur["ids"], np.fromiter(self._aborted, dtype=np.int64))
         if not alive.any():
             return
         nxt_pos = cur["pos"] + 1
@@ -739,8 +767,7 @@ class LLMEngine:
                     self._decode_forward(b, buf, dist=d)
                 self.graphs[(b, d)] = g
         torch.cuda.synchronize()
-        if self._tbo_cands:
-            self._tbo_ab(pool, modes)
+        self._graph_pool, self._graph_modes = pool, modes  # for the capture-time A/B (_capture_agreed)
         log.info("captured %d decode graphs: buckets %s, samplers %s", len(self.graphs), self.buckets,
                  ["candidates" if d else "gathered" for d in modes])
 

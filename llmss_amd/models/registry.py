@@ -51,11 +51,7 @@ class CausalLM:
 
     def __init__(self, config, weights, max_blocks: int = 4096, block_size: int = 16):
         cfg = config if isinstance(config, ModelConfig) else ModelConfig.from_hf_dict(config.to_dict())
-        pgv = getattr(weights, "process_group", None)
-        tp = getattr(weights, "tp", None)
-        if tp is None and pgv is not None and getattr(pgv, "pg", None) is not None:  # a raw torch ProcessGroup
-            tp = TPGroup(pgv.rank(), pgv.size(), group=pgv.pg)
-        tp = tp or TPGroup()
+        tp = getattr(weights, "tp", None) or TPGroup()
         w = load_hf_weights(cfg, weights.reader, tp.size, tp.rank, device=weights.device, dtype=weights.dtype)
         self.model = DecoderLM(cfg, w, tp)
         self.config = cfg
@@ -180,7 +176,7 @@ class Weights:
         self.dtype = dtype
         self.reader = CheckpointReader(self.filenames, aliases=aliases)
         self.process_group = as_group_view(process_group if process_group is not None else TPGroup())
-        self.tp = self.process_group.tp  # the native TPGroup (None for a raw torch ProcessGroup)
+        self.tp = self.process_group.tp  # the TPGroup behind whatever group the caller passed
 
     def _cast(self, t: torch.Tensor) -> torch.Tensor:
         if t.dtype not in (torch.int32, torch.int64):  # reference :66-69: integers keep their dtype

@@ -24,46 +24,31 @@ from __future__ import annotations
 from typing import List, Optional
 
 import torch
-import torch.distributed as dist
 from torch import nn
 
 from .. import ops
-from ..parallel.dist import TPGroup
+from ..parallel.dist import TPGroup, as_tp_group
 
 
 class ProcessGroupView:
-    """``size()`` / ``rank()`` view of a :class:`TPGroup` (or a torch ProcessGroup) - the interface the
-    reference layer code calls (``weights.process_group.size()``), plus the two collectives it needs."""
+    """``size()`` / ``rank()`` view of a :class:`TPGroup`, a reference ``FakeGroup`` or a torch ProcessGroup -
+    the interface the reference layer code calls (``weights.process_group.size()``), plus the two collectives
+    it needs. Every kind maps to a TPGroup (parallel/dist.py as_tp_group)."""
 
     def __init__(self, group=None):
-        self.tp = group if isinstance(group, TPGroup) else None
-        self.pg = None if isinstance(group, TPGroup) else group
+        self.tp = as_tp_group(group)
 
     def size(self) -> int:
-        if self.tp is not None:
-            return self.tp.size
-        return 1 if self.pg is None else self.pg.size()
+        return self.tp.size
 
     def rank(self) -> int:
-        if self.tp is not None:
-            return self.tp.rank
-        return 0 if self.pg is None else self.pg.rank()
+        return self.tp.rank
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
-        if self.tp is not None:
-            return self.tp.all_reduce(t)
-        if self.pg is not None and self.size() > 1:
-            dist.all_reduce(t, group=self.pg)
-        return t
+        return self.tp.all_reduce(t)
 
     def all_gather_last_dim(self, t: torch.Tensor) -> torch.Tensor:
-        if self.tp is not None:
-            return self.tp.all_gather_last_dim(t)
-        if self.pg is None or self.size() == 1:
-            return t
-        parts = [torch.empty_like(t) for _ in range(self.size())]
-        dist.all_gather(parts, t.contiguous(), group=self.pg)
-        return torch.cat(parts, -1)
+        return self.tp.all_gather_last_dim(t)
 
 
 def as_group_view(group) -> ProcessGroupView:

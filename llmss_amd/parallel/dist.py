@@ -238,6 +238,19 @@ class TPGroup:
         dist.all_reduce(t, op=rop, group=self.group)
         return int(t.item())
 
+    def agree(self, fn) -> Tuple[bool, str]:
+        """Run ``fn()`` on every rank and agree on its success: ``(True, "")`` on every rank only if it raised
+        on none. A rank where it raised (RuntimeError) reports ``(False, its error)``, the others
+        ``(False, "")``, so all ranks take the same branch afterwards - a decision taken per rank (one rank
+        eager, its peers in graphs) would leave the peers waiting in a collective the failed rank never joins."""
+        err = ""
+        try:
+            fn()
+        except RuntimeError as e:
+            err = str(e) or repr(e)
+        ok = self.all_reduce_int(0 if err else 1, "min")
+        return bool(ok), err
+
     def check_consistent(self, what: str, fingerprint: dict) -> None:
         """Raise on every rank if any rank's ``fingerprint`` differs from rank 0's (a mismatched
         model / engine config would otherwise surface as a hang in the first diverging collective)."""
@@ -393,6 +406,82 @@ def initialize_distributed(timeout_s: Optional[int] = None, backend: Optional[st
     return g, rank, world_size
 
 
-# Reference-compatible alias (dist.py:40).
+class FakeBarrier:
+    """Reference ``FakeBarrier`` (``dist.py:9-11``): the completed "work" a FakeGroup collective returns."""
+
+    def wait(self):
+        pass
+
+
+class FakeGroup:
+    """Reference ``FakeGroup(rank, size)`` (``dist.py:14-37``): the process group ``world_size == 1`` (or
+    ``DEBUG=1``) code paths get. Collectives are no-ops, ``allgather`` copies the local tensor into the single
+    output slot, ``size()`` / ``rank()`` report the constructor arguments. Anything in this package that takes
+    a process group accepts one (:func:`as_tp_group` turns it into a :class:`TPGroup`: identity collectives at
+    size 1, the fake no-communication mode above)."""
+
+    def __init__(self, rank: int, size: int):
+        self._rank = int(rank)
+        self._size = int(size)
+
+    def allreduce(self, *args, **kwargs):
+        return FakeBarrier()
+
+    def allgather(self, inputs, local_tensor, **kwargs):
+        if not (len(inputs[0]) == len(local_tensor) == 1):
+            raise ValueError(f"{len(inputs[0])} != {len(local_tensor)} != 1: FakeGroup joins single tensors")
+        for inp in inputs:
+            inp[0].data = local_tensor[0].data
+        return FakeBarrier()
+
+    def barrier(self, *args, **kwargs):
+        return FakeBarrier()
+
+    def size(self) -> int:
+        return self._size
+
+    def rank(self) -> int:
+        return self._rank
+
+    def __repr__(self):
+        return f"FakeGroup(rank={self._rank}, size={self._size})"
+
+
+# TPGroups created by initialize_torch_distributed for the torch ProcessGroup it hands out, so that code which
+# passes that ProcessGroup back (Weights(..., process_group=pg)) runs on the same native communicator
+_TP_FOR_PG = {}
+
+
+def as_tp_group(group) -> TPGroup:
+    """The :class:`TPGroup` for whatever a caller passes as a process group: a TPGroup itself, a reference
+    :class:`FakeGroup` (size 1: identity collectives; size > 1: DEBUG-style fake, no communication), a torch
+    ``ProcessGroup`` (the TPGroup initialize_torch_distributed built for it, else one over torch's collectives),
+    or None (single process)."""
+    if group is None:
+        return TPGroup()
+    if isinstance(group, TPGroup):
+        return group
+    if isinstance(group, FakeGroup):
+        return TPGroup(group.rank(), group.size(), fake=group.size() > 1)
+    tp = _TP_FOR_PG.get(id(group))
+    if tp is not None and tp[0] is group:
+        return tp[1]
+    return TPGroup(group.rank(), group.size(), group=group)
+
+
 def initialize_torch_distributed():
-    return initialize_distributed()
+    """Reference-compatible ``initialize_torch_distributed() -> (process_group, rank, world_size)``
+    (``dist.py:40-77``): a :class:`FakeGroup` at ``world_size == 1`` or ``DEBUG=1``, otherwise the default
+    (world) torch ProcessGroup - so ``torch.distributed.barrier(process_group)`` works as in the reference's
+    ``generate.py:62`` - after :func:`initialize_distributed` has set up the native data plane, which
+    ``as_tp_group(process_group)`` (and so ``Weights`` / ``MODEL_REGISTRY``) picks up again. Unlike the reference
+    the default process group exists at ``world_size == 1`` too when torch.distributed is used at all later
+    (un-grouped ``dist.broadcast`` in the reference's single-GPU generate.py raises): here callers get
+    a FakeGroup and no default group, exactly like the reference, so use the returned group."""
+    tp, rank, world_size = initialize_distributed()
+    if world_size == 1 or tp.fake:
+        return FakeGroup(rank, world_size), rank, world_size
+    pg = dist.group.WORLD
+    if tp.dp == 1:
+        _TP_FOR_PG[id(pg)] = (pg, tp)
+    return pg, rank, world_size

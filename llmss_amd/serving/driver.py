@@ -332,7 +332,16 @@ class EngineDriver:
             msg = self._bcast(msg)
             self._last_bcast = time.perf_counter()
             for rid, prompt, pd in msg["new"]:
-                eng.add_request(prompt, SamplingParams(**pd), req_id=rid)
+                try:
+                    eng.add_request(prompt, SamplingParams(**pd), req_id=rid)
+                except ValueError as e:
+                    # the validation is deterministic, so every rank rejects the same request: it fails on its
+                    # own handle and the replica keeps serving the rest
+                    log.warning("rank %d: request %d rejected: %s", self.rank, rid, e)
+                    h = self.handles.get(rid) if self.leader else None
+                    if h is not None:
+                        h.error = f"rejected: {e}"
+                        self._complete(h, "error")
             for rid in msg["abort"]:
                 eng.abort(rid)
                 self._finish_abort(rid)

@@ -1,0 +1,65 @@
+"""Decode-graph capture is agreed across TP ranks: when capture fails on ONE rank, every rank
+drops its graphs and decodes eagerly, the post-capture consistency check passes, and generation still matches
+across ranks - no rank is left waiting in a collective (the capture-time A/B's all_gather_object) that a peer
+never joins. CPU / gloo: the capture itself is stubbed (a no-op that succeeds), the failure is injected on rank 1
+with LLMSS_FAULT_INJECT="1:capture:raise"."""
+import os
+import socket
+
+import torch
+import torch.multiprocessing as mp
+
+from helpers import save_hf_model
+
+
+def _worker(rank, port, ckpt, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                      LOCAL_RANK=str(rank), LLMSS_FAULT_INJECT="1:capture:raise")
+    torch.set_num_threads(1)
+    try:
+        from llmss_amd.engine import LLMEngine, SamplingParams, build_model
+        from llmss_amd.parallel.dist import initialize_distributed
+
+        tp, r, _ = initialize_distributed(backend="gloo")
+        ok, err = tp.agree(lambda: (_ for _ in ()).throw(RuntimeError("boom")) if r == 0 else None)
+        assert (ok, err) == (False, "boom" if r == 0 else ""), (ok, err)
+        assert tp.agree(lambda: None) == (True, "")
+        m = build_model(ckpt, tp, "fp32", "cpu")
+        eng = LLMEngine(m, max_num_seqs=4, block_size=4, num_blocks=64, check_tokens=True)
+        calls = []
+        eng.capture_graphs = lambda: calls.append(1)  # the GPU capture, stubbed: succeeds wherever it runs
+        eng.use_graphs = True
+        eng._capture_agreed()
+        assert not eng.use_graphs and not eng.graphs
+        assert calls == ([1] if r == 0 else [])  # rank 1 failed before capturing
+        out = eng.generate([[1, 2, 3, 4], [5, 6, 7]], SamplingParams(max_new_tokens=5, is_greedy=True,
+                                                                      ignore_eos=True))
+        q.put((r, out))
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+def test_capture_failure_on_one_rank_is_agreed(tmp_path):
+    d = str(tmp_path / "llama")
+    save_hf_model("llama", d, vocab=101)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(i, port, d, q)) for i in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        got = dict(q.get(timeout=180) for _ in range(2))
+        for p in procs:
+            p.join(60)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    assert isinstance(got[0], list) and got[0] == got[1], got
+    assert [p.exitcode for p in procs] == [0, 0]

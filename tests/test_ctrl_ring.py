@@ -95,3 +95,46 @@ def test_ring_rejects_bad_args():
         C.CtrlRing("no_slash", True, 1 << 16, 1, 0)
     with pytest.raises(RuntimeError):
         C.CtrlRing(_name(), False, 0, 0, 0)  # nothing to attach to
+
+
+def test_ring_close_drains_pending_records():
+    """A record published right before close_producer() is still delivered; only then does recv raise."""
+    C = _native()
+    name = _name()
+    ring = C.CtrlRing(name, True, 1 << 16, 1, 0)
+    reader = C.CtrlRing(name, False, 0, 0, 0)
+    assert ring.wait_attached(5.0)
+    ring.send(b"stop-record", 1.0)
+    ring.send(b"z" * 40000, 1.0)  # fragmented (> capacity / 4)
+    ring.close_producer()
+    assert reader.recv(1.0) == b"stop-record"
+    assert reader.recv(1.0) == b"z" * 40000
+    with pytest.raises(RuntimeError, match="closed"):
+        reader.recv(1.0)
+
+
+def test_ring_timeout_between_fragments_resumes_message():
+    """A reader that times out in the middle of a fragmented message resumes it on the next recv() instead of
+    returning the remaining fragments as a message of their own."""
+    import threading
+
+    C = _native()
+    name = _name()
+    ring = C.CtrlRing(name, True, 1 << 16, 2, 0)
+    fast = C.CtrlRing(name, False, 0, 0, 0)
+    slow = C.CtrlRing(name, False, 0, 0, 1)
+    assert ring.wait_attached(5.0)
+    first = b"a" * 40000
+    big = os.urandom(60000)  # 4 fragments of ~16 KiB: only the first fits while `slow` holds `first`
+    ring.send(first, 1.0)
+    t = threading.Thread(target=ring.send, args=(big, 30.0))
+    t.start()
+    try:
+        assert fast.recv(5.0) == first
+        with pytest.raises(TimeoutError):
+            fast.recv(0.2)  # one fragment of `big` is there, the rest waits for `slow`
+        assert slow.recv(5.0) == first  # frees the ring: the producer finishes `big`
+        assert fast.recv(5.0) == big
+        assert slow.recv(5.0) == big
+    finally:
+        t.join(30)
