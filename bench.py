@@ -60,6 +60,9 @@ def main():
     ap.add_argument("--sim-comm", default="",
                     help="with --simulate-tp: model each all-reduce / all-gather as LAT_US,GBPS (latency + bytes / "
                          "algorithmic bandwidth, a spin kernel on the collective's stream) to measure comm overlap")
+    ap.add_argument("--clients", type=int, default=4,
+                    help="gRPC client processes for the served secondary config (each sends its share of the "
+                         "step's concurrent requests)")
     ap.add_argument("--secondary-serve", default="grpc", choices=["grpc", "engine"],
                     help="secondary config timed through the in-process gRPC Generate service with a separate "
                          "client process (BASELINE config #2 'served over gRPC'; the engine-direct number is "
@@ -78,11 +81,13 @@ def main():
             and args.secondary_serve == "grpc":
         from llmss_amd.models.config import get_preset
 
-        client = subprocess.Popen(
-            [sys.executable, "-m", "llmss_amd.serving.loadgen", "--batch", str(args.batch_per_gpu), "--prompt-len",
+        nc = max(1, min(args.clients, args.batch_per_gpu))
+        share = [args.batch_per_gpu // nc + (i < args.batch_per_gpu % nc) for i in range(nc)]
+        client = [subprocess.Popen(
+            [sys.executable, "-m", "llmss_amd.serving.loadgen", "--batch", str(share[i]), "--prompt-len",
              str(args.prompt_len), "--gen-len", str(args.gen_len), "--vocab", str(get_preset(args.secondary).vocab_size),
-             "--seed", str(4321 + int(os.environ.get("RANK", "0")))] + (["--greedy"] if args.greedy else []),
-            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, cwd=ROOT)
+             "--seed", str(4321 + 97 * i + int(os.environ.get("RANK", "0")))] + (["--greedy"] if args.greedy else []),
+            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, cwd=ROOT) for i in range(nc)]
 
     from llmss_amd.parallel.dist import TPGroup, initialize_distributed
 
@@ -114,10 +119,11 @@ def main():
             torch.cuda.empty_cache()
         res["secondary"] = run_config(args, args.secondary, tp, args.batch_per_gpu * world, progress, dp=True,
                                       client=client)
-    if client is not None and client.poll() is None:
-        client.stdin.write("quit\n")
-        client.stdin.flush()
-        client.wait(timeout=60)
+    for c in client or []:
+        if c.poll() is None:
+            c.stdin.write("quit\n")
+            c.stdin.flush()
+            c.wait(timeout=60)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if tp.is_real:
@@ -288,7 +294,7 @@ def _world_gather(obj):
 
 def run_served(args, eng, client, progress, world, rank_sync):
     """The same engine behind the in-process gRPC Generate service (EngineDriver thread + EngineServicer);
-    the client process sends each step's ``batch`` requests concurrently. Returns (seconds, tokens, client
+    the client processes send each step's ``batch`` requests concurrently. Returns (seconds, tokens, client
     step reports) over ``args.steps`` timed steps after ``args.warmup`` untimed ones."""
     from llmss_amd.serving.driver import EngineDriver
     from llmss_amd.serving.grpc_api import EngineServicer, serve
@@ -296,16 +302,26 @@ def run_served(args, eng, client, progress, world, rank_sync):
 
     drv = EngineDriver(eng).start()
     server = serve(EngineServicer(drv, load_tokenizer(args.secondary, eng.cfg.vocab_size)), port=0, host="127.0.0.1")
-    client.stdin.write(f"{server.bound_port}\n")
-    client.stdin.flush()
+    for c in client:
+        c.stdin.write(f"{server.bound_port}\n")
+        c.stdin.flush()
 
     def step():
-        client.stdin.write("step\n")
-        client.stdin.flush()
-        line = client.stdout.readline()
-        if not line:
-            raise RuntimeError(f"gRPC client process ended (exit code {client.poll()})")
-        return json.loads(line)
+        for c in client:  # every client process sends its share of the step's requests at once
+            c.stdin.write("step\n")
+            c.stdin.flush()
+        reps = []
+        for c in client:
+            line = c.stdout.readline()
+            if not line:
+                raise RuntimeError(f"gRPC client process ended (exit code {c.poll()})")
+            reps.append(json.loads(line))
+        lat = [v for r in reps for v in r["latency_s"]]
+        ttft = [v for r in reps for v in r["ttft_s"]]
+        tpot = [v for r in reps for v in r["tpot_s"]]
+        return {"tokens": sum(r["tokens"] for r in reps), "wall_s": max(r["wall_s"] for r in reps),
+                "p50_latency_s": float(np.median(lat)), "p50_ttft_s": float(np.median(ttft)),
+                "p50_tpot_s": float(np.median(tpot)) if tpot else None}
 
     try:
         for i in range(args.warmup):
@@ -474,9 +490,9 @@ def run_config(args, model_name, tp, batch, progress, dp=False, client=None):
                    p50_ttft_ms=round(float(np.median([r["p50_ttft_s"] for r in reps])) * 1e3, 3),
                    p50_request_latency_ms=round(float(np.median([r["p50_latency_s"] for r in reps])) * 1e3, 3),
                    rank_elapsed_s=[round(v, 4) for v in grank], engine_direct=engine_direct)
-        out["config"]["serving"] = (f"gRPC Generate (in-process server, {local_batch} concurrent requests per step "
-                                    f"from a separate client process); engine_direct = the same engine stepped "
-                                    f"directly")
+        out["config"]["serving"] = (f"gRPC Generate (in-process grpc.aio server, {local_batch} concurrent requests "
+                                    f"per step from {len(client)} client processes); engine_direct = the same "
+                                    f"engine stepped directly")
         out["served_over_engine"] = round(out["value"] / engine_direct["value"], 4)
         out["config"]["driver_stats"] = {k: (round(v, 4) if isinstance(v, float) else v)
                                          for k, v in reps[0].get("driver_stats", {}).items()}

@@ -320,10 +320,15 @@ class EngineDriver:
         steps = 0
         while True:
             if self.leader:
-                idle = not eng.has_unfinished()
+                # idle = no sequence left to schedule. A speculatively launched decode step may still be in flight
+                # (pipelined decode; its rows all finished): it is collected on the next step, and a request
+                # burst arriving meanwhile still gets the admission window, i.e. lands in one prefill step
+                idle = not eng.sched.has_work()
                 msg = self._collect(block=idle)
+                if msg["new"]:
+                    self.stats["admit_steps"] = self.stats.get("admit_steps", 0) + 1
                 quiet = not msg["new"] and not msg["abort"] and not msg["stop"] and not self._stop
-                if idle and quiet:
+                if idle and quiet and not eng.has_unfinished():
                     if not self.tp.is_real or time.perf_counter() - self._last_bcast < self.heartbeat_s:
                         continue  # nothing to do, nothing to tell the followers
                     msg["hb"] = True  # heartbeat: followers time out if the leader disappears

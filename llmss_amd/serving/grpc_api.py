@@ -8,13 +8,20 @@ file interoperates (same package, service, method and field numbers).
 
 Two servicers:
 * :class:`EngineServicer` - in-process on the TP leader, feeding :class:`EngineDriver` directly
-  (lowest latency; config "GPT-2-XL TP=1 served over gRPC").
+  (lowest latency; config "GPT-2-XL TP=1 served over gRPC"). Its handlers are coroutines served by a
+  ``grpc.aio`` server on an event-loop thread of its own: a request holds a future completed by the
+  driver's ``on_done`` callback, not a pool thread parked in ``Handle.wait`` - with one thread per
+  in-flight request, a 64-request burst took ~20 ms to dispatch and the 64 replies ~15 ms to go out
+  (Python per-call overhead under one GIL), about half of that on the event loop.
 * :class:`BrokerServicer` - a front-end that enqueues to the pub/sub broker and waits for the
   correlated reply (config "pub/sub producer/consumer under concurrent gRPC clients").
 """
 from __future__ import annotations
 
+import asyncio
+import inspect
 import json
+import threading
 import time
 from concurrent import futures
 from typing import Optional
@@ -88,7 +95,12 @@ def add_servicer(server: grpc.Server, servicer) -> None:
     server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(SERVICE, handlers),))
 
 
-def serve(servicer, port: int = 50051, host: str = "0.0.0.0", max_workers: int = 64) -> grpc.Server:
+def serve(servicer, port: int = 50051, host: str = "0.0.0.0", max_workers: int = 64):
+    """Start a gRPC server for ``servicer``: a ``grpc.aio`` server on its own event-loop thread when the
+    servicer's handlers are coroutines (:class:`EngineServicer`), else a thread-pool server (blocking
+    handlers, :class:`BrokerServicer`). Either object has ``bound_port`` and ``stop(grace).wait()``."""
+    if inspect.iscoroutinefunction(getattr(servicer, "Generate", None)):
+        return AioServer(servicer, port, host)
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers),
                          options=[("grpc.max_receive_message_length", 64 << 20)])
     add_servicer(server, servicer)
@@ -96,6 +108,57 @@ def serve(servicer, port: int = 50051, host: str = "0.0.0.0", max_workers: int =
     server.start()
     server.bound_port = bound
     return server
+
+
+class AioServer:
+    """``grpc.aio`` server running on a dedicated event-loop thread (the engine driver keeps its own thread)."""
+
+    def __init__(self, servicer, port: int, host: str):
+        self.loop = asyncio.new_event_loop()
+        self.bound_port = None
+        self._server = None
+        self._err: Optional[BaseException] = None
+        self._ready = threading.Event()
+        self._thread = threading.Thread(target=self._run, args=(servicer, port, host), daemon=True,
+                                        name="grpc-aio-server")
+        self._thread.start()
+        self._ready.wait(60)
+        if self._err is not None:
+            raise self._err
+        if self.bound_port is None:
+            raise RuntimeError("gRPC aio server did not start")
+
+    def _run(self, servicer, port, host):
+        asyncio.set_event_loop(self.loop)
+
+        async def main():
+            self._server = grpc.aio.server(options=[("grpc.max_receive_message_length", 64 << 20)])
+            add_servicer(self._server, servicer)
+            self.bound_port = self._server.add_insecure_port(f"{host}:{port}")
+            await self._server.start()
+            self._ready.set()
+            await self._server.wait_for_termination()
+
+        try:
+            self.loop.run_until_complete(main())
+        except BaseException as e:  # noqa: BLE001 - reported to the constructor
+            self._err = e
+            self._ready.set()
+
+    def stop(self, grace: Optional[float] = None):
+        fut = asyncio.run_coroutine_threadsafe(self._server.stop(grace), self.loop)
+        th = self._thread
+
+        class _Done:
+            def wait(self, timeout: Optional[float] = None) -> bool:
+                fut.result(timeout)
+                th.join(timeout)
+                return not th.is_alive()
+        return _Done()
+
+    def wait_for_termination(self, timeout: Optional[float] = None) -> bool:
+        self._thread.join(timeout)
+        return not self._thread.is_alive()
 
 
 class Stub:
@@ -112,8 +175,13 @@ class Stub:
 
 
 # ------------------------------------------------------------------------------ servicers
+def _resolve(fut, value):
+    if not fut.done():
+        fut.set_result(value)
+
+
 class EngineServicer:
-    """Direct servicer on the TP leader."""
+    """Direct servicer on the TP leader (coroutine handlers: :func:`serve` runs it on a ``grpc.aio`` server)."""
 
     def __init__(self, driver, tokenizer):
         self.driver = driver
@@ -126,38 +194,60 @@ class EngineServicer:
             return list(req.prompt_token_ids)
         return encode(self.tok, req.prompt)
 
-    def Generate(self, req, ctx):
+    async def Generate(self, req, ctx):
         try:
             params = _params(req)
         except ValueError as e:
-            ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+            await ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
         remaining = ctx.time_remaining()  # gRPC deadline -> server-side deadline on every rank
-        h = self.driver.submit(self._prompt_ids(req), params, deadline_s=remaining)
-        if not h.wait(remaining if remaining is not None else None):
+        h = self.driver.submit(self._prompt_ids(req), params, deadline_s=remaining,
+                               on_done=lambda h_: loop.call_soon_threadsafe(_resolve, fut, h_))
+        try:
+            await (asyncio.wait_for(fut, remaining) if remaining is not None else fut)
+        except asyncio.TimeoutError:
             self.driver.abort(h.rid)
-            ctx.abort(grpc.StatusCode.DEADLINE_EXCEEDED, "generation deadline exceeded")
+            await ctx.abort(grpc.StatusCode.DEADLINE_EXCEEDED, "generation deadline exceeded")
+        except asyncio.CancelledError:  # the client went away
+            self.driver.abort(h.rid)
+            raise
         if h.finish_reason == "error":
-            ctx.abort(grpc.StatusCode.UNAVAILABLE, h.error or "engine failure")
+            await ctx.abort(grpc.StatusCode.UNAVAILABLE, h.error or "engine failure")
         m = h.metrics or {}
         return GenerateResponse(prompt=req.prompt, continuation=self.tok.decode(h.output_ids), request_id=req.request_id,
                                 token_ids=h.output_ids, finish_reason=h.finish_reason,
                                 ttft_s=float(m.get("ttft_s", 0.0) or 0.0), e2e_s=float(m.get("e2e_s", 0.0) or 0.0))
 
-    def GenerateStream(self, req, ctx):
+    async def GenerateStream(self, req, ctx):
         try:
             params = _params(req)
         except ValueError as e:
-            ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
-        h = self.driver.submit(self._prompt_ids(req), params, deadline_s=ctx.time_remaining(), stream=True)
-        ctx.add_callback(lambda: (not h.done.is_set()) and self.driver.abort(h.rid))
+            await ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
+        loop = asyncio.get_running_loop()
+        q: asyncio.Queue = asyncio.Queue()
+        # tokens and the final None reach the queue in the driver's order (call_soon_threadsafe is FIFO)
+        h = self.driver.submit(self._prompt_ids(req), params, deadline_s=ctx.time_remaining(),
+                               on_token=lambda h_, t: loop.call_soon_threadsafe(q.put_nowait, t),
+                               on_done=lambda h_: loop.call_soon_threadsafe(q.put_nowait, None))
         from ..utils.tokenizer import StreamDecoder
 
         dec = StreamDecoder(self.tok)  # one short-window decode per token, not the whole prefix again
-        for t in h.iter_tokens():
-            yield Token(token_id=t, text=dec.push(t), finished=False)
+        try:
+            while True:
+                t = await q.get()
+                if t is None:
+                    break
+                yield Token(token_id=t, text=dec.push(t), finished=False)
+        except asyncio.CancelledError:
+            if not h.done.is_set():
+                self.driver.abort(h.rid)
+            raise
+        if h.finish_reason == "error":
+            await ctx.abort(grpc.StatusCode.UNAVAILABLE, h.error or "engine failure")
         yield Token(token_id=-1, text=dec.flush(), finished=True, finish_reason=h.finish_reason)
 
-    def Stats(self, req, ctx):
+    async def Stats(self, req, ctx):
         st = dict(self.driver.engine.stats)
         st["healthy"] = self.driver.error is None
         if self.driver.error is not None:

@@ -5,8 +5,9 @@ model over HTTP -> Redis -> consumer (``poc-server/producer-consumer/producer_se
 no gRPC. ``bench.py`` runs the engine behind the in-process gRPC ``Generate`` service and this process
 acts as the clients: it is started before the bench touches the GPU, learns the server port on stdin,
 then executes one *step* per ``step`` line - ``batch`` concurrent ``Generate`` calls with synthetic
-pre-tokenized prompts (``prompt_token_ids``), exactly the engine bench's step - and answers with one JSON
-line (tokens received, per-request latency / server TTFT / TPOT). ``quit`` ends it.
+pre-tokenized prompts (``prompt_token_ids``) - and answers with one JSON line (tokens received, per-request
+latency / server TTFT / TPOT). ``quit`` ends it. ``bench.py`` runs several of these processes side by side
+(``--clients``), each with its share of the step's requests, as independent clients would.
 
 usage: python -m llmss_amd.serving.loadgen --batch 64 --prompt-len 128 --gen-len 128 --vocab 50257
 """
@@ -65,7 +66,8 @@ def main(argv=None):
                 tpot.append((float(resp.e2e_s) - float(resp.ttft_s)) / (n - 1))
         print(json.dumps({"step": step, "tokens": ntok, "wall_s": time.perf_counter() - t0,
                           "p50_latency_s": float(np.median(lat)), "p50_ttft_s": float(np.median(ttft)),
-                          "p50_tpot_s": float(np.median(tpot)) if tpot else None}), flush=True)
+                          "p50_tpot_s": float(np.median(tpot)) if tpot else None,
+                          "latency_s": lat, "ttft_s": ttft, "tpot_s": tpot}), flush=True)
         step += 1
     ch.close()
     return 0

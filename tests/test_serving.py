@@ -236,3 +236,34 @@ def test_admission_window_batches_a_burst(driver):
     finally:
         drv.batch_window_s = old
     assert eng.stats["prefill_steps"] - before == 1
+
+
+def test_grpc_burst_lands_in_one_admission_step(model_dir):
+    """The engine servicer runs on a grpc.aio server (coroutine handlers, no thread per in-flight request), and a
+    burst of concurrent requests arriving while the engine is idle is admitted in ONE step (the driver's admission
+    window), bursts after bursts included (the last step of a burst may leave a speculative decode step in flight)."""
+    import concurrent.futures as cf
+
+    from llmss_amd.serving.grpc_api import AioServer
+
+    m = build_model(model_dir, None, "fp32", "cpu")
+    tok = load_tokenizer(model_dir, m.cfg.vocab_size)
+    eng = LLMEngine(m, max_num_seqs=8, block_size=4, num_blocks=256, eos_token_id=None)
+    drv = EngineDriver(eng)
+    drv.batch_window_s = 0.05  # CPU test box: generous gap between arrivals
+    drv.start()
+    server = serve(EngineServicer(drv, tok), port=0, host="127.0.0.1")
+    try:
+        assert isinstance(server, AioServer)
+        stub = Stub(grpc.insecure_channel(f"127.0.0.1:{server.bound_port}"))
+        with cf.ThreadPoolExecutor(8) as ex:
+            for burst in range(3):
+                reqs = [GenerateRequest(prompt_token_ids=[1 + i, 2, 3, 4 + burst], max_new_tokens=6, is_greedy=True,
+                                        ignore_eos=True) for i in range(8)]
+                outs = list(ex.map(lambda r: stub.Generate(r, timeout=60), reqs))
+                assert all(len(o.token_ids) == 6 for o in outs)
+        assert drv.stats["admit_steps"] == 3, drv.stats
+        assert drv.stats["admit_window_reqs"] == 24
+    finally:
+        server.stop(0).wait(10)
+        drv.stop()
