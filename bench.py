@@ -274,7 +274,7 @@ def runtime_record(tp, eng, dp: bool) -> dict:
            "data_plane": "none (independent replicas)" if dp else tp.backend,
            "device": torch.cuda.get_device_name() if torch.cuda.is_available() else "cpu",
            "use_graphs": bool(eng.use_graphs), "graph_buckets": sorted({b for b, _ in eng.graphs}),
-           "tbo_choice": {str(b): v for b, v in sorted(eng.tbo_choice.items())},
+           "decode_schedule": {str(b): v for b, v in sorted(eng.decode_schedule.items())},
            "env": {k: v for k, v in sorted(os.environ.items())
                    if k.startswith(("NCCL_", "RCCL_", "HSA_", "LLMSS_", "TORCH_NCCL_", "GPU_MAX_HW_QUEUES"))}}
     try:

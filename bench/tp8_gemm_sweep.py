@@ -18,6 +18,9 @@ from llmss_amd.ops import hip as H  # noqa: E402
 # name -> (N, K, glu, consumer sums split-K slabs itself); Llama-2-7B / TP=8: 4096 hidden, 11008 MLP
 SHAPES = {"qkv": (1536, 4096, False, True), "o": (4096, 512, False, False), "up": (2752, 4096, True, False),
           "down": (4096, 1376, False, False)}
+# TP=1 (--tp1): o / down partials are summed by the next add_norm
+SHAPES_TP1 = {"qkv": (12288, 4096, False, True), "o": (4096, 4096, False, True), "up": (22016, 4096, True, False),
+              "down": (4096, 11008, False, True)}
 
 
 def family(nt: int) -> str:
@@ -39,13 +42,15 @@ def main():
     ap.add_argument("--top", type=int, default=8)
     ap.add_argument("--shapes", default="qkv,o,up,down")
     ap.add_argument("--extra", nargs="*", default=[], help="additional HINT,SPLIT plans (hex ok)")
+    ap.add_argument("--tp1", action="store_true", help="Llama-2-7B TP=1 shapes instead of the TP=8 shard")
+    ap.add_argument("--deep", action="store_true", help="add deeper LDS rings (depth code 48) of the gemm_mid tiles")
     ap.add_argument("--warm", action="store_true", help="one weight copy (cache-resident) instead of HBM-streamed")
     a = ap.parse_args()
     dev = torch.device("cuda")
     M = a.m
     total_best = 0.0
     for name in a.shapes.split(","):
-        N, K, glu, partial = SHAPES[name]
+        N, K, glu, partial = (SHAPES_TP1 if a.tp1 else SHAPES)[name]
         ncopy = 1 if a.warm else max(2, min(64, math.ceil((600 << 20) / (N * K * 2))))
         base = (torch.randn(N, K, device=dev) * K ** -0.5).to(torch.bfloat16)
         ws = [base.clone() for _ in range(ncopy)]
@@ -53,6 +58,10 @@ def main():
         y = torch.empty(M, N // 2 if glu else N, dtype=torch.bfloat16, device=dev)
         cands = [(0, 0)] + AT.candidates(M, N, K, glu, False)
         cands += [tuple(int(v, 0) for v in e.split(",")) for e in a.extra]
+        if a.deep:
+            nk = -(-K // 64)
+            cands += [(((t | 48) << 8), sp) for t in (11, 13, 15, 10, 8) for sp in (1, 2, 3, 4, 5, 6, 8)
+                      if sp == 1 or nk // sp >= 2]
         res = []
         for nt, s in cands:
             for fin in ((True, False) if partial else (True,)):

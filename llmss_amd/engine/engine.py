@@ -204,7 +204,10 @@ class LLMEngine:
         if self.buckets[-1] < max_num_seqs:
             self.buckets.append(max_num_seqs)
         self._tbo_cands = self._tbo_candidates()
-        self.tbo_choice: Dict[int, bool] = {}  # bucket -> two-micro-batch graph chosen by the capture-time A/B
+        self._rsag_cands = self._rsag_candidates()
+        # bucket -> decode schedule the capture-time A/B kept: "one" (all-reduce per row-parallel output),
+        # "tbo" (two interleaved micro-batches) or "rsag" (row-sharded: reduce-scatter / all-gather)
+        self.decode_schedule: Dict[int, str] = {}
         self.tp.check_consistent("LLMEngine", self.fingerprint())
         self.buf = _DecodeBuffers(self.buckets[-1], self.max_blocks, self.device) if self.is_gpu else None
         if self.is_gpu:
@@ -246,8 +249,8 @@ class LLMEngine:
                     torch.cuda.synchronize()
                 self.graphs.clear()
                 self.use_graphs = False
-            elif self._tbo_cands:
-                self._tbo_ab(self._graph_pool, self._graph_modes)
+            elif self._tbo_cands or self._rsag_cands:
+                self._schedule_ab(self._graph_pool, self._graph_modes)
         self.tp.check_consistent("LLMEngine (after graph capture)", self.fingerprint())
 
     # -------------------------------------------------------------------------- sizing
@@ -263,7 +266,7 @@ class LLMEngine:
                 "dist_sampling": self.dist_sampling, "kv_fp8": bool(self.model.kv_fp8),
                 "overlap_rows": self.model.overlap_rows, "bucket_bytes": self.model.bucket_bytes,
                 "tbo_min": self.model.tbo_min, "graph_keys": sorted(self.graphs),
-                "tbo_choice": sorted(self.tbo_choice.items()),
+                "decode_schedule": sorted(self.decode_schedule.items()), "rsag_mode": self.model.rsag_mode,
                 "fp8": any(L.qkv.w_scale is not None for L in self.model.w.layers[:1])}
 
     def _default_buckets(self):
@@ -355,6 +358,17 @@ class LLMEngine:
             return []
         lo = int(os.environ.get("LLMSS_TBO_AUTO_MIN", "128"))
         return [b for b in self.buckets if b >= lo]
+
+    def _rsag_candidates(self) -> List[int]:
+        """Decode buckets whose row-sharded schedule (reduce-scatter -> add + norm on M / tp rows -> all-gather,
+        DecoderLM._hidden_states_rsag) is timed against the all-reduce one at capture: real multi-rank
+        communicator, LLMSS_TP_RSAG=auto (default), buckets divisible by the TP degree of at least
+        LLMSS_TP_RSAG_MIN (default 8 rows per rank)."""
+        m = self.model
+        if not (self.is_gpu and self.tp.is_real and not self.tp.host_staged and m.rsag_mode == "auto"):
+            return []
+        lo = int(os.environ.get("LLMSS_TP_RSAG_MIN", str(8 * self.tp.size)))
+        return [b for b in self.buckets if b >= lo and m.rsag_ok(b)]
 
     def _tbo_half(self, b: int) -> int:
         if b not in getattr(self, "_tbo_cands", ()):
@@ -771,75 +785,102 @@ class LLMEngine:
         log.info("captured %d decode graphs: buckets %s, samplers %s", len(self.graphs), self.buckets,
                  ["candidates" if d else "gathered" for d in modes])
 
-    def _tbo_ab(self, pool, modes):
-        """Capture-time A/B of the two-micro-batch decode schedule (each half's all-reduces on the comm stream
-        while the other half computes, DecoderLM._hidden_states_overlap) against the single-batch graphs, on
-        the real communicator: per candidate bucket both graphs are replayed with a realistic context length
-        (the bench's 128 + 64 average), every rank's times are gathered and the max over ranks decides, so all
-        ranks keep the same graph. The split loses on one GPU (half-batch kernels are nearly as long as full
-        ones, profiles/r1_tbo) and can win only where collectives cost real time - hence measured, not assumed."""
+    @contextlib.contextmanager
+    def _schedule(self, b: int, name: str):
+        """Decode bucket ``b`` runs schedule ``name`` inside the block (capture / warm-up of an A/B variant)."""
+        m = self.model
+        old_tbo, had = m.tbo_min, b in m.rsag
+        if name == "tbo":
+            m.tbo_min = b
+        elif name == "rsag":
+            m.rsag.add(b)
+        try:
+            yield
+        finally:
+            m.tbo_min = old_tbo
+            if name == "rsag" and not had:
+                m.rsag.discard(b)
+
+    def _schedule_ab(self, pool, modes):
+        """Capture-time A/B of the decode schedules on the real communicator: per candidate bucket the
+        all-reduce graph ("one") against the two-micro-batch one ("tbo": each half's all-reduces on the comm
+        stream while the other half computes, DecoderLM._hidden_states_overlap) and the row-sharded one ("rsag":
+        reduce-scatter, add + norm on M / tp rows, all-gather, DecoderLM._hidden_states_rsag). Each graph is
+        replayed with a realistic context length (the bench's 128 + 64 average), every rank's times are
+        gathered and the max over ranks decides, so all ranks keep the same graph; an alternative must beat
+        "one" by 3 %. Which wins depends on what collectives cost on the node - hence measured, not assumed
+        (the split loses on one GPU: half-batch kernels are nearly as long as full ones, profiles/r1_tbo)."""
         buf, m = self.buf, self.model
         ctx = int(os.environ.get("LLMSS_TBO_AUTO_CTX", "192"))
         ctx = max(1, min(ctx, self.max_model_len - 1))
         nblk = -(-ctx // self.block_size)
         if nblk > self.num_blocks:
             return
-        alt = {}
+        variants = {b: [n for n, c in (("tbo", self._tbo_cands), ("rsag", self._rsag_cands)) if b in c]
+                    for b in self.buckets}
+        variants = {b: v for b, v in variants.items() if v}
         st = torch.cuda.Stream()
         st.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(st):  # eager warm-up of the split schedule (comm stream, half-batch workspaces)
-            for b in reversed(self._tbo_cands):
-                old, m.tbo_min = m.tbo_min, b
-                try:
-                    self._decode_forward(b, buf, dist=modes[0])
-                finally:
-                    m.tbo_min = old
+        with torch.cuda.stream(st):  # eager warm-up: comm stream, half-batch workspaces, each collective's first use
+            for b in sorted(variants, reverse=True):
+                for name in variants[b]:
+                    with self._schedule(b, name):
+                        self._decode_forward(b, buf, dist=modes[0])
         torch.cuda.current_stream().wait_stream(st)
         torch.cuda.synchronize()
-        for b in reversed(self._tbo_cands):
+        alt = {}
+        for b in sorted(variants, reverse=True):
             for d in modes:
-                old, m.tbo_min = m.tbo_min, b
-                try:
-                    g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
-                        self._decode_forward(b, buf, dist=d)
-                finally:
-                    m.tbo_min = old
-                alt[(b, d)] = g
+                for name in variants[b]:
+                    with self._schedule(b, name):
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
+                            self._decode_forward(b, buf, dist=d)
+                    alt[(b, d, name)] = g
         torch.cuda.synchronize()
         # realistic rows for timing: every row attends `ctx` cached positions (garbage K/V, no cache writes)
         buf.ctx.fill_(ctx)
         buf.bt.zero_()
         buf.bt[:, :nblk] = torch.arange(nblk, dtype=torch.int32, device=buf.bt.device)
-        times = {}
-        for (b, d), g_alt in alt.items():
-            g_one = self.graphs[(b, d)]
-            for g in (g_one, g_alt):  # warm both
+
+        def timed(g):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(3):
                 g.replay()
-            torch.cuda.synchronize()
-            res = []
-            for g in (g_one, g_alt, g_one, g_alt):
-                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                s.record()
-                for _ in range(3):
+            e.record()
+            e.synchronize()
+            return s.elapsed_time(e) / 3
+
+        times = {}
+        for b in sorted(variants, reverse=True):
+            for d in modes:
+                gs = {"one": self.graphs[(b, d)], **{n: alt[(b, d, n)] for n in variants[b]}}
+                for g in gs.values():  # warm every graph
                     g.replay()
-                e.record()
-                e.synchronize()
-                res.append(s.elapsed_time(e) / 3)
-            times[(b, d)] = (min(res[0], res[2]), min(res[1], res[3]))
+                torch.cuda.synchronize()
+                res = {n: [] for n in gs}
+                for _ in range(2):  # interleaved rounds, best of each
+                    for n, g in gs.items():
+                        res[n].append(timed(g))
+                times[(b, d)] = {n: min(v) for n, v in res.items()}
         allt = self.tp.all_gather_object(times)
-        for key in times:
-            one = max(t[key][0] for t in allt)
-            two = max(t[key][1] for t in allt)
-            if two < 0.97 * one:
-                self.graphs[key] = alt[key]
-            self.tbo_choice[key[0]] = self.tbo_choice.get(key[0], False) or two < 0.97 * one
-            self.stats.setdefault("tbo_ab_ms", {})[f"{key[0]}{'c' if key[1] else 'g'}"] = [round(one, 3), round(two, 3)]
+        for (b, d), tv in times.items():
+            worst = {n: max(t[(b, d)][n] for t in allt) for n in tv}
+            best = min(worst, key=lambda n: worst[n] if n == "one" else worst[n] / 0.97)
+            if best != "one":
+                self.graphs[(b, d)] = alt[(b, d, best)]
+            if best == "rsag":  # eager steps of this bucket (none while its graph exists) take it too
+                m.rsag.add(b)
+            if self.decode_schedule.get(b, "one") == "one":
+                self.decode_schedule[b] = best
+            self.stats.setdefault("schedule_ab_ms", {})[f"{b}{'c' if d else 'g'}"] = \
+                {n: round(v, 3) for n, v in worst.items()}
         buf.ctx.zero_()
         buf.bt.zero_()
         torch.cuda.synchronize()
-        log.info("decode micro-batch overlap A/B (max over ranks, ms one/two micro-batches): %s",
-                 self.stats.get("tbo_ab_ms"))
+        log.info("decode schedule A/B (max over ranks, ms per step): %s -> %s", self.stats.get("schedule_ab_ms"),
+                 self.decode_schedule)
 
     # -------------------------------------------------------------------------- offline API
     def generate(self, prompts: Iterable[Sequence[int]], params=None) -> List[List[int]]:

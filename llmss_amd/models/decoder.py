@@ -112,6 +112,13 @@ class DecoderLM:
         # the VALU split-K decode kernel; filled by LLMEngine's capture-time timing for G >= 4 groups
         self.gqa_mfma: set = set()
         self._norm_quant = os.environ.get("LLMSS_FP8_NORM_QUANT", "1") != "0"
+        # row-sharded decode schedule (TP > 1): each row-parallel output is reduce-scattered instead of
+        # all-reduced, add + norm run on this rank's M / tp rows (the residual stream stays sharded) and the
+        # normed rows are all-gathered for the next column-parallel GEMM (_hidden_states_rsag). Decode batch
+        # sizes in `rsag` take it: LLMSS_TP_RSAG=1 every divisible decode batch, "auto" (default) the buckets
+        # the engine's capture-time A/B picks on the real communicator, 0 never
+        self.rsag_mode = os.environ.get("LLMSS_TP_RSAG", "auto")
+        self.rsag: set = set()
         self._cu_decode = {}
         self._comm_stream = None
         # norm fold (TP = 1 decode): no add_norm launch inside the layer stack - see fold_norms. Opt-in
@@ -441,9 +448,45 @@ class DecoderLM:
             ops.add_norm(delta[j], w.lnf_w, w.lnf_b, eps, rms, res[j], out=out[r0:r1])
         return out
 
+    def rsag_ok(self, M: int) -> bool:
+        """Can an M-row decode step run the row-sharded (reduce-scatter / all-gather) schedule?"""
+        return self.tp.comm_active and self.tp.size > 1 and M % self.tp.size == 0 and M >= self.tp.size
+
+    def _hidden_states_rsag(self, inp: StepInput, kv_caches) -> torch.Tensor:
+        """Decode step with the residual stream sharded by rows across the TP ranks.
+
+        Per layer: the row-parallel partial output (o, or down(up(.))) is REDUCE-SCATTERED - this rank gets the
+        sums of its M / tp rows - the residual add + norm runs on those rows only, and the normed rows are
+        ALL-GATHERED as the next column-parallel GEMM's input. The bytes on the wire equal the all-reduce's (an
+        RCCL ring all-reduce is a reduce-scatter followed by an all-gather), but the two add_norm launches of a
+        layer touch 1 / tp of the rows, and the embedding rows / residual need no replication. Numerically it
+        is the all-reduce schedule: every row's sum and norm are computed once, on the rank owning the row."""
+        cfg, w, tp = self.cfg, self.w, self.tp
+        eps, rms = cfg.norm_eps, self.rms
+        x = ops.embed(inp.input_ids, w.wte, inp.positions if w.wpe is not None else None, w.wpe)
+        m = x.shape[0] // tp.size
+        delta = x[tp.rank * m:(tp.rank + 1) * m]
+        residual = None
+        for i, L in enumerate(w.layers):
+            kc, vc = kv_caches[i]
+            y_sh, residual = ops.add_norm(delta, L.ln1_w, L.ln1_b, eps, rms, residual)
+            y = tp.all_gather_rows(y_sh)
+            a = self._attention(L, y, inp, kc, vc)
+            if cfg.parallel_block:  # GPT-J: one reduce-scatter for attention + MLP
+                delta = tp.reduce_scatter_rows(L.o(a).add_(L.down(L.up(y, self.act))))
+                continue
+            o_sh = tp.reduce_scatter_rows(L.o(a))
+            y2_sh, residual = ops.add_norm(o_sh, L.ln2_w, L.ln2_b, eps, rms, residual)
+            delta = tp.reduce_scatter_rows(L.down(L.up(tp.all_gather_rows(y2_sh), self.act)))
+        h_sh, _ = ops.add_norm(delta, w.lnf_w, w.lnf_b, eps, rms, residual)
+        return tp.all_gather_rows(h_sh)
+
     def hidden_states(self, inp: StepInput, kv_caches) -> torch.Tensor:
         if inp.kind == "decode":
-            h = self.overlap_split(inp.input_ids.shape[0])
+            B = inp.input_ids.shape[0]
+            if self.rsag_ok(B) and (self.rsag_mode == "1" or B in self.rsag):
+                return self._hidden_states_rsag(inp, kv_caches)
+            h = self.overlap_split(B)
             if h:
                 return self._hidden_states_overlap(inp, kv_caches, h)
         elif inp.kind == "prefill":

@@ -183,6 +183,58 @@ class TPGroup:
         out = out.view((self.size,) + tuple(t.shape))
         return out.movedim(0, -2).reshape(*t.shape[:-1], self.size * t.shape[-1])
 
+    def reduce_scatter_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """Sum ``t`` ([M, ...], M % size == 0) over the ranks and return this rank's block of M / size rows
+        (RCCL reduce-scatter; the row-sharded decode schedule of DecoderLM). Fake / suspended groups return
+        the local block (a modelled group spends the collective's time first)."""
+        n = self.size
+        if t.shape[0] % n:
+            raise ValueError(f"reduce_scatter_rows: {t.shape[0]} rows do not split over {n} ranks")
+        m = t.shape[0] // n
+        if self._suspend or not self.is_real:
+            if self.sim_comm is not None and t.is_cuda and not self._suspend:
+                self._sim_wait(t.numel() * t.element_size() // max(1, n))
+            return t[self.rank * m:(self.rank + 1) * m]
+        t = t.contiguous()
+        out = torch.empty((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if self._native_ok(t):
+            self.comm.reduce_scatter(t.data_ptr(), out.data_ptr(), out.numel(), self._code(t),
+                                     torch.cuda.current_stream().cuda_stream)
+        elif t.is_cuda and self.host_staged:
+            self._no_capture()
+            h = t.cpu()
+            dist.all_reduce(h, group=self.group)
+            out.copy_(h[self.rank * m:(self.rank + 1) * m])
+        elif dist.get_backend(self.group) == "gloo":  # gloo has no reduce-scatter: all-reduce, keep the block
+            h = t.clone()
+            dist.all_reduce(h, group=self.group)
+            out.copy_(h[self.rank * m:(self.rank + 1) * m])
+        else:
+            dist.reduce_scatter_tensor(out, t, group=self.group)
+        return out
+
+    def all_gather_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """[m, ...] on every rank -> [size * m, ...], rank r's rows at block r (RCCL all-gather). Fake /
+        suspended groups return ``size`` copies of the local block."""
+        n = self.size
+        if self._suspend or not self.is_real:
+            if self.sim_comm is not None and t.is_cuda and not self._suspend:
+                self._sim_wait(n * t.numel() * t.element_size())
+            return torch.cat([t] * n) if n > 1 else t
+        t = t.contiguous()
+        out = torch.empty((n * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if self._native_ok(t):
+            self.comm.all_gather(t.data_ptr(), out.data_ptr(), t.numel(), self._code(t),
+                                 torch.cuda.current_stream().cuda_stream)
+        elif t.is_cuda and self.host_staged:
+            self._no_capture()
+            h = torch.empty((n * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype)
+            dist.all_gather_into_tensor(h, t.cpu(), group=self.group)
+            out.copy_(h)
+        else:
+            dist.all_gather_into_tensor(out, t, group=self.group)
+        return out
+
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.is_real and self._native_ok(t):
             if not t.is_contiguous():

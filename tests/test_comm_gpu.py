@@ -133,6 +133,7 @@ def test_decode_overlap_ab_at_capture(comm, monkeypatch):
             return [obj, obj]
 
     monkeypatch.setenv("LLMSS_TBO_AUTO_MIN", "16")
+    monkeypatch.setenv("LLMSS_TP_RSAG", "0")  # the one-rank stand-in's reduce-scatter is no TP=2 reduce-scatter
     tp = OneRankNative(0, 2, comm=comm)
     cfg = get_preset("tiny-llama", hidden_size=256, num_heads=4, num_kv_heads=2, head_dim=64, rotary_dim=64,
                      intermediate_size=512, max_position_embeddings=256)
@@ -140,7 +141,8 @@ def test_decode_overlap_ab_at_capture(comm, monkeypatch):
     prompts = [[int(x) for x in torch.randint(0, cfg.vocab_size, (n,))] for n in range(3, 23)]
     sp = SamplingParams(max_new_tokens=10, is_greedy=True, ignore_eos=True)
     e = LLMEngine(m, max_num_seqs=24, block_size=16, use_graphs=True, autotune=False, graph_buckets=[1, 8, 16, 24])
-    assert e._tbo_cands == [16, 24] and set(e.stats["tbo_ab_ms"]) >= {"16c", "24c"}
+    assert e._tbo_cands == [16, 24] and set(e.stats["schedule_ab_ms"]) >= {"16c", "24c"}
+    assert all(set(v) == {"one", "tbo"} for v in e.stats["schedule_ab_ms"].values())
     out_g = e.generate(prompts, sp)
     del e
     e2 = LLMEngine(m, max_num_seqs=24, block_size=16, use_graphs=False, autotune=False)

@@ -34,10 +34,16 @@ def _worker(rank, world, port, ckpt, prompts, q, env=None):
     if "LLMSS_TP_PREFILL_OVERLAP_MIN" in (env or {}):  # the 3-prompt prefill splits at a sequence boundary
         from llmss_amd.models.decoder import StepInput
         assert m.prefill_split(StepInput("prefill", *(torch.zeros(21),) * 3, cu_host=[0, 5, 12, 21])) == (2, 12)
+    calls = [0]
+    if (env or {}).get("LLMSS_TP_RSAG") == "1":  # the row-sharded decode schedule really runs
+        inner = m._hidden_states_rsag
+        m._hidden_states_rsag = lambda *a_, **k_: (calls.__setitem__(0, calls[0] + 1), inner(*a_, **k_))[1]
     eng = LLMEngine(m, max_num_seqs=4, block_size=4, num_blocks=64, check_tokens=True)
     greedy = eng.generate(prompts, SamplingParams(max_new_tokens=8, is_greedy=True, ignore_eos=True))
     sampled = eng.generate(prompts, [SamplingParams(max_new_tokens=8, temperature=0.9, top_k=20, top_p=0.9, seed=5 + i,
                                                     ignore_eos=True) for i in range(len(prompts))])
+    if (env or {}).get("LLMSS_TP_RSAG") == "1":
+        assert calls[0] > 0, "row-sharded decode schedule never ran"
     if r == 0:
         q.put((greedy, sampled))
     torch.distributed.barrier()
@@ -63,6 +69,7 @@ def _run(world, ckpt, prompts, env=None):
 _ROWS = {"LLMSS_TP_OVERLAP_ROWS": "4"}
 _TBO = {"LLMSS_TP_DECODE_OVERLAP_MIN": "2"}
 _PTBO = {"LLMSS_TP_PREFILL_OVERLAP_MIN": "2"}  # prefill steps as two micro-batches split at a sequence boundary
+_RSAG = {"LLMSS_TP_RSAG": "1"}  # row-sharded decode: reduce-scatter -> add + norm on M / tp rows -> all-gather
 
 
 @pytest.mark.parametrize("name,world,overlap", [("llama", 2, None), ("gptj", 2, None), ("bigcode", 4, None),
@@ -70,11 +77,15 @@ _PTBO = {"LLMSS_TP_PREFILL_OVERLAP_MIN": "2"}  # prefill steps as two micro-batc
                                                 ("gptj", 2, {"LLMSS_TP_OVERLAP_ROWS": "5"}), ("llama", 2, _TBO),
                                                 ("llama", 2, {"LLMSS_TP_BUCKET_BYTES": "64"}),
                                                 ("gptj", 2, _TBO), ("bigcode", 4, _TBO), ("llama", 2, _PTBO),
-                                                ("gptj", 2, _PTBO), ("bigcode", 4, {**_PTBO, **_TBO})])
+                                                ("gptj", 2, _PTBO), ("bigcode", 4, {**_PTBO, **_TBO}),
+                                                ("llama", 2, _RSAG), ("gptj", 2, _RSAG), ("bigcode", 4, _RSAG),
+                                                ("gpt2", 4, _RSAG)])
 def test_tp_matches_single(tmp_path, name, world, overlap):
     d = str(tmp_path / name)
     save_hf_model(name, d, vocab=101)  # 101 % world != 0 -> exercises the padded vocab-parallel head
-    prompts = [[(3 * i + 7 * j) % 100 for j in range(5 + 2 * i)] for i in range(3)]
+    # the row-sharded schedule needs decode batches divisible by the TP degree: 4 sequences
+    n = 4 if overlap is not None and "LLMSS_TP_RSAG" in overlap else 3
+    prompts = [[(3 * i + 7 * j) % 100 for j in range(5 + 2 * i)] for i in range(n)]
     from llmss_amd.engine import LLMEngine, SamplingParams, build_model
 
     m = build_model(d, None, "fp32", "cpu")

@@ -73,11 +73,12 @@ def _prefill_logits(m):
     return m(inp, kv)[:, :m.cfg.vocab_size].float().cpu()
 
 
-def _worker(rank, world, port, ckpt, q):
+def _worker(rank, world, port, ckpt, q, env=None):
     # both ranks share the box's one GPU: device 0 for both (LOCAL_RANK=rank would make rank 1's current
     # device cuda:1 on a multi-GPU box while its tensors live on cuda:0)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0")
+    os.environ.update(env or {})
     torch.set_num_threads(2)
     from llmss_amd.engine import LLMEngine, build_model
     from llmss_amd.ops import hip
@@ -96,8 +97,10 @@ def _worker(rank, world, port, ckpt, q):
     torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["llama", "gptj"])
-def test_tp2_native_matches_tp1(tmp_path, name):
+@pytest.mark.parametrize("name,rsag", [("llama", "0"), ("gptj", "0"), ("llama", "1"), ("gptj", "1")])
+def test_tp2_native_matches_tp1(tmp_path, name, rsag):
+    """rsag=1: decode steps run the row-sharded schedule (reduce-scatter, add + norm on half the rows, all-gather;
+    4 prompts = decode batches divisible by 2)."""
     from llmss_amd.engine import LLMEngine, build_model
 
     d = str(tmp_path / name)
@@ -112,7 +115,7 @@ def test_tp2_native_matches_tp1(tmp_path, name):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, d, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, d, q, {"LLMSS_TP_RSAG": rsag})) for r in range(2)]
     for p in procs:
         p.start()
     try:
