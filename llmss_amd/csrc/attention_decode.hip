@@ -16,108 +16,6 @@
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kNegBig = -1.0e30f;
 
-// Fused new-token prologue (decode): RoPE of q and of the new k, paged-cache write of the new k/v,
-// optionally from the QKV GEMM's split-K slabs. Replaces the rope_cache launch of a decode step.
-struct FusedRope {
-  const float* part;  // [S, B, N] fp32 split-K slabs of the QKV GEMM, or nullptr (read q)
-  int S;
-  int64_t slab;
-  const bf16_t* bias;  // QKV bias (with part) or nullptr
-  int N;               // qkv row width (elements)
-  const int64_t* pos;
-  const float* cos_t;
-  const float* sin_t;
-  const int64_t* slot;
-  int rot;    // rotary dims (0 = no rotation)
-  int style;  // 0 neox, 1 gptj
-  int k_off, v_off;
-};
-
-// 8 consecutive qkv elements [col, col+8) of row b, as the GEMM epilogue would have rounded them
-__device__ __forceinline__ void fused_load8(const bf16_t* q, int64_t q_stride, const FusedRope& fr, int b, int col,
-                                            float (&v)[8]) {
-  if (fr.part) {
-    const float* p = fr.part + (int64_t)b * fr.N + col;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = 0.f;
-    for (int z0 = 0; z0 < fr.S; z0 += 4) {  // 4 slabs in flight at a time (keeps the kernel at 8 waves/SIMD)
-      f32x4 x[4][2];
-#pragma unroll
-      for (int z = 0; z < 4; ++z) {
-        const float* pz = p + min(z0 + z, fr.S - 1) * fr.slab;
-        x[z][0] = *reinterpret_cast<const f32x4*>(pz);
-        x[z][1] = *reinterpret_cast<const f32x4*>(pz + 4);
-      }
-#pragma unroll
-      for (int z = 0; z < 4; ++z)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          v[j] += z0 + z < fr.S ? x[z][0][j] : 0.f;
-          v[4 + j] += z0 + z < fr.S ? x[z][1][j] : 0.f;
-        }
-    }
-    if (fr.bias) {
-      const u16x8 bb = *reinterpret_cast<const u16x8*>(fr.bias + col);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += bf2f(bb[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(v[j]));
-  } else {
-    const u16x8 a = *reinterpret_cast<const u16x8*>(q + b * q_stride + col);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = bf2f(a[j]);
-  }
-}
-
-// rotate the lane's 8 dims [8*sub, 8*sub+8) of one head at position p (result rounded to bf16, like
-// the standalone rope kernel that stores bf16); neox partners live in lane sub ^ (rot/16)
-template <int D>
-__device__ __forceinline__ void fused_rotate(float (&x)[8], const FusedRope& fr, int64_t p, int sub) {
-  if (fr.rot <= 0) return;
-  const int rh = fr.rot >> 1;
-  float y[8];
-  if (fr.style == 1) {  // gptj: pairs (2i, 2i+1) inside the lane's octet (table entries 4 sub .. 4 sub + 3)
-    if (8 * sub < fr.rot) {
-      const f32x4 c = *reinterpret_cast<const f32x4*>(fr.cos_t + p * rh + 4 * sub);
-      const f32x4 sn = *reinterpret_cast<const f32x4*>(fr.sin_t + p * rh + 4 * sub);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        y[2 * i] = x[2 * i] * c[i] - x[2 * i + 1] * sn[i];
-        y[2 * i + 1] = x[2 * i + 1] * c[i] + x[2 * i] * sn[i];
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) y[j] = x[j];
-    }
-  } else {  // neox: dim d < rot/2 pairs with d + rot/2 (all 8 dims of an octet are on one side)
-    const int xo = fr.rot >> 4;  // partner lane distance (power of two, < LPT)
-    float partner[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) partner[j] = __shfl_xor(x[j], xo, 64);
-    const int d0 = 8 * sub;
-    if (d0 < fr.rot) {
-      const int i0 = d0 < rh ? d0 : d0 - rh;  // 8 consecutive table entries
-      const f32x4 c0 = *reinterpret_cast<const f32x4*>(fr.cos_t + p * rh + i0);
-      const f32x4 c1 = *reinterpret_cast<const f32x4*>(fr.cos_t + p * rh + i0 + 4);
-      const f32x4 s0 = *reinterpret_cast<const f32x4*>(fr.sin_t + p * rh + i0);
-      const f32x4 s1 = *reinterpret_cast<const f32x4*>(fr.sin_t + p * rh + i0 + 4);
-      const float sg = d0 < rh ? -1.f : 1.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        y[j] = x[j] * c0[j] + sg * partner[j] * s0[j];
-        y[4 + j] = x[4 + j] * c1[j] + sg * partner[4 + j] * s1[j];
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) y[j] = x[j];
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) x[j] = bf2f(f2bf(y[j]));
-}
-
-
 // Sum over the LPT lanes that hold one token (LPT = D / 8 consecutive lanes) with DPP lane moves
 // instead of ds_bpermute shuffles (no LDS round trip in the per-token dependency chain).
 template <int CTRL>
@@ -146,16 +44,15 @@ __device__ __forceinline__ float token_sum(float s) {
 // KV8: the paged cache holds fp8 rows (D e4m3 bytes + fp32 scale at byte D, 16-B tail; reference.py
 // kv_rows_quant): each lane loads 8 bytes per token instead of 16 and the row scales multiply the score
 // (K) and the probability (V) instead of every element.
-template <int D, int GB, int UNROLL, bool FUSED, bool PIPE = false, bool KV8 = false>
-__global__ __launch_bounds__(256, (!FUSED && GB == 1) ? 8 : 1) void attn_decode_kernel(
+template <int D, int GB, int UNROLL, bool PIPE = false, bool KV8 = false>
+__global__ __launch_bounds__(256, GB == 1 ? 8 : 1) void attn_decode_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, void* __restrict__ kcv, void* __restrict__ vcv,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, bf16_t* __restrict__ out,
     int64_t out_stride, float* __restrict__ part_o, float* __restrict__ part_ml, int nh, int nkv, int G, int ngroups,
-    int block_size, int part_size, float scale_log2, FusedRope fr) {
+    int block_size, int part_size, float scale_log2) {
   constexpr int LPT = D / 8;
   constexpr int TPW = 64 / LPT;
   constexpr int RB = KV8 ? D + 16 : D;  // cache row, in cache elements (bytes for fp8 rows)
-  static_assert(!(KV8 && FUSED), "the fused new-token path writes bf16 rows");
   bf16_t* __restrict__ kc = (bf16_t*)kcv;
   bf16_t* __restrict__ vc = (bf16_t*)vcv;
   const unsigned char* __restrict__ kc8 = (const unsigned char*)kcv;
@@ -170,36 +67,16 @@ __global__ __launch_bounds__(256, (!FUSED && GB == 1) ? 8 : 1) void attn_decode_
 
   // q (pre-scaled into the log2 domain)
   float qv[GB][8];
-  float kn[8], vn[8];  // FUSED: the new token's (rotated) k and v, this lane's 8 dims
-  int64_t ppos = 0;
-  if constexpr (FUSED) ppos = fr.pos[b];
 #pragma unroll
   for (int h = 0; h < GB; ++h) {
     if (h < nvalid) {
-      if constexpr (FUSED) {
-        __builtin_amdgcn_sched_barrier(0);
-        fused_load8(q, q_stride, fr, b, (h0 + h) * D + sub * 8, qv[h]);
-        fused_rotate<D>(qv[h], fr, ppos, sub);
+      u16x8 a = *reinterpret_cast<const u16x8*>(q + b * q_stride + (int64_t)(h0 + h) * D + sub * 8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) qv[h][j] *= scale_log2;
-      } else {
-        u16x8 a = *reinterpret_cast<const u16x8*>(q + b * q_stride + (int64_t)(h0 + h) * D + sub * 8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qv[h][j] = bf2f(a[j]) * scale_log2;
-      }
+      for (int j = 0; j < 8; ++j) qv[h][j] = bf2f(a[j]) * scale_log2;
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) qv[h][j] = 0.f;
     }
-  }
-  if constexpr (FUSED) {
-    // one operand at a time: the prologue's register peak sets the whole kernel's occupancy
-    __builtin_amdgcn_sched_barrier(0);
-    fused_load8(q, q_stride, fr, b, fr.k_off + kvh * D + sub * 8, kn);
-    fused_rotate<D>(kn, fr, ppos, sub);
-    __builtin_amdgcn_sched_barrier(0);
-    fused_load8(q, q_stride, fr, b, fr.v_off + kvh * D + sub * 8, vn);
-    __builtin_amdgcn_sched_barrier(0);
   }
   float m[GB], l[GB], acc[GB][8];
 #pragma unroll
@@ -216,36 +93,7 @@ __global__ __launch_bounds__(256, (!FUSED && GB == 1) ? 8 : 1) void attn_decode_
   const int64_t head_off = (int64_t)kvh * block_size * RB + sub * 8;
   const int64_t page_stride = (int64_t)nkv * block_size * RB;
   constexpr int STEP = 4 * TPW;  // tokens per workgroup-iteration
-  // FUSED: the new token (position ctx-1) comes from registers, never from the cache this launch writes
-  const bool has_new = FUSED && ctx >= 1 && end == ctx && start < end;
-  const int lend = has_new ? ctx - 1 : end;
-  if constexpr (FUSED) {
-    const int64_t sl = fr.slot[b];
-    if (has_new && grp == 0 && sl >= 0 && w == 0 && slot == 0) {  // one writer per (sequence, kv head)
-      const int64_t a = (sl / block_size) * page_stride + head_off + (sl % block_size) * D;
-      u16x8 ko, vo;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { ko[j] = f2bf(kn[j]); vo[j] = f2bf(vn[j]); }
-      *reinterpret_cast<u16x8*>(kc + a) = ko;
-      *reinterpret_cast<u16x8*>(vc + a) = vo;
-    }
-    if (has_new) {  // the new token seeds slot 0 of wave 0 (kn / vn are dead before the token loop)
-#pragma unroll
-      for (int h = 0; h < GB; ++h) {
-        float sc = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) sc = fmaf(qv[h][j], kn[j], sc);
-#pragma unroll
-        for (int o = 1; o < LPT; o <<= 1) sc += __shfl_xor(sc, o, 64);
-        if (w == 0 && slot == 0) {
-          m[h] = sc;
-          l[h] = 1.f;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[h][j] = vn[j];
-        }
-      }
-    }
-  }
+  const int lend = end;
 
   // page ids of this workgroup's context range, staged once in LDS: the token loop then needs no
   // dependent block-table load (an L2 round trip) in front of every K/V load. The staged range is the
@@ -432,31 +280,28 @@ void attn_decode_set_unroll(int u) { g_decode_unroll = (u == 1 || u == 2 || u ==
 template <int D, int GB>
 static void launch_decode_t(const bf16_t* q, int64_t qs, bf16_t* kc, bf16_t* vc, const int* bt, int bts,
                             const int* cl, bf16_t* out, int64_t os, float* po, float* pml, int B, int nh, int nkv,
-                            int bs, int nsplit, int psize, float scale, hipStream_t st, const FusedRope* fr, bool kv8) {
+                            int bs, int nsplit, int psize, float scale, hipStream_t st, bool kv8) {
   const int G = nh / nkv;
   const int ngroups = (G + GB - 1) / GB;
   dim3 grid(B, nkv * ngroups, nsplit);
   const float sl2 = scale * kLog2e;
-#define AD(U_, FUSED_, PIPE_, KV8_)                                                                               \
-  attn_decode_kernel<D, GB, U_, FUSED_, PIPE_, KV8_><<<grid, 256, 0, st>>>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, \
-                                                                          nh, nkv, G, ngroups, bs, psize, sl2,      \
-                                                                          fr ? *fr : FusedRope{})
-  if (fr) {
-    AD(2, true, false, false);
-  } else if (kv8) {
+#define AD(U_, PIPE_, KV8_)                                                                                      \
+  attn_decode_kernel<D, GB, U_, PIPE_, KV8_><<<grid, 256, 0, st>>>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, nh, \
+                                                                  nkv, G, ngroups, bs, psize, sl2)
+  if (kv8) {
     switch (g_decode_unroll) {
-      case 2: AD(2, false, false, true); break;
-      case 12: AD(2, false, true, true); break;
-      default: AD(1, false, true, true); break;
+      case 2: AD(2, false, true); break;
+      case 12: AD(2, true, true); break;
+      default: AD(1, true, true); break;
     }
   } else {
     switch (g_decode_unroll) {
-      case 1: AD(1, false, false, false); break;
-      case 2: AD(2, false, false, false); break;
-      case 4: AD(4, false, false, false); break;
-      case 12: AD(2, false, true, false); break;
-      case 14: AD(4, false, true, false); break;
-      default: AD(1, false, true, false); break;
+      case 1: AD(1, false, false); break;
+      case 2: AD(2, false, false); break;
+      case 4: AD(4, false, false); break;
+      case 12: AD(2, true, false); break;
+      case 14: AD(4, true, false); break;
+      default: AD(1, true, false); break;
     }
   }
 #undef AD
@@ -470,20 +315,19 @@ static void launch_decode_t(const bf16_t* q, int64_t qs, bf16_t* kc, bf16_t* vc,
 template <int D>
 static void launch_decode_d(const bf16_t* q, int64_t qs, bf16_t* kc, bf16_t* vc, const int* bt, int bts,
                             const int* cl, bf16_t* out, int64_t os, float* po, float* pml, int B, int nh, int nkv,
-                            int bs, int nsplit, int psize, float scale, hipStream_t st, const FusedRope* fr, bool kv8) {
+                            int bs, int nsplit, int psize, float scale, hipStream_t st, bool kv8) {
   const int G = nh / nkv;
-  if (G == 1) launch_decode_t<D, 1>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, fr, kv8);
-  else if (G == 2) launch_decode_t<D, 2>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, fr, kv8);
-  else if (G <= 4) launch_decode_t<D, 4>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, fr, kv8);
-  else launch_decode_t<D, 8>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, fr, kv8);
+  if (G == 1) launch_decode_t<D, 1>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, kv8);
+  else if (G == 2) launch_decode_t<D, 2>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, kv8);
+  else if (G <= 4) launch_decode_t<D, 4>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, kv8);
+  else launch_decode_t<D, 8>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, kv8);
 }
 
 static void attn_decode_dispatch(const void* q, int64_t q_stride, void* kc, void* vc, const void* block_tables,
                                  int bt_stride, const void* ctx_lens, void* out, int64_t out_stride, void* part_o,
                                  void* part_ml, int B, int nh, int nkv, int D, int block_size, int nsplit,
-                                 int part_size, float scale, hipStream_t st, const FusedRope* fr, bool kv8 = false) {
+                                 int part_size, float scale, hipStream_t st, bool kv8 = false) {
   if (nh % nkv) throw std::runtime_error("attn_decode: nh must be a multiple of nkv");
-  if (kv8 && fr) throw std::runtime_error("attn_decode: the fused path writes bf16 cache rows");
   if (nsplit > 1 && (!part_o || !part_ml)) throw std::runtime_error("attn_decode: split needs workspaces");
   if (B == 0) return;
   auto Q = (const bf16_t*)q;
@@ -495,9 +339,9 @@ static void attn_decode_dispatch(const void* q, int64_t q_stride, void* kc, void
   auto PO = (float*)part_o;
   auto PML = (float*)part_ml;
   switch (D) {
-    case 64: launch_decode_d<64>(Q, q_stride, K, V, BT, bt_stride, CL, O, out_stride, PO, PML, B, nh, nkv, block_size, nsplit, part_size, scale, st, fr, kv8); break;
-    case 128: launch_decode_d<128>(Q, q_stride, K, V, BT, bt_stride, CL, O, out_stride, PO, PML, B, nh, nkv, block_size, nsplit, part_size, scale, st, fr, kv8); break;
-    case 256: launch_decode_d<256>(Q, q_stride, K, V, BT, bt_stride, CL, O, out_stride, PO, PML, B, nh, nkv, block_size, nsplit, part_size, scale, st, fr, kv8); break;
+    case 64: launch_decode_d<64>(Q, q_stride, K, V, BT, bt_stride, CL, O, out_stride, PO, PML, B, nh, nkv, block_size, nsplit, part_size, scale, st, kv8); break;
+    case 128: launch_decode_d<128>(Q, q_stride, K, V, BT, bt_stride, CL, O, out_stride, PO, PML, B, nh, nkv, block_size, nsplit, part_size, scale, st, kv8); break;
+    case 256: launch_decode_d<256>(Q, q_stride, K, V, BT, bt_stride, CL, O, out_stride, PO, PML, B, nh, nkv, block_size, nsplit, part_size, scale, st, kv8); break;
     default: throw std::runtime_error("attn_decode: head_dim must be 64, 128 or 256");
   }
 }
@@ -508,22 +352,5 @@ void launch_attn_decode(const void* q, int64_t q_stride, const void* kc, const v
                         float scale, hipStream_t st, bool kv8) {
   attn_decode_dispatch(q, q_stride, const_cast<void*>(kc), const_cast<void*>(vc), block_tables, bt_stride, ctx_lens,
                        out, out_stride, part_o, part_ml, B, nh, nkv, D, block_size, nsplit, part_size, scale, st,
-                       nullptr, kv8);
-}
-
-// decode attention with the rope + KV-cache write of the new token fused in (q = the QKV GEMM output
-// rows, or `part` = its split-K slabs); requires rot = 0 or a power of two >= 16 for neox, <= D
-void launch_attn_decode_fused(const void* qkv, int64_t q_stride, const void* part, int S, int64_t slab,
-                              const void* bias, int N, const void* pos, const void* cos_t, const void* sin_t,
-                              const void* slots, int rot, int style, int k_off, int v_off, void* kc, void* vc,
-                              const void* block_tables, int bt_stride, const void* ctx_lens, void* out,
-                              int64_t out_stride, void* part_o, void* part_ml, int B, int nh, int nkv, int D,
-                              int block_size, int nsplit, int part_size, float scale, hipStream_t st) {
-  if (rot < 0 || rot > D || rot % 8) throw std::runtime_error("attn_decode_fused: bad rotary_dim");
-  if (rot && style == 0 && (rot < 16 || (rot & (rot - 1)))) throw std::runtime_error("attn_decode_fused: neox rot");
-  if (part && (S < 1 || N % 8)) throw std::runtime_error("attn_decode_fused: bad partial slabs");
-  FusedRope fr{(const float*)part, S, slab, (const bf16_t*)bias, N, (const int64_t*)pos, (const float*)cos_t,
-               (const float*)sin_t, (const int64_t*)slots, rot, style, k_off, v_off};
-  attn_decode_dispatch(qkv, q_stride, kc, vc, block_tables, bt_stride, ctx_lens, out, out_stride, part_o, part_ml, B,
-                       nh, nkv, D, block_size, nsplit, part_size, scale, st, &fr);
+                       kv8);
 }

@@ -39,21 +39,10 @@ void launch_attn_extend(const void* q, int64_t q_stride, const void* k_cache, co
                         const void* block_tables, int max_blocks, const void* cu_q, const void* ctx_lens, void* out,
                         int64_t out_stride, int B, int max_qlen, int nh, int nkv, int D, int bs, float scale,
                         hipStream_t st, bool kv8);
-void launch_attn_decode_fused(const void* qkv, int64_t q_stride, const void* part, int S, int64_t slab,
-                              const void* bias, int N, const void* pos, const void* cos_t, const void* sin_t,
-                              const void* slots, int rot, int style, int k_off, int v_off, void* kc, void* vc,
-                              const void* block_tables, int bt_stride, const void* ctx_lens, void* out,
-                              int64_t out_stride, void* part_o, void* part_ml, int B, int nh, int nkv, int D,
-                              int block_size, int nsplit, int part_size, float scale, hipStream_t st);
 int launch_gemm_qkv_args(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y, int64_t ldy,
                          int M, int N, int K, void* workspace, int64_t ws_bytes, int nt_hint, int split_hint,
                          const void* pos, const void* cos_t, const void* sin_t, void* kc, void* vc, const void* slot,
-                         int nh, int nkv, int D, int rot, int block_size, int style, bool do_rope, hipStream_t st,
-                         const void* rstat, const void* c1, float inv_k, float eps);
-int launch_gemm_fold_args(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y,
-                          int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace, int64_t ws_bytes,
-                          int nt_hint, int split_hint, const void* rstat, const void* c1, float inv_k, float eps,
-                          void* wstat, hipStream_t st);
+                         int nh, int nkv, int D, int rot, int block_size, int style, bool do_rope, hipStream_t st);
 int launch_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, bool w_fp8, const void* w_scale,
                 const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace,
                 int64_t ws_bytes, int nt_hint, int split_hint, bool partial_out, hipStream_t st);
@@ -115,15 +104,6 @@ PYBIND11_MODULE(_C, m) {
     launch_attn_decode(CP(q), qs, CP(kc), CP(vc), CP(bt), bts, CP(cl), P(out), os, P(po), P(pml), B, nh, nkv, D, bs,
                        nsplit, psize, scale, S(st), kv8);
   });
-  m.def("attn_decode_fused", [](uintptr_t qkv, int64_t qs, uintptr_t part, int S, int64_t slab, uintptr_t bias, int N,
-                                uintptr_t pos, uintptr_t cos_t, uintptr_t sin_t, uintptr_t slots, int rot, int style,
-                                int k_off, int v_off, uintptr_t kc, uintptr_t vc, uintptr_t bt, int bts, uintptr_t cl,
-                                uintptr_t out, int64_t os, uintptr_t po, uintptr_t pml, int B, int nh, int nkv, int D,
-                                int bs, int nsplit, int psize, float scale, uintptr_t st) {
-    launch_attn_decode_fused(CP(qkv), qs, CP(part), S, slab, CP(bias), N, CP(pos), CP(cos_t), CP(sin_t), CP(slots), rot,
-                             style, k_off, v_off, P(kc), P(vc), CP(bt), bts, CP(cl), P(out), os, P(po), P(pml), B, nh,
-                             nkv, D, bs, nsplit, psize, scale, S(st));
-  });
   m.def("attn_prefill", [](uintptr_t qkv, int64_t rs, int T, uintptr_t cu, uintptr_t out, int64_t os, int B,
                            int maxlen, int nh, int nkv, int D, int k_off, int v_off, float scale, uintptr_t st) {
     launch_attn_prefill(CP(qkv), rs, T, CP(cu), P(out), os, B, maxlen, nh, nkv, D, k_off, v_off, scale, S(st));
@@ -159,25 +139,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_qkv", [](uintptr_t x, int64_t ldx, uintptr_t w, int64_t ldw, uintptr_t bias, uintptr_t y, int64_t ldy,
                        int M, int N, int K, uintptr_t work, int64_t wbytes, int nt_hint, int split_hint, uintptr_t pos,
                        uintptr_t cos_t, uintptr_t sin_t, uintptr_t kc, uintptr_t vc, uintptr_t slot, int nh, int nkv,
-                       int D, int rot, int bs, int style, bool do_rope, uintptr_t st, uintptr_t rstat, uintptr_t c1,
-                       float inv_k, float eps) {
+                       int D, int rot, int bs, int style, bool do_rope, uintptr_t st) {
     return launch_gemm_qkv_args(CP(x), ldx, CP(w), ldw, CP(bias), P(y), ldy, M, N, K, P(work), wbytes, nt_hint,
                                 split_hint, CP(pos), CP(cos_t), CP(sin_t), P(kc), P(vc), CP(slot), nh, nkv, D, rot, bs,
-                                style, do_rope, S(st), CP(rstat), CP(c1), inv_k, eps);
+                                style, do_rope, S(st));
   }, pybind11::arg("x"), pybind11::arg("ldx"), pybind11::arg("w"), pybind11::arg("ldw"), pybind11::arg("bias"),
      pybind11::arg("y"), pybind11::arg("ldy"), pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"),
      pybind11::arg("work"), pybind11::arg("wbytes"), pybind11::arg("nt_hint"), pybind11::arg("split_hint"),
      pybind11::arg("pos"), pybind11::arg("cos_t"), pybind11::arg("sin_t"), pybind11::arg("kc"), pybind11::arg("vc"),
      pybind11::arg("slot"), pybind11::arg("nh"), pybind11::arg("nkv"), pybind11::arg("D"), pybind11::arg("rot"),
-     pybind11::arg("bs"), pybind11::arg("style"), pybind11::arg("do_rope"), pybind11::arg("st"),
-     pybind11::arg("rstat") = 0, pybind11::arg("c1") = 0, pybind11::arg("inv_k") = 0.f, pybind11::arg("eps") = 0.f);
-  m.def("gemm_fold", [](uintptr_t x, int64_t ldx, uintptr_t w, int64_t ldw, uintptr_t bias, uintptr_t y, int64_t ldy,
-                        int M, int N, int K, int act, bool glu, uintptr_t work, int64_t wbytes, int nt_hint,
-                        int split_hint, uintptr_t rstat, uintptr_t c1, float inv_k, float eps, uintptr_t wstat,
-                        uintptr_t st) {
-    return launch_gemm_fold_args(CP(x), ldx, CP(w), ldw, CP(bias), P(y), ldy, M, N, K, act, glu, P(work), wbytes,
-                                 nt_hint, split_hint, CP(rstat), CP(c1), inv_k, eps, P(wstat), S(st));
-  });
+     pybind11::arg("bs"), pybind11::arg("style"), pybind11::arg("do_rope"), pybind11::arg("st"));
   m.def("gemm_plan", [](int M, int N, int K, bool fp8) {
     int nt, s;
     gemm_plan(M, N, K, fp8, &nt, &s);

@@ -162,17 +162,6 @@ __device__ __forceinline__ TileWork tile_work(int ntm, int ntn, int bm, int bn) 
 // with head-aligned tiles; gptj: pairs inside the group), stores the row to the qkv buffer and the k / v
 // groups to their paged-cache rows (bf16 caches). D == 0: not a QKV projection.
 //
-// The same struct carries the norm-folded decode epilogues (TP = 1; models/decoder.py "norm fold"), which
-// remove both add_norm launches of a layer:
-//   * consumer (rstat != nullptr): the GEMM's A operand is the raw residual stream h and its weights were
-//     multiplied by the norm weight along K at load, so the tile is finished as
-//         v = rstd[m] * acc - rstd[m] * mean[m] * c1[n]      (c1 = row sums of the folded weight; LayerNorm)
-//         v = rstd[m] * acc                                 (RMSNorm: c1 == nullptr, mean unused)
-//     before bias / activation / SwiGLU / RoPE, with mean and rstd from rstat[m] = (sum h, sum h^2) over
-//     the inv_k = 1 / K columns of the row;
-//   * producer (wstat != nullptr): the output tile is the residual update h[m, n] += acc + bias, stored
-//     in place into Y (= h) and the bf16-rounded row sums (sum, sum of squares) are added into
-//     wstat[m] with fp32 atomics - the next consumer's rstat.
 struct QkvEpi {
   const int64_t* pos;
   const float* cos_t;
@@ -181,11 +170,6 @@ struct QkvEpi {
   bf16_t* vc;
   const int64_t* slot;
   int nh, nkv, D, rot, block_size, style, do_rope;
-  const float* rstat;  // consumer: [M][2] row (sum, sum of squares) of the A operand
-  const float* c1;     // consumer, LayerNorm: [N] fp32 column sums of the folded weight
-  float inv_k, eps;
-  float* wstat;  // producer: [M][2] accumulated (sum, sum of squares) of the new residual rows
-  __host__ __device__ bool fold() const { return rstat != nullptr || wstat != nullptr; }
 };
 
 // One LDS row chunk of the QKV epilogue: each thread owns ITEMS (row, 8-column) groups of the chunk and
@@ -290,11 +274,10 @@ __device__ __forceinline__ void tile_store_lds(const f32x4 (&acc)[MT][NT], char*
                                                bf16_t* __restrict__ Y, int64_t ldy, const bf16_t* __restrict__ bias,
                                                int act, int glu, const QkvEpi& qe = QkvEpi{}) {
   constexpr int LDW = BN + 4;  // padded row: the 4 rows a wave-instruction writes hit different banks
-  constexpr int RMAX = (LDSB - 2 * BM * 4) / (LDW * 4);  // the tail holds the norm-fold row factors
+  constexpr int RMAX = LDSB / (LDW * 4);
   constexpr int R = (RMAX >= BM ? BM : RMAX) / 16 * 16;
   static_assert(R >= 16, "LDS too small for a 16-row epilogue chunk");
   float* ct = reinterpret_cast<float*>(lds);
-  float* rowf = reinterpret_cast<float*>(lds + LDSB - 2 * BM * 4);  // (rstd, rstd * mean) per chunk row
   const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every wave is done reading the operand stages
   __builtin_amdgcn_s_barrier();
@@ -313,37 +296,6 @@ __device__ __forceinline__ void tile_store_lds(const f32x4 (&acc)[MT][NT], char*
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const int rows = BM - r0 < R ? BM - r0 : R;  // the last chunk may be shorter
-    if (qe.rstat) {  // norm-fold consumer: finish the normalisation on the fp32 tile, in place
-      for (int r = threadIdx.x; r < rows; r += NTHR) {
-        const int m = min(m0 + r0 + r, M - 1);
-        const float s1 = qe.rstat[2 * m], s2 = qe.rstat[2 * m + 1];
-        const float mean = qe.c1 ? s1 * qe.inv_k : 0.f;
-        const float rs = rsqrtf(fmaxf(s2 * qe.inv_k - mean * mean, 0.f) + qe.eps);
-        rowf[2 * r] = rs;
-        rowf[2 * r + 1] = rs * mean;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      constexpr int VPR = BN / 4;
-      for (int v = threadIdx.x; v < rows * VPR; v += NTHR) {
-        const int r = v / VPR, c = (v - r * VPR) * 4, n = n0 + c;
-        f32x4 x = *reinterpret_cast<const f32x4*>(&ct[r * LDW + c]);
-        const float a = rowf[2 * r], b = rowf[2 * r + 1];
-        f32x4 cs = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (qe.c1) {
-          if (n + 3 < N && (N & 3) == 0) cs = *reinterpret_cast<const f32x4*>(qe.c1 + n);
-          else
-            for (int j = 0; j < 4; ++j) cs[j] = n + j < N ? qe.c1[n + j] : 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) x[j] = a * x[j] - b * cs[j];
-        *reinterpret_cast<f32x4*>(&ct[r * LDW + c]) = x;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
     if (qe.D) {  // QKV projection: RoPE + paged KV write (N % 8 == 0, ldy % 8 == 0: host-checked)
       qkv_store_chunk<BN, NTHR, R>(qe, ct, LDW, rows, r0, m0, n0, M, N, Y, ldy, bias);
     } else if (part) {  // fp32 slab rows: 4 floats (16 B) per thread-step
@@ -376,50 +328,6 @@ __device__ __forceinline__ void tile_store_lds(const f32x4 (&acc)[MT][NT], char*
         if (ng + 16 + 7 < N && (ldy & 7) == 0) *reinterpret_cast<u16x8*>(dst) = o;
         else
           for (int e = 0; e < 8 && ng + 16 + e < N; ++e) dst[e] = o[e];
-      }
-    } else if (qe.wstat) {  // norm-fold producer: h += acc + bias in place, row (sum, sum^2) of the new h
-      // per-row partial sums gather in LDS (rowf, beside the image), then one global atomic pair per row
-      constexpr int VPR = BN / 8;
-      for (int r = threadIdx.x; r < 2 * rows; r += NTHR) rowf[r] = 0.f;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      for (int v = threadIdx.x; v < rows * VPR; v += NTHR) {
-        const int r = v / VPR, c = (v - r * VPR) * 8;
-        const int m = m0 + r0 + r, n = n0 + c;
-        if (m >= M || n >= N) continue;
-        const bool full = n + 7 < N && (ldy & 7) == 0;
-        bf16_t* dst = Y + (int64_t)m * ldy + n;
-        u16x8 h;
-        if (full) h = *reinterpret_cast<const u16x8*>(dst);
-        else
-          for (int e = 0; e < 8; ++e) h[e] = n + e < N ? dst[e] : (bf16_t)0;
-        u16x8 o;
-        float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float x = ct[r * LDW + c + e] + bf2f(h[e]);
-          if (bias && n + e < N) x += bf2f(bias[n + e]);
-          o[e] = f2bf(x);
-          const float q = n + e < N ? bf2f(o[e]) : 0.f;
-          s1 += q;
-          s2 += q * q;
-        }
-        if (full) *reinterpret_cast<u16x8*>(dst) = o;
-        else
-          for (int e = 0; e < 8 && n + e < N; ++e) dst[e] = o[e];
-        atomicAdd(rowf + 2 * r, s1);
-        atomicAdd(rowf + 2 * r + 1, s2);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      for (int r = threadIdx.x; r < rows; r += NTHR) {
-        const int m = m0 + r0 + r;
-        if (m < M) {
-          atomicAdd(qe.wstat + 2 * m, rowf[2 * r]);
-          atomicAdd(qe.wstat + 2 * m + 1, rowf[2 * r + 1]);
-        }
       }
     } else {  // bf16 rows: 8 values (16 B) per thread-step
       constexpr int VPR = BN / 8;

@@ -622,9 +622,9 @@ __global__ __launch_bounds__(64 * NW) void gemm_tiled_kernel(const bf16_t* __res
     part = nullptr;
   }
   if constexpr (!F8) {
-    // QKV projection (RoPE + paged KV write) and the norm-fold epilogues run in the LDS-staged epilogue
+    // QKV projection (RoPE + paged KV write) runs in the LDS-staged epilogue
     // (unsplit / combined plans only)
-    if (qe.D || qe.fold()) {
+    if (qe.D) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       tile_store_lds<BM, BN, MTW, NTW, 64 * NW, NS * STAGE>(acc, smem, wr * (MTW * 16), wc * (NTW * 16), m0, n0, M,
                                                              N, nullptr, Y, ldy, bias, act, glu, qe);
@@ -1383,7 +1383,7 @@ namespace {
 std::mutex g_tuned_mu;
 std::unordered_map<uint64_t, std::pair<int, int>> g_tuned;
 // kind: 0 = bf16 [N, K] weights, 1 = fp8 weights, 2 = packed bf16 weights (launch_gemm_packed), 3 = QKV
-// RoPE / KV-write epilogue, 4 = norm-fold consumer, 5 = norm-fold producer (launch_gemm_epi)
+// RoPE / KV-write epilogue (launch_gemm_qkv)
 uint64_t tune_key(int M, int N, int K, bool glu, int kind) {
   return ((uint64_t)(kind & 7) << 61) | ((uint64_t)(M & 0x7FFFF) << 42) | ((uint64_t)N << 22) |
          ((uint64_t)K << 2) | (glu ? 2u : 0u) | (kind == 1 ? 1u : 0u);
@@ -1743,92 +1743,44 @@ int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int n
   return s > 1 ? s : 0;
 }
 
-// GEMMs with an LDS-staged epilogue that needs finished sums (common.h QkvEpi): the QKV projection's
-// RoPE + paged-KV write (qe.D > 0, tuned kind 3) and the norm-fold consumer / producer (qe.rstat / qe.wstat,
-// kinds 4 / 5; models/decoder.py). Plan: the hints, else the tuned entry of `kind`, else (fold only) the
-// plain plan of the shape, else the static tiled plan; a split plan always runs as an in-launch combine.
-// QKV-only calls return -1 when the shape / plan cannot take the epilogue (stream / big-tile / stream-K
-// plans, neox RoPE on tiles that are not head-aligned) - the caller then runs the plain GEMM and the
-// rope_cache kernel. Fold calls cannot fall back (their weights are folded), so an unusable plan is
-// replaced by the static tiled plan instead. Returns 0 when launched.
-int launch_gemm_epi(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y, int64_t ldy,
-                    int M, int N, int K, int act, bool glu, void* workspace, int64_t ws_bytes, int nt_hint,
-                    int split_hint, int kind, const QkvEpi& qe, hipStream_t st) {
-  if (M == 0) return 0;
-  const bool fold = qe.fold();
-  if (!y) throw std::runtime_error("gemm_epi: output buffer required");
-  if (K % 16) throw std::runtime_error("gemm_epi: K must be a multiple of 16");
-  if (glu && (N % 32)) throw std::runtime_error("gemm_epi: glu needs N % 32 == 0");
-  if (qe.wstat && (glu || act || qe.D || qe.rstat))
-    throw std::runtime_error("gemm_epi: the residual producer takes no activation / consumer epilogue");
-  if (qe.D) {
-    if (qe.D < 0 || qe.D % 8 || N != (qe.nh + 2 * qe.nkv) * qe.D || N % 8 || ldy % 8 || glu || act) return -1;
-    if (qe.do_rope && (qe.rot % 8 || qe.rot > qe.D || (qe.style == 0 && qe.rot % 16))) return -1;
-  }
-  if (nt_hint == 0 && split_hint == 0 && !gemm_tuned_get(M, N, K, glu, kind, &nt_hint, &split_hint) && fold &&
-      !qe.D)
-    gemm_tuned_get(M, N, K, glu, 0, &nt_hint, &split_hint);
-  if (nt_hint & 0xff) {  // streaming kernels have no LDS-staged epilogue
-    if (!fold) return -1;
-    nt_hint = split_hint = 0;
-  }
-  int tsel = nt_hint >> 8, s = split_hint;
-  gemm_tiled_plan(M, N, K, &tsel, &s, glu);
-  if ((tsel & 15) == 4 || (tsel & 128)) {
-    if (!fold) return -1;
-    tsel = M <= 64 ? 3 : 1;
-    s = 0;
-    gemm_tiled_plan(M, N, K, &tsel, &s, glu);
-  }
-  int bm, bn;
-  tile_dims(tsel & 15, &bm, &bn);
-  if (qe.D && qe.do_rope && qe.style == 0 && bn % qe.D) return -1;  // neox partner columns must share the tile
-  if (s > 1) {
-    if ((int64_t)tiles_of(M, N, bm, bn) * s * bm * bn * 4 > ws_bytes) {
-      if (!fold) return -1;
-      s = 1;
-    } else {
-      tsel |= 256;
-    }
-  }
-  launch_tiled((const bf16_t*)x, ldx, w, ldw, (const bf16_t*)bias, (bf16_t*)y, ldy, M, N, K, act, glu ? 1 : 0, tsel,
-               s, workspace, ws_bytes, false, st, nullptr, &qe);
-  return 0;
-}
-
+// QKV projection with the RoPE + paged-KV write in its LDS-staged epilogue (common.h QkvEpi, tuned kind 3).
+// Plan: the hints, else the tuned kind-3 entry, else the static tiled plan; a split plan runs as an in-launch
+// combine (the epilogue needs finished sums). Returns -1 when the shape / plan cannot take the epilogue
+// (stream / big-tile / stream-K plans, neox RoPE on tiles that are not head-aligned, workspace too small) -
+// the caller then runs the plain GEMM and the rope_cache kernel; 0 when launched.
 int launch_gemm_qkv(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y, int64_t ldy,
                     int M, int N, int K, void* workspace, int64_t ws_bytes, int nt_hint, int split_hint,
                     const QkvEpi& qe, hipStream_t st) {
+  if (M == 0) return 0;
   if (qe.D <= 0) return -1;
-  return launch_gemm_epi(x, ldx, w, ldw, bias, y, ldy, M, N, K, 0, false, workspace, ws_bytes, nt_hint, split_hint, 3,
-                         qe, st);
+  if (!y) throw std::runtime_error("gemm_qkv: output buffer required");
+  if (K % 16) throw std::runtime_error("gemm_qkv: K must be a multiple of 16");
+  if (qe.D % 8 || N != (qe.nh + 2 * qe.nkv) * qe.D || N % 8 || ldy % 8) return -1;
+  if (qe.do_rope && (qe.rot % 8 || qe.rot > qe.D || (qe.style == 0 && qe.rot % 16))) return -1;
+  if (nt_hint == 0 && split_hint == 0) gemm_tuned_get(M, N, K, false, 3, &nt_hint, &split_hint);
+  if (nt_hint & 0xff) return -1;  // streaming kernels have no LDS-staged epilogue
+  int tsel = nt_hint >> 8, s = split_hint;
+  gemm_tiled_plan(M, N, K, &tsel, &s, false);
+  if ((tsel & 15) == 4 || (tsel & 128)) return -1;
+  int bm, bn;
+  tile_dims(tsel & 15, &bm, &bn);
+  if (qe.do_rope && qe.style == 0 && bn % qe.D) return -1;  // neox partner columns must share the tile
+  if (s > 1) {
+    if ((int64_t)tiles_of(M, N, bm, bn) * s * bm * bn * 4 > ws_bytes) return -1;
+    tsel |= 256;
+  }
+  launch_tiled((const bf16_t*)x, ldx, w, ldw, (const bf16_t*)bias, (bf16_t*)y, ldy, M, N, K, 0, 0, tsel, s, workspace,
+               ws_bytes, false, st, nullptr, &qe);
+  return 0;
 }
 
 int launch_gemm_qkv_args(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y, int64_t ldy,
                          int M, int N, int K, void* workspace, int64_t ws_bytes, int nt_hint, int split_hint,
                          const void* pos, const void* cos_t, const void* sin_t, void* kc, void* vc, const void* slot,
-                         int nh, int nkv, int D, int rot, int block_size, int style, bool do_rope, hipStream_t st,
-                         const void* rstat, const void* c1, float inv_k, float eps) {
+                         int nh, int nkv, int D, int rot, int block_size, int style, bool do_rope, hipStream_t st) {
   const QkvEpi qe{(const int64_t*)pos, (const float*)cos_t, (const float*)sin_t, (bf16_t*)kc, (bf16_t*)vc,
-                  (const int64_t*)slot, nh, nkv, D, rot, block_size, style, do_rope ? 1 : 0,
-                  (const float*)rstat, (const float*)c1, inv_k, eps, nullptr};
+                  (const int64_t*)slot, nh, nkv, D, rot, block_size, style, do_rope ? 1 : 0};
   return launch_gemm_qkv(x, ldx, w, ldw, bias, y, ldy, M, N, K, workspace, ws_bytes, nt_hint, split_hint, qe, st);
-}
-
-// norm-fold GEMM (kind 4: consumer with rstat [M][2] / c1 [N]; kind 5: producer accumulating wstat [M][2])
-int launch_gemm_fold_args(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y,
-                          int64_t ldy, int M, int N, int K, int act, bool glu, void* workspace, int64_t ws_bytes,
-                          int nt_hint, int split_hint, const void* rstat, const void* c1, float inv_k, float eps,
-                          void* wstat, hipStream_t st) {
-  QkvEpi qe{};
-  qe.rstat = (const float*)rstat;
-  qe.c1 = (const float*)c1;
-  qe.inv_k = inv_k;
-  qe.eps = eps;
-  qe.wstat = (float*)wstat;
-  if (!qe.fold()) throw std::runtime_error("gemm_fold: neither row statistics in nor out");
-  return launch_gemm_epi(x, ldx, w, ldw, bias, y, ldy, M, N, K, act, glu, workspace, ws_bytes, nt_hint, split_hint,
-                         wstat ? 5 : 4, qe, st);
 }
 
 void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk) {

@@ -190,15 +190,6 @@ class LLMEngine:
         self.dist_sampling = (self.tp.size > 1 and os.environ.get("LLMSS_DIST_SAMPLER", "1") != "0"
                               and self.tp.size * CAND_KC <= 2048  # sample_cand's gathered-candidate limit
                               and (not self.is_gpu or model.plan.v_l <= CAND_MAX_SHARD))
-        # one GPU (TP=1), opt-in (LLMSS_CAND_SHARDS=8): the same two-kernel candidate sampler over column shards
-        # of the vocabulary (one launch, B x shards workgroups) instead of one workgroup per row scanning all of
-        # it; exact for the same rows. Measured end to end it LOST (bench.py: Llama-2-7B 11.69K -> 10.96K tok/s,
-        # GPT-2-XL 18.0K -> 16.7K; profiles/r2_s4/bench_cand_shards.log), so the one-kernel v3 sampler stays
-        self.cand_shards = 1
-        shards = int(os.environ.get("LLMSS_CAND_SHARDS", "0"))
-        if self.tp.size == 1 and self.is_gpu and shards > 1 and os.environ.get("LLMSS_DIST_SAMPLER", "1") != "0" \
-                and -(-model.plan.v_l // shards) <= CAND_MAX_SHARD and shards * CAND_KC <= 2048:
-            self.dist_sampling, self.cand_shards = True, shards
         self.buckets = sorted(set(graph_buckets or self._default_buckets()))
         self.buckets = [b for b in self.buckets if b <= max_num_seqs] or [max_num_seqs]
         if self.buckets[-1] < max_num_seqs:
@@ -584,8 +575,7 @@ class LLMEngine:
             h = m.hidden_states(inp, self.kv)
             if inp.last_idx is not None:
                 h = h.index_select(0, inp.last_idx)
-            return ops.sample_distributed(m.local_logits(h), self.tp, m.vocab_lo, V, temp, topk, topp, seeds, out=out,
-                                          shards=self.cand_shards)
+            return ops.sample_distributed(m.local_logits(h), self.tp, m.vocab_lo, V, temp, topk, topp, seeds, out=out)
         logits = m(inp, self.kv)
         if logits.is_cuda:
             return _hip_ops.sample(logits, temp, topk, topp, seeds, vocab=min(V, logits.shape[-1]), out=out)

@@ -68,8 +68,7 @@ class StepInput:
 
 
 class DecoderLM:
-    def __init__(self, cfg: ModelConfig, weights: ModelWeights, tp: Optional[TPGroup] = None,
-                 norm_fold: Optional[bool] = None):
+    def __init__(self, cfg: ModelConfig, weights: ModelWeights, tp: Optional[TPGroup] = None):
         if weights.rope_interleaved and cfg.rope_style == "neox":
             # q / k head dims were interleaved at load: the same rotation in its gptj (adjacent-pair) form
             cfg = dataclasses.replace(cfg, rope_style="gptj")
@@ -88,9 +87,6 @@ class DecoderLM:
         rows = os.environ.get("LLMSS_TP_OVERLAP_ROWS")
         self.overlap_rows = int(rows) if rows else None
         self.bucket_bytes = int(os.environ.get("LLMSS_TP_BUCKET_BYTES", str(32 << 20)))
-        # fused RoPE+KV-write+attention decode: correct, but measured slower (its prologue halves the
-        # attention kernel's occupancy), so opt-in
-        self.fused_decode = os.environ.get("LLMSS_FUSED_DECODE", "0") == "1"
         # fp8 (e4m3 + per-row scale) paged KV cache (LLMSS_KV_DTYPE=fp8 or LLMEngine(kv_dtype="fp8"))
         self.kv_fp8 = os.environ.get("LLMSS_KV_DTYPE", "bf16") == "fp8"
         # decode steps of at least this many sequences run as two interleaved micro-batches so each
@@ -121,73 +117,6 @@ class DecoderLM:
         self.rsag: set = set()
         self._cu_decode = {}
         self._comm_stream = None
-        # norm fold (TP = 1 decode): no add_norm launch inside the layer stack - see fold_norms. Opt-in
-        # (LLMSS_NORM_FOLD=1): measured on MI355X it LOSES (profiles/r3_fold: Llama-2-7B 11.50 K vs 11.73 K
-        # tok/s, GPT-2-XL TPOT 3.66 vs 3.26 ms) - the o / down producers need finished sums, and the in-launch
-        # split-K combine behind them costs more (+5-7 us per GEMM) than the add_norm launches it removes
-        if norm_fold is None:
-            norm_fold = os.environ.get("LLMSS_NORM_FOLD", "0") == "1" and weights.wte.is_cuda
-        self.norm_fold = bool(norm_fold) and self.fold_norms()
-
-    # ---------------------------------------------------------------------------- norm fold
-    def fold_norms(self) -> bool:
-        """Fold each layer's norm weight (and LayerNorm bias) into the linear that consumes the norm's output.
-
-        With  W' = W * g (along K),  c0 = W b + bias  and (LayerNorm)  c1 = W' 1:
-            W norm(h) + bias = rstd(h) * (W' h - mean(h) * c1) + c0,
-        so a decode step's QKV and up projections read the raw residual stream h and finish the norm in their
-        epilogue from per-row (sum, sum of squares) that the PREVIOUS GEMM - o / down, whose epilogue adds its
-        output into h in place - accumulated (csrc/common.h QkvEpi). Both add_norm launches of every layer go
-        away (reference: the fused add + LayerNorm of layers.py:217-253, taken one launch further). Prefill /
-        extend steps run the same weights after an add_norm without affine terms (g = 1, b = 0).
-        Only TP = 1 (a row-parallel output must be all-reduced before the residual add), sequential blocks,
-        bf16 row-major weights. In place on the weights (``extra["norm_fold"]`` marks it); returns whether
-        the model runs folded."""
-        cfg, w = self.cfg, self.w
-        if w.extra.get("norm_fold"):
-            return True
-        if self.tp.size != 1 or cfg.parallel_block:
-            return False
-        for L in w.layers:
-            for lin in (L.qkv, L.o, L.up, L.down):
-                if lin.packed or lin.w_scale is not None or lin.w.dtype not in (torch.bfloat16, torch.float32):
-                    return False
-        ln = not self.rms
-        with torch.no_grad():
-            for L in w.layers:
-                for lin, g, b in ((L.qkv, L.ln1_w, L.ln1_b), (L.up, L.ln2_w, L.ln2_b)):
-                    wq, c0, c1 = ops.ref.fold_norm_into(lin.w, lin.b, g, b if ln else None, ln)
-                    lin.w.copy_(wq)
-                    lin.b, lin.c1 = c0, c1
-                L.ln1_w, L.ln2_w = torch.ones_like(L.ln1_w), torch.ones_like(L.ln2_w)
-                if ln:
-                    L.ln1_b = torch.zeros_like(L.ln1_w)
-                    L.ln2_b = torch.zeros_like(L.ln2_w)
-                else:
-                    L.ln1_b = L.ln2_b = None
-        w.extra["norm_fold"] = True
-        return True
-
-    def _hidden_states_folded(self, inp: StepInput, kv_caches) -> torch.Tensor:
-        """Decode step on folded norms: per layer QKV(+RoPE/KV) -> attention -> o (h += o, stats) -> up (norm in
-        the epilogue) -> down (h += down, stats); layer 0's input norm and the final norm stay add_norm."""
-        cfg, w = self.cfg, self.w
-        eps, rms = cfg.norm_eps, self.rms
-        h = ops.embed(inp.input_ids, w.wte, inp.positions if w.wpe is not None else None, w.wpe)
-        M = h.shape[0]
-        stats = torch.zeros(2 * len(w.layers), M, 2, dtype=torch.float32, device=h.device)
-        for i, L in enumerate(w.layers):
-            kc, vc = kv_caches[i]
-            if i == 0:
-                y, _ = ops.add_norm(h, L.ln1_w, L.ln1_b, eps, rms)
-                a = self._attention(L, y, inp, kc, vc)
-            else:
-                a = self._attention(L, h, inp, kc, vc, fold=stats[2 * i - 1])
-            ops.linear_fold(a, L.o.w, L.o.b, resid=h, wstat=stats[2 * i])
-            m = ops.linear_fold(h, L.up.w, L.up.b, self.act, L.up.glu, rstat=stats[2 * i], c1=L.up.c1, eps=eps)
-            ops.linear_fold(m, L.down.w, L.down.b, resid=h, wstat=stats[2 * i + 1])
-        y, _ = ops.add_norm(h, w.lnf_w, w.lnf_b, eps, rms)
-        return y
 
     @property
     def device(self):
@@ -215,7 +144,7 @@ class DecoderLM:
                  torch.zeros(shp, dtype=dt, device=self.device)) for _ in range(self.cfg.num_layers)]
 
     # ---------------------------------------------------------------------------- forward
-    def _qkv_rope_cache(self, L, y, inp: StepInput, kc, vc, fold=None):
+    def _qkv_rope_cache(self, L, y, inp: StepInput, kc, vc):
         """QKV projection, RoPE and the paged KV write of the step's tokens -> the bf16 qkv rows.
 
         Where the autotuner found it faster (a kind-3 plan for this M, ops/autotune.py tune_qkv_epilogue)
@@ -223,30 +152,20 @@ class DecoderLM:
         GEMM (split-K slabs allowed) followed by the rope_cache kernel, which sums the slabs itself."""
         cfg, p = self.cfg, self.plan
         do_rope = cfg.position == "rope"
-        fk = dict(rstat=fold, c1=L.qkv.c1, eps=cfg.norm_eps) if fold is not None else {}
         if y.is_cuda and self.qkv_epi and not self.kv_fp8 and L.qkv.w.dim() == 2 and L.qkv.w_scale is None \
                 and _hip_ops().lib().gemm_tuned_get(y.shape[0], L.qkv.N, L.qkv.K, False, 3) is not None:
             out = _hip_ops().linear_qkv(y, L.qkv.w, L.qkv.b, inp.positions, self.w.cos, self.w.sin, kc, vc, inp.slots,
-                                        p.nh_l, p.nkv_l, cfg.head_dim, cfg.rotary_dim, cfg.rope_style, do_rope, **fk)
+                                        p.nh_l, p.nkv_l, cfg.head_dim, cfg.rotary_dim, cfg.rope_style, do_rope)
             if out is not None:
                 return out
-        qkv = ops.linear_fold(y, L.qkv.w, L.qkv.b, **fk) if fold is not None else L.qkv(y, partial_ok=True)
+        qkv = L.qkv(y, partial_ok=True)
         return ops.rope_cache(qkv, inp.positions, self.w.cos, self.w.sin, kc, vc, inp.slots,
                               p.nh_l, p.nkv_l, cfg.head_dim, cfg.rotary_dim, cfg.rope_style, do_rope=do_rope)
 
-    def _attention(self, L, y, inp: StepInput, kc, vc, fold=None):
-        """``fold``: ``y`` is the raw residual stream and ``fold`` its row statistics (norm fold)."""
+    def _attention(self, L, y, inp: StepInput, kc, vc):
         cfg, p = self.cfg, self.plan
         D = cfg.head_dim
-        do_rope = cfg.position == "rope"
-        if fold is None and inp.kind == "decode" and y.is_cuda and self.fused_decode and not self.kv_fp8 and \
-                _hip_ops().fused_decode_ok(D, cfg.rotary_dim, cfg.rope_style, do_rope):
-            # one launch: RoPE + paged KV write of the new token + attention (no rope_cache kernel)
-            return _hip_ops().attn_decode_fused(
-                L.qkv(y, partial_ok=True), inp.positions, self.w.cos, self.w.sin, kc, vc, inp.slots,
-                inp.block_tables, inp.ctx_lens, p.nh_l, p.nkv_l, D, cfg.rotary_dim, cfg.rope_style, self.scale,
-                inp.max_ctx, do_rope=do_rope, splits=inp.decode_splits)
-        qkv = self._qkv_rope_cache(L, y, inp, kc, vc, fold)
+        qkv = self._qkv_rope_cache(L, y, inp, kc, vc)
         if inp.kind == "decode" and qkv.is_cuda and qkv.shape[0] in self.gqa_mfma:
             B = qkv.shape[0]
             return ops.attn_extend(qkv, kc, vc, inp.block_tables, self.decode_cu(B, qkv.device), inp.ctx_lens, 1,
@@ -397,10 +316,8 @@ class DecoderLM:
         cur = torch.cuda.current_stream() if on_gpu else None
         comm = self._comm(inp.input_ids.device) if on_gpu else None
 
-        diag = os.environ.get("LLMSS_TBO_DIAG", "")
-
         def reduce(t):  # all-reduce t on the comm stream; returns the event to wait on before reading t
-            if not on_gpu or diag == "onestream":
+            if not on_gpu:
                 self.tp.all_reduce(t)
                 return None
             comm.wait_stream(cur)
@@ -493,8 +410,6 @@ class DecoderLM:
             sp = self.prefill_split(inp)
             if sp is not None:
                 return self._hidden_states_overlap(inp, kv_caches, sp[1], subs=self._sub_prefill(inp, *sp))
-        if inp.kind == "decode" and self.norm_fold:
-            return self._hidden_states_folded(inp, kv_caches)
         cfg, w = self.cfg, self.w
         eps, rms = cfg.norm_eps, self.rms
         x = ops.embed(inp.input_ids, w.wte, inp.positions if w.wpe is not None else None, w.wpe)

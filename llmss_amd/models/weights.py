@@ -77,8 +77,6 @@ class Linear:
     w_scale: Optional[torch.Tensor] = None
     glu: bool = False
     k: int = 0
-    # norm fold (models/decoder.py fold_norms): fp32 row sums of the folded weight, the LayerNorm mean correction
-    c1: Optional[torch.Tensor] = None
 
     def __call__(self, x, act="none", partial_ok=False):
         return ops.linear(x, self.w, self.b, act, self.glu, self.w_scale, partial_ok=partial_ok)

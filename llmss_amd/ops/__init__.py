@@ -85,14 +85,6 @@ def linear(x, w, bias=None, act="none", glu=False, w_scale: Optional[torch.Tenso
     return ref.linear(x, w, bias, act, glu, w_scale)
 
 
-def linear_fold(x, w, bias=None, act="none", glu=False, rstat=None, c1=None, eps=0.0, resid=None, wstat=None):
-    """Norm-fold GEMM: consumer (rstat / c1: finishes the folded norm) or producer (resid += x @ w^T + bias
-    in place, row statistics into wstat). Semantics: ops/reference.py linear_fold."""
-    if x.is_cuda:
-        return _hip().linear_fold(x, w, bias, act, glu, rstat, c1, eps, resid, wstat)
-    return ref.linear_fold(x, w, bias, act, glu, rstat, c1, eps, resid, wstat)
-
-
 def sample(logits, temperature, top_k, top_p, seeds, vocab=None):
     if logits.is_cuda:
         return _hip().sample(logits, temperature, top_k, top_p, seeds, vocab)

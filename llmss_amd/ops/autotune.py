@@ -307,89 +307,8 @@ def _reinstall_qkv(lib, model, results):
             lib.gemm_tuned_set(M, L.qkv.N, L.qkv.K, False, 3, plan[0], plan[1])
 
 
-def fold_candidates(M: int, N: int, K: int, glu: bool) -> List[Tuple[int, int]]:
-    """(nt_hint, split) plans for the norm-fold epilogues (LDS-staged, finished sums): tiled / gemm_mid tiles,
-    unsplit or split-K combined in-launch."""
-    tiles = [(3, (16, 32)), (2, (16, 32)), (11, (16, 32)), (10, (16,)), (13, (16, 32)), (14, (32,)), (15, (16,)), (7, (32,))]
-    if M > 64:
-        tiles += [(1, (0, 16)), (8, (16,)), (12, (16,))]
-    if M >= 256:
-        tiles += [(9, (0,))]
-    nk = -(-K // 64)
-    out = []
-    for t, depths in tiles:
-        for d in depths:
-            out += [((t | d | (256 if s > 1 else 0)) << 8, s) for s in (1, 2, 3, 4, 5, 6, 8)
-                    if s == 1 or nk // s >= 2]
-    return out
-
-
-_FOLD_DONE: Dict[tuple, Tuple[int, int, float, float]] = {}
-
-
-def tune_fold(model, ms: Sequence[int], native=None, iters: int = 16) -> Dict[Tuple[str, int], Tuple[int, int, float, float]]:
-    """Plans of the norm-fold GEMMs (models/decoder.py fold_norms) per decode bucket: kind 4 (consumer: QKV
-    without the RoPE epilogue, up) and kind 5 (producer: o, down), timed with HBM-cold weights like tune_shape."""
-    from .. import _native
-    from . import hip as H
-
-    lib = native or _native()
-    dev = model.device
-    L = model.w.layers[0]
-    res = {}
-    for name, lin, kind in (("qkv", L.qkv, 4), ("up", L.up, 4), ("o", L.o, 5), ("down", L.down, 5)):
-        N, K, glu = lin.N, lin.K, lin.glu
-        act = model.act if name == "up" and not glu else "none"
-        for M in sorted(set(int(m) for m in ms)):
-            key = (M, N, K, glu, act, kind, str(dev))
-            if key not in _FOLD_DONE:
-                ncopy = max(2, min(64, math.ceil((600 << 20) / (N * K * 2))))
-                g = torch.Generator(device=dev)
-                g.manual_seed(99)
-                base = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(torch.bfloat16)
-                ws = [base.clone() for _ in range(ncopy)]
-                x = (torch.randn(M, K, device=dev, generator=g) * 0.5).to(torch.bfloat16)
-                st = torch.stack([x.float().sum(1), x.float().pow(2).sum(1)], 1).contiguous()
-                c1 = base.float().sum(1) if lin.c1 is not None else None
-                hres = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
-                wst = torch.zeros(M, 2, device=dev)
-
-                def fn(nt, s):
-                    def f(i):
-                        if kind == 5:
-                            H.linear_fold(x, ws[i % ncopy], lin.b, resid=hres, wstat=wst, nt_hint=nt, split_hint=s)
-                        else:
-                            H.linear_fold(x, ws[i % ncopy], lin.b, act, glu, rstat=st, c1=c1, eps=1e-5, nt_hint=nt,
-                                          split_hint=s)
-                    return f
-
-                best = (0, 0, float("inf"))
-                default = None
-                for nt, s in [(0, 0)] + fold_candidates(M, N, K, glu):
-                    try:
-                        f = fn(nt, s)
-                        f(0)
-                        torch.cuda.synchronize(dev)
-                        t = _time(f, iters)
-                    except (RuntimeError, ValueError):
-                        continue
-                    if default is None:
-                        default = t
-                    if t < best[2]:
-                        best = (nt, s, t)
-                del ws
-                _FOLD_DONE[key] = (best[0], best[1], best[2], default if default is not None else best[2])
-            nt, s, t, t0_us = _FOLD_DONE[key]
-            if nt:
-                lib.gemm_tuned_set(M, N, K, glu, kind, nt, s)
-            res[(f"fold_{name}", M)] = (nt, s, t, t0_us)
-    log.info("norm-fold GEMMs: %s", ", ".join(f"{k[0]}@{k[1]} {v[2]:.1f}us" for k, v in res.items()))
-    return res
-
-
 def tune_model(model, ms: Sequence[int], native=None) -> Dict[Tuple[str, int], Tuple[int, int, float, float]]:
-    """Tune every (shape, M) pair and install the winners in the native plan table. A norm-folded model
-    (decode runs the fold GEMMs) tunes its fold plans instead of the plain decode plans of its projections."""
+    """Tune every (shape, M) pair and install the winners in the native plan table."""
     from .. import _native
 
     lib = native or _native()
@@ -397,10 +316,7 @@ def tune_model(model, ms: Sequence[int], native=None) -> Dict[Tuple[str, int], T
     t0 = time.perf_counter()
     res = {}
     done = _DONE
-    folded = getattr(model, "norm_fold", False)
     for name, shp in model_shapes(model).items():
-        if folded and name != "head":
-            continue
         for M in sorted(set(int(m) for m in ms)):
             key = (M, shp, str(dev))
             if key not in done:
@@ -418,8 +334,6 @@ def tune_model(model, ms: Sequence[int], native=None) -> Dict[Tuple[str, int], T
             _reinstall_qkv(lib, model, _QKV_DONE[key])
         for M, (u, f) in _QKV_DONE[key].items():
             res[("qkv_epi", M)] = (0, 0, min(u, f), u)
-    if folded:
-        res.update(tune_fold(model, ms, lib))
     torch.cuda.synchronize(dev)
     gain = sum(v[3] - v[2] for v in res.values())
     log.info("autotuned %d GEMM shapes in %.1fs (sum of per-call gains %.1f us)", len(res),

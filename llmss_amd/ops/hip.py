@@ -312,61 +312,6 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale, 
     return y
 
 
-def fused_decode_ok(D: int, rot: int, style: str, do_rope: bool) -> bool:
-    """Whether attn_decode_fused supports this rotary setup (neox partners need a power-of-two lane stride)."""
-    if D not in (64, 128, 256):
-        return False
-    if not do_rope or rot == 0:
-        return True
-    if style == "gptj":
-        return rot % 8 == 0 and rot <= D
-    return rot >= 16 and rot <= D and (rot & (rot - 1)) == 0
-
-
-def attn_decode_fused(qkv, positions, cos, sin, k_cache, v_cache, slots, block_tables, ctx_lens, nh, nkv, D, rot,
-                      style, scale, max_ctx, do_rope=True, out=None, splits=None):
-    """Decode attention with the new token's RoPE + paged KV-cache write fused in (replaces rope_cache +
-    attn_decode). ``qkv`` = the QKV GEMM output [B, (nh+2nkv)*D] or its split-K :class:`PartialSum`."""
-    part = qkv if isinstance(qkv, PartialSum) else None
-    N = (nh + 2 * nkv) * D
-    if part is not None:
-        _check(part.N == N, "partial qkv width")
-        B = part.M
-        qptr, qstride = 0, N
-    else:
-        _bf16_rows(qkv, "qkv")
-        _check(qkv.shape[1] >= N, "qkv too narrow")
-        B = qkv.shape[0]
-        qptr, qstride = qkv.data_ptr(), qkv.stride(0)
-    _check(fused_decode_ok(D, rot, style, do_rope), "unsupported head_dim / rotary setup for the fused path")
-    rot = rot if do_rope else 0
-    if rot:
-        _check(cos.dtype == torch.float32 and cos.is_contiguous() and cos.shape[1] == rot // 2, "cos table")
-        _check(sin.shape == cos.shape and sin.is_contiguous(), "sin table")
-    _check(positions.dtype == torch.int64 and positions.numel() >= B and positions.is_contiguous(), "positions")
-    _check(slots.dtype == torch.int64 and slots.numel() >= B and slots.is_contiguous(), "slots")
-    _check(k_cache.dtype == torch.bfloat16 and k_cache.is_contiguous() and k_cache.shape[1] == nkv
-           and k_cache.shape[3] == D, "k_cache [nb, nkv, bs, D]")
-    _check(v_cache.shape == k_cache.shape and v_cache.is_contiguous(), "v_cache")
-    _check(block_tables.dtype == torch.int32 and block_tables.dim() == 2 and block_tables.shape[0] >= B
-           and block_tables.stride(1) == 1, "block_tables int32 [B, maxb]")
-    _check(ctx_lens.dtype == torch.int32 and ctx_lens.numel() >= B and ctx_lens.is_contiguous(), "ctx_lens int32")
-    bs = k_cache.shape[2]
-    _check(block_tables.shape[1] * bs >= max_ctx, "block table too short for max_ctx")
-    nsplit, psize = splits if splits is not None else decode_splits(B, nkv, max_ctx, bs)
-    _check(nsplit * psize >= max_ctx, "splits do not cover max_ctx")
-    y = out if out is not None else torch.empty(B, nh * D, dtype=torch.bfloat16, device=k_cache.device)
-    po, pml = _DECODE_WS.get(B, nh, nsplit, D, k_cache.device) if nsplit > 1 else (None, None)
-    lib().attn_decode_fused(qptr, qstride, part.buf.data_ptr() if part else 0, part.S if part else 0,
-                            part.M * part.N if part else 0, _ptr(part.bias) if part else 0, N, positions.data_ptr(),
-                            _ptr(cos) if rot else 0, _ptr(sin) if rot else 0, slots.data_ptr(), int(rot),
-                            1 if style == "gptj" else 0, nh * D, (nh + nkv) * D, k_cache.data_ptr(),
-                            v_cache.data_ptr(), block_tables.data_ptr(), block_tables.stride(0), ctx_lens.data_ptr(),
-                            y.data_ptr(), y.stride(0), _ptr(po), _ptr(pml), B, nh, nkv, D, bs, nsplit, psize,
-                            float(scale), _stream())
-    return y
-
-
 # ------------------------------------------------------------------------------------- GEMM
 class GemmWorkspace:
     def __init__(self):
@@ -623,53 +568,8 @@ def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hi
     return y
 
 
-def _fold_args(x, rstat, c1, eps, N):
-    """Validated (rstat ptr, c1 ptr, 1 / K, eps) of a norm-fold consumer (ops/reference.py linear_fold)."""
-    if rstat is None:
-        return 0, 0, 0.0, 0.0
-    M, K = x.shape
-    _check(rstat.dtype == torch.float32 and rstat.is_contiguous() and rstat.shape == (M, 2), "rstat [M, 2] fp32")
-    if c1 is not None:
-        _check(c1.dtype == torch.float32 and c1.is_contiguous() and c1.numel() == N, "c1 [N] fp32")
-    return rstat.data_ptr(), _ptr(c1), 1.0 / K, float(eps)
-
-
-def linear_fold(x, w, bias=None, act="none", glu=False, rstat=None, c1=None, eps=0.0, resid=None, wstat=None,
-                nt_hint=0, split_hint=0):
-    """Norm-fold GEMM (csrc/gemm.hip launch_gemm_epi; semantics: ops/reference.py linear_fold). Consumer:
-    ``rstat`` [M, 2] row statistics of ``x`` (the raw residual stream), ``c1`` the LayerNorm mean correction
-    (None for RMSNorm) -> new bf16 output. Producer: ``resid`` [M, N] updated in place (+= x @ w^T + bias) and
-    its new row statistics added into ``wstat`` [M, 2]. Tuned kinds 4 / 5 (ops/autotune.py tune_fold)."""
-    M, K = x.shape
-    _bf16_rows(x, "x")
-    _bf16_rows(w, "w")
-    _check(w.dim() == 2 and w.is_contiguous() and w.shape[1] == K, "fold weights are bf16 [N, K]")
-    N = w.shape[0]
-    _check(K % 16 == 0, "K must be a multiple of 16")
-    if bias is not None:
-        _check(bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.numel() == N, "bias [N] bf16")
-    ws = _GEMM_WS.get(64 << 20, x.device)
-    if resid is not None:
-        _check(rstat is None and not glu and act in ("none", None), "the producer takes no consumer epilogue")
-        _check(resid.dtype == torch.bfloat16 and resid.shape == (M, N) and resid.stride(1) == 1, "resid [M, N] bf16")
-        _check(wstat is not None and wstat.dtype == torch.float32 and wstat.is_contiguous()
-               and wstat.shape == (M, 2), "wstat [M, 2] fp32")
-        y, rs, c1p, inv_k, ep, wsp = resid, 0, 0, 0.0, 0.0, wstat.data_ptr()
-    else:
-        _check(rstat is not None, "fold consumer needs rstat")
-        if glu:
-            _check(N % 32 == 0, "glu needs N % 32 == 0")
-        y = torch.empty(M, N // 2 if glu else N, dtype=x.dtype, device=x.device)
-        rs, c1p, inv_k, ep = _fold_args(x, rstat, c1, eps, N)
-        wsp = 0
-    lib().gemm_fold(x.data_ptr(), x.stride(0), w.data_ptr(), K, _ptr(bias), y.data_ptr(), y.stride(0), M, N, K,
-                    _ACT[act], bool(glu), ws.data_ptr(), ws.numel() * 4, int(nt_hint), int(split_hint), rs, c1p,
-                    inv_k, ep, wsp, _stream())
-    return y
-
-
 def linear_qkv(x, w, bias, positions, cos, sin, k_cache, v_cache, slots, nh, nkv, D, rot, style, do_rope=True,
-               nt_hint=0, split_hint=0, rstat=None, c1=None, eps=0.0):
+               nt_hint=0, split_hint=0):
     """QKV projection whose GEMM epilogue applies RoPE and writes k / v into the paged cache (one launch
     instead of GEMM + rope_cache; same values). Returns the bf16 [T, N] qkv tensor, or None when this
     weight / cache / plan cannot take the fused epilogue (packed or fp8 weights, fp8 KV rows, streaming or
@@ -689,7 +589,6 @@ def linear_qkv(x, w, bias, positions, cos, sin, k_cache, v_cache, slots, nh, nkv
     if do_rope:
         _check(cos.dtype == torch.float32 and cos.is_contiguous() and cos.shape[1] == rot // 2, "cos table")
         _check(sin.shape == cos.shape and sin.is_contiguous(), "sin table")
-    rs, c1p, inv_k, ep = _fold_args(x, rstat, c1, eps, N)
     bs = 1
     if k_cache is not None:
         _kv_cache_check(k_cache, v_cache, nkv, D)
@@ -702,7 +601,7 @@ def linear_qkv(x, w, bias, positions, cos, sin, k_cache, v_cache, slots, nh, nkv
                         ws.data_ptr(), ws.numel() * 4, int(nt_hint), int(split_hint), positions.data_ptr(),
                         _ptr(cos) if do_rope else 0, _ptr(sin) if do_rope else 0, _ptr(k_cache), _ptr(v_cache),
                         _ptr(slots) if k_cache is not None else 0, nh, nkv, D, rot, bs, 1 if style == "gptj" else 0,
-                        do_rope, _stream(), rs, c1p, inv_k, ep)
+                        do_rope, _stream())
     return y if rc == 0 else None
 
 

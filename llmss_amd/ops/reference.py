@@ -292,54 +292,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act: str = "none", glu: 
     return y.to(x.dtype)
 
 
-def fold_norm_into(w: torch.Tensor, bias, norm_w, norm_b, layernorm: bool):
-    """Norm fold of a linear that consumes norm(h) (models/decoder.py "norm fold"): returns (w', c0, c1) with
-    w' = w * norm_w along K (bf16), c0 = w @ norm_b + bias (the new bias, or None) and, for LayerNorm,
-    c1 = row sums of w' in fp32 (the mean correction). Then  linear(norm(h)) = rstd * (w' h - mean * c1) + c0."""
-    wf = w.float()
-    c0 = wf @ norm_b.float() if norm_b is not None else None
-    if bias is not None:
-        c0 = bias.float() if c0 is None else c0 + bias.float()
-    wq = (wf * norm_w.float()[None, :]).to(w.dtype)
-    c1 = wq.float().sum(1) if layernorm else None
-    return wq, (c0.to(w.dtype) if c0 is not None else None), c1
-
-
-def linear_fold(x, w, bias=None, act: str = "none", glu: bool = False, rstat=None, c1=None, eps: float = 0.0,
-                resid=None, wstat=None):
-    """CPU definition of the norm-fold GEMM epilogues (csrc/common.h QkvEpi, gemm.hip launch_gemm_epi).
-
-    consumer (rstat [M, 2] = per-row (sum, sum of squares) of x over its K columns): the tile is finished as
-    rstd * acc - rstd * mean * c1 (mean = 0 for RMSNorm, c1 None) before bias / activation / SwiGLU;
-    producer (resid [M, N] bf16 and wstat [M, 2] fp32): resid += x @ w^T + bias in place (one bf16 rounding)
-    and wstat += the new rows' (sum, sum of squares). Returns the consumer output / the updated resid."""
-    acc = x.float() @ w.float().t()
-    if resid is not None:
-        y = acc + resid.float()
-        if bias is not None:
-            y = y + bias.float()
-        out = y.to(resid.dtype)
-        resid.copy_(out)
-        of = out.float()
-        wstat[:, 0] += of.sum(1)
-        wstat[:, 1] += of.pow(2).sum(1)
-        return resid
-    K = x.shape[1]
-    mean = rstat[:, 0] / K if c1 is not None else torch.zeros_like(rstat[:, 0])
-    rs = torch.rsqrt((rstat[:, 1] / K - mean * mean).clamp_min(0) + eps)
-    y = rs[:, None] * acc
-    if c1 is not None:
-        y = y - (rs * mean)[:, None] * c1.float()[None, :]
-    if bias is not None:
-        y = y + bias.float()
-    if glu:
-        g, u = glu_split(y, -1)
-        y = F.silu(g) * u
-    else:
-        y = _act(y, act)
-    return y.to(x.dtype)
-
-
 def quant_fp8_rows(w: torch.Tensor):
     wf = w.float()
     amax = wf.abs().amax(dim=1).clamp_min(0)

@@ -80,12 +80,6 @@ class TPGroup:
             self._cycles_per_us = 2_000_000 / (s.elapsed_time(e) * 1e3)
         lat, gbps = self.sim_comm
         us = lat + nbytes / (gbps * 1e3)
-        if os.environ.get("LLMSS_SIM_COMM_OP") == "touch":  # diagnostic: a tiny real kernel instead of a spin
-            self._touch = getattr(self, "_touch", None)
-            if self._touch is None:
-                self._touch = torch.zeros(64, device="cuda")
-            self._touch.add_(1.0)
-            return
         torch.cuda._sleep(max(1, int(us * self._cycles_per_us)))
 
     @property

@@ -147,3 +147,54 @@ def test_decode_overlap_ab_at_capture(comm, monkeypatch):
     del e
     e2 = LLMEngine(m, max_num_seqs=24, block_size=16, use_graphs=False, autotune=False)
     assert e2.generate(prompts, sp) == out_g
+
+
+def _graph_node_types(g):
+    """Types of the nodes of a captured torch CUDAGraph (keep_graph=True), read with hipGraphGetNodes."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    graph = ctypes.c_void_p(g.raw_cuda_graph())
+    n = ctypes.c_size_t(0)
+    assert hip.hipGraphGetNodes(graph, None, ctypes.byref(n)) == 0
+    nodes = (ctypes.c_void_p * max(1, n.value))()
+    assert hip.hipGraphGetNodes(graph, nodes, ctypes.byref(n)) == 0
+    types = []
+    for i in range(n.value):
+        t = ctypes.c_int(-1)
+        assert hip.hipGraphNodeGetType(ctypes.c_void_p(nodes[i]), ctypes.byref(t)) == 0
+        types.append(t.value)
+    return types
+
+
+def test_captured_collectives_are_graph_nodes(comm):
+    """'capture succeeded' is not the check. Out-of-place all-gather / all-reduce /
+    reduce-scatter on the native communicator captured into one graph leave one node each (a one-rank
+    collective is a device copy: memcpy or kernel nodes, never an empty graph), and the replay moves the
+    CURRENT inputs."""
+    xs = [torch.zeros(4096, dtype=dt, device="cuda") for dt in (torch.bfloat16, torch.float32, torch.bfloat16)]
+    outs = [torch.empty_like(x) for x in xs]
+    ops = [lambda: comm.all_gather(xs[0].data_ptr(), outs[0].data_ptr(), xs[0].numel(), _code(xs[0]), _st()),
+           lambda: comm.all_reduce(xs[1].data_ptr(), outs[1].data_ptr(), xs[1].numel(), _code(xs[1]), _st()),
+           lambda: comm.reduce_scatter(xs[2].data_ptr(), outs[2].data_ptr(), xs[2].numel(), _code(xs[2]), _st())]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for op in ops:
+            op()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        for op in ops:
+            op()
+    types = _graph_node_types(g)
+    # hipGraphNodeType: 0 kernel, 1 memcpy, 2 memset, 5 empty; one-rank collectives copy
+    assert len([t for t in types if t in (0, 1)]) >= len(ops), types
+    g.instantiate()
+    for v in (3.0, 7.0):
+        for x in xs:
+            x.fill_(v)
+        g.replay()
+        torch.cuda.synchronize()
+        assert all(bool((o == v).all()) for o in outs)

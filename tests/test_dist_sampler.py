@@ -96,31 +96,6 @@ def test_gpu_sharded_candidates_one_gpu(shards, V, Vp):
 
 
 @pytest.mark.gpu
-def test_gpu_engine_sharded_candidates_match_v3(monkeypatch):
-    """A TP=1 engine sampling through vocabulary-sharded candidates (LLMSS_CAND_SHARDS) generates exactly the
-    tokens of the one-kernel v3 sampler engine - greedy and seeded top-k / top-p rows, inside decode graphs."""
-    from llmss_amd.engine import LLMEngine, SamplingParams
-    from llmss_amd.models.config import get_preset
-    from llmss_amd.models.decoder import DecoderLM
-    from llmss_amd.models.weights import random_weights
-
-    cfg = get_preset("tiny-llama", hidden_size=256, num_heads=4, num_kv_heads=2, head_dim=64, rotary_dim=64,
-                     intermediate_size=512, max_position_embeddings=256, vocab_size=5000)
-    m = DecoderLM(cfg, random_weights(cfg, device="cuda", dtype=torch.bfloat16, seed=9, std=0.08))
-    prompts = [[(7 * i + 3 * j) % 5000 for j in range(5 + 3 * i)] for i in range(6)]
-    sps = [SamplingParams(max_new_tokens=12, temperature=0.8 if i % 2 else 0.0, top_k=(10, 40, 64)[i % 3],
-                          top_p=0.9, seed=100 + i, ignore_eos=True) for i in range(len(prompts))]
-    outs = []
-    for shards in ("0", "8"):
-        monkeypatch.setenv("LLMSS_CAND_SHARDS", shards)
-        eng = LLMEngine(m, max_num_seqs=8, block_size=16, use_graphs=True, autotune=False)
-        assert eng.dist_sampling == (shards == "8")
-        outs.append(eng.generate(prompts, sps))
-        del eng
-    assert outs[0] == outs[1]
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("tp", [2, 8])
 def test_gpu_candidates_tie_mass_above_kc(tp):
     """more than KC = 128 logits of a shard tie at the top-k boundary. The candidate kernel keeps the

@@ -420,34 +420,6 @@ def test_fp8_norm_twin_matches_separate_quantisation():
     assert torch.equal(got, ref)
 
 
-@pytest.mark.parametrize("name", ["tiny-gpt2", "tiny-llama"])
-def test_norm_fold_decode_matches_reference(name):
-    """Norm-folded decode (opt-in LLMSS_NORM_FOLD=1: o / down add into the residual stream and accumulate row
-    statistics, QKV / up finish the norm in their epilogues) vs the unfolded CPU fp32 forward."""
-    over = dict(head_dim=64, hidden_size=256, num_heads=4, num_kv_heads=4 if name != "tiny-llama" else 2,
-                rotary_dim=64 if name == "tiny-llama" else 0)
-    cfg = get_preset(name, **over)
-    wc = random_weights(cfg, device="cpu", dtype=torch.float32, seed=1, std=0.05)
-    m_cpu = DecoderLM(cfg, wc)
-    m_gpu = DecoderLM(cfg, _to_gpu(wc), norm_fold=True)
-    assert m_gpu.norm_fold and not m_cpu.norm_fold
-    V, T = cfg.vocab_size, 25
-    ids = torch.randint(0, V, (2 * T,))
-    cu = torch.tensor([0, T, 2 * T], dtype=torch.int32)
-    pos = torch.cat([torch.arange(T), torch.arange(T)])
-    kv_c, kv_g = m_cpu.allocate_kv_cache(16, 16), m_gpu.allocate_kv_cache(16, 16)
-    slots = torch.cat([torch.arange(T), 32 + torch.arange(T)])
-    pre = dict(kind="prefill", input_ids=ids, positions=pos, slots=slots, cu_seqlens=cu, max_seqlen=T)
-    m_cpu(StepInput(**pre), kv_c)
-    m_gpu(StepInput(**{k: (v.cuda() if torch.is_tensor(v) else v) for k, v in pre.items()}), kv_g)
-    d_in = dict(kind="decode", input_ids=torch.randint(0, V, (2,)), positions=torch.tensor([T, T]),
-                slots=torch.tensor([T, 32 + T]), block_tables=torch.tensor([[0, 1], [2, 3]], dtype=torch.int32),
-                ctx_lens=torch.tensor([T + 1, T + 1], dtype=torch.int32), max_ctx=32)
-    ref = m_cpu(StepInput(**d_in), kv_c)
-    out = m_gpu(StepInput(**{k: (v.cuda() if torch.is_tensor(v) else v) for k, v in d_in.items()}), kv_g)
-    _assert_logits_close(out[:, :V].float().cpu(), ref[:, :V])
-
-
 def test_pipelined_decode_across_kv_block_boundaries():
     """The pipelined decode launches step t+1 before collecting step t, also when a sequence enters a new KV
     block (the block is reserved ahead of the scheduler: Scheduler.reserve). Greedy tokens equal the

@@ -487,46 +487,6 @@ def test_sample_kept_set_exact(V, k, p, temp):
             assert seen[b] == sets[b]
 
 
-@pytest.mark.parametrize("style,D,rot,nh,nkv", [("neox", 128, 128, 8, 2), ("gptj", 256, 64, 4, 4), ("neox", 64, 32, 4, 1),
-                                               ("none", 64, 0, 8, 8)])
-@pytest.mark.parametrize("partial", [False, True])
-def test_attn_decode_fused_rope(style, D, rot, nh, nkv, partial):
-    """Fused decode (RoPE + KV write of the new token + attention) == rope_cache followed by attn_decode."""
-    torch.manual_seed(0)
-    B, bs, maxctx = 5, 16, 300
-    maxb = (maxctx + bs - 1) // bs
-    nb = B * maxb + 2
-    kc, vc = rnd(nb, nkv, bs, D), rnd(nb, nkv, bs, D)
-    bt = torch.randperm(nb, device=dev)[: B * maxb].view(B, maxb).to(torch.int32)
-    ctx = torch.tensor([1, 17, 300, 64, 0], dtype=torch.int32, device=dev)  # row 4 = padding (ctx 0, slot -1)
-    pos = (ctx.long() - 1).clamp(min=0)
-    slots = torch.tensor([int(bt[b, int(pos[b]) // bs]) * bs + int(pos[b]) % bs for b in range(B)], device=dev)
-    slots[4] = -1
-    N = (nh + 2 * nkv) * D
-    if partial:
-        K = 512
-        x, w, bias = rnd(B, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
-        src = H.linear(x, w, bias, partial_ok=True, split_hint=4)
-        qkv = H.linear(x, w, bias)
-    else:
-        qkv = rnd(B, N)
-        src = qkv
-    do_rope = style != "none"
-    sty = "neox" if style == "none" else style
-    cos, sin = R.rope_tables(512, max(rot, 8), 10000.0, dev)
-    sc = 1 / math.sqrt(D)
-    k1, v1 = kc.clone(), vc.clone()
-    out = H.attn_decode_fused(src, pos, cos, sin, k1, v1, slots, bt, ctx, nh, nkv, D, rot, sty, sc, maxctx,
-                              do_rope=do_rope)
-    k2, v2, q2 = kc.clone(), vc.clone(), qkv.clone()
-    H.rope_cache(q2, pos, cos, sin, k2, v2, slots, nh, nkv, D, rot, sty, do_rope=do_rope)
-    ref = H.attn_decode(q2, k2, v2, bt, ctx, nh, nkv, D, sc, maxctx)
-    close(out[:4], ref[:4], 2e-2)
-    assert bool((out[4] == 0).all())
-    close(k1, k2, 2e-2)
-    close(v1, v2, 1e-2)
-
-
 @pytest.mark.parametrize("tile,stages", [(1, 2), (1, 3), (2, 2), (2, 4), (3, 3), (3, 4)])
 @pytest.mark.parametrize("per_cu", [1, 2, 3])
 @pytest.mark.parametrize("M,N,K", [(512, 1536, 4096), (300, 2752, 1376), (64, 4096, 11008), (130, 544, 208)])
@@ -655,91 +615,6 @@ def test_w8a8_decode_plan_in_graph(M):
 def _row_stats(h):
     hf = h.float()
     return torch.stack([hf.sum(1), hf.pow(2).sum(1)], 1).contiguous()
-
-
-@pytest.mark.parametrize("tile,split", [(0, 0), (3, 1), (3, 4), (2, 2), (11, 1), (11, 3), (10, 2), (1, 1), (8, 2),
-                                        (9, 1), (12, 2), (13, 1), (13, 5), (14, 1), (14, 2), (15, 1), (7, 1), (7, 3)])
-@pytest.mark.parametrize("M", [1, 37, 64, 200])
-@pytest.mark.parametrize("mode", ["rms", "ln_gelu", "rms_glu"])
-def test_gemm_norm_fold_consumer(tile, split, M, mode):
-    """Norm-fold consumer epilogue (rstd * acc - rstd * mean * c1, then bias / GELU / SwiGLU) on every tile and
-    split (a split runs as an in-launch combine) vs the fp32 oracle ops/reference.py linear_fold; the same value
-    as the unfolded add_norm + GEMM up to bf16 rounding."""
-    torch.manual_seed(0)
-    K, N = 1600, 1024
-    h = rnd(M, K, scale=2.0) + 0.3
-    w = rnd(N, K, scale=K ** -0.5)
-    b = rnd(N, scale=0.1) if mode != "rms" else None
-    ln = mode.startswith("ln")
-    glu = mode.endswith("glu")
-    if glu and tile in ODD_NT_TILES:
-        pytest.skip("SwiGLU needs an even number of 16-column tiles per wave")
-    act = "gelu_tanh" if mode == "ln_gelu" else "none"
-    c1 = w.float().sum(1).contiguous() if ln else None
-    rst = _row_stats(h)
-    d = 16 if tile not in (0, 1, 9) else 0
-    hint = (tile | d) << 8 if tile else 0
-    y = H.linear_fold(h, w, b, act, glu, rstat=rst, c1=c1, eps=1e-5, nt_hint=hint, split_hint=split)
-    y_ref = R.linear_fold(h, w, b, act, glu, rstat=rst, c1=c1, eps=1e-5)
-    close(y, y_ref, 2e-2)
-    # == explicit norm (no affine) + plain GEMM
-    xn, _ = R.add_norm(h, torch.ones(K, dtype=torch.bfloat16, device=dev),
-                       torch.zeros(K, dtype=torch.bfloat16, device=dev) if ln else None, 1e-5, not ln)
-    close(y, R.linear(xn, w, b, act, glu), 5e-2)
-
-
-@pytest.mark.parametrize("tile,split", [(0, 0), (3, 1), (3, 8), (2, 4), (11, 2), (10, 1), (1, 2), (8, 1), (12, 3),
-                                        (13, 1), (13, 3), (14, 1), (15, 2), (7, 1)])
-@pytest.mark.parametrize("M,N", [(1, 4096), (64, 4096), (64, 1600), (130, 1000), (512, 4096)])
-def test_gemm_norm_fold_producer(tile, split, M, N):
-    """Norm-fold producer epilogue: h += x @ w^T + bias in place and the new rows' (sum, sum^2) added into
-    wstat by fp32 atomics (pre-filled wstat: accumulation, not overwrite)."""
-    torch.manual_seed(0)
-    K = 1024
-    x, w, b = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
-    h = rnd(M, N)
-    ws = torch.rand(M, 2, device=dev)
-    h_ref, ws_ref = h.clone(), ws.clone()
-    d = 16 if tile not in (0, 1, 9) else 0
-    hint = (tile | d) << 8 if tile else 0
-    H.linear_fold(x, w, b, resid=h, wstat=ws, nt_hint=hint, split_hint=split)
-    R.linear_fold(x, w, b, resid=h_ref, wstat=ws_ref)
-    close(h, h_ref, 2e-2)
-    # the sums are over the kernel's own bf16 outputs: compare with the stats of what it wrote
-    close(ws, ws_ref - _row_stats(h_ref) + _row_stats(h), 1e-3, 1e-4)
-    close(ws, ws_ref, 1e-1, 2e-2)
-
-
-@pytest.mark.parametrize("style,D,rot,nh,nkv", [("neox", 128, 128, 8, 2), ("none", 64, 0, 6, 6)])
-@pytest.mark.parametrize("ln", [False, True])
-@pytest.mark.parametrize("tile,split", [(3, 1), (11, 2), (2, 1)])
-def test_qkv_epilogue_with_norm_fold(style, D, rot, nh, nkv, ln, tile, split):
-    """QKV GEMM with RoPE + KV write AND the norm-fold consumer epilogue == norm (no affine) + QKV epilogue."""
-    torch.manual_seed(0)
-    K, T, bs, nb = 512, 40, 16, 8
-    N = (nh + 2 * nkv) * D
-    h, w = rnd(T, K, scale=1.5) + 0.2, rnd(N, K, scale=K ** -0.5)
-    b = rnd(N, scale=0.1) if ln else None
-    do_rope = style != "none"
-    pos = torch.randint(0, 120, (T,), device=dev)
-    cos, sin = R.rope_tables(128, rot if do_rope else 64, 10000.0, dev)
-    slots = torch.randperm(nb * bs, device=dev)[:T]
-    c1 = w.float().sum(1).contiguous() if ln else None
-    hint = (tile | 16) << 8
-    caches = [torch.zeros(nb, nkv, bs, D, dtype=torch.bfloat16, device=dev) for _ in range(4)]
-    y = H.linear_qkv(h, w, b, pos, cos, sin, caches[0], caches[1], slots, nh, nkv, D, rot, "neox", do_rope,
-                     nt_hint=hint, split_hint=split, rstat=_row_stats(h), c1=c1, eps=1e-5)
-    if do_rope and {3: 64, 11: 128, 2: 128}[tile] % D:  # neox partner columns must share the tile
-        assert y is None
-        return
-    assert y is not None
-    xn, _ = R.add_norm(h, torch.ones(K, dtype=torch.bfloat16, device=dev),
-                       torch.zeros(K, dtype=torch.bfloat16, device=dev) if ln else None, 1e-5, not ln)
-    y2 = H.linear_qkv(xn, w, b, pos, cos, sin, caches[2], caches[3], slots, nh, nkv, D, rot, "neox", do_rope,
-                      nt_hint=hint, split_hint=split)
-    close(y, y2, 5e-2)
-    close(caches[0], caches[2], 5e-2)
-    close(caches[1], caches[3], 5e-2)
 
 
 @pytest.mark.parametrize("variant,nt", [(1, 1), (1, 2), (2, 1), (2, 2)])

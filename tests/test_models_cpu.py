@@ -163,47 +163,3 @@ def test_rope_interleave_matches_checkpoint_order(ckpts, monkeypatch, tmp_path):
     p = str(tmp_path / "shard.safetensors")
     save_shard(w_il, p)
     assert load_shard(cfg, p, "cpu", torch.float32).rope_interleaved
-
-
-@pytest.mark.parametrize("name", FAMILIES)
-def test_norm_fold_decode_matches_hf(ckpts, name):
-    """Norm fold (DecoderLM.fold_norms): decode steps run without add_norm inside the layer stack - QKV / up
-    finish the folded norm from row statistics that o / down accumulate while adding into the residual stream
-    (ops/reference.py linear_fold). Greedy decoding stays identical to HF; GPT-J's parallel block is not folded."""
-    d, hf = ckpts[name]
-    cfg, w = _load(d)
-    m = DecoderLM(cfg, w, norm_fold=True)
-    assert m.norm_fold == (name != "gptj")
-    eng = LLMEngine(m, max_num_seqs=4, block_size=4, num_blocks=64)
-    torch.manual_seed(2)
-    prompts = [torch.randint(0, 100, (n,)) for n in (9, 3, 14)]
-    outs = eng.generate([p.tolist() for p in prompts], SamplingParams(max_new_tokens=10, is_greedy=True,
-                                                                      ignore_eos=True))
-    for p, o in zip(prompts, outs):
-        with torch.no_grad():
-            ref = hf.generate(p[None], max_new_tokens=10, do_sample=False, pad_token_id=0,
-                              eos_token_id=None)[0, len(p):].tolist()
-        assert o == ref
-
-
-@pytest.mark.parametrize("name", ["gpt2", "llama"])
-def test_norm_fold_decode_logits(ckpts, name):
-    """One decode step, folded vs unfolded model on the same checkpoint: logits agree to fp32 rounding."""
-    d, _ = ckpts[name]
-    outs = []
-    for fold in (False, True):
-        cfg, w = _load(d)
-        m = DecoderLM(cfg, w, norm_fold=fold)
-        assert m.norm_fold == fold
-        kv = m.allocate_kv_cache(16, 4)
-        torch.manual_seed(3)
-        ids = torch.randint(0, 100, (10,))
-        cu = torch.tensor([0, 6, 10], dtype=torch.int32)
-        pos = torch.cat([torch.arange(6), torch.arange(4)])
-        m(StepInput("prefill", ids, pos, torch.tensor([0, 1, 2, 3, 4, 5, 8, 9, 10, 11]), cu_seqlens=cu,
-                    max_seqlen=6, last_idx=torch.tensor([5, 9])), kv)
-        bt = torch.tensor([[0, 1], [2, 3]], dtype=torch.int32)
-        dec = StepInput("decode", torch.tensor([5, 7]), torch.tensor([6, 4]), torch.tensor([6, 12]), block_tables=bt,
-                        ctx_lens=torch.tensor([7, 5], dtype=torch.int32), max_ctx=7)
-        outs.append(m(dec, kv))
-    assert (outs[0] - outs[1]).abs().max() < 1e-4 * outs[0].abs().max()

@@ -23,8 +23,8 @@ def test_candidates_cover_the_round3_tiles(M, N, K, glu):
         assert any(s == 11 for _, s in c)
 
 
-def test_fold_and_qkv_epilogue_candidates_are_combined_or_unsplit():
-    for nt, s in A.fold_candidates(64, 4096, 4096, False) + A.qkv_epi_candidates(64, 12288, 4096, 128, False):
+def test_qkv_epilogue_candidates_are_combined_or_unsplit():
+    for nt, s in A.qkv_epi_candidates(64, 12288, 4096, 128, False):
         assert s == 1 or (nt >> 8) & 256, (hex(nt), s)  # a split plan must combine in-launch
     # neox RoPE needs head-aligned tiles: no 64x48 / 64x96 / 64x192 plans for D = 128
     neox = _tiles(A.qkv_epi_candidates(64, 12288, 4096, 128, True))
