@@ -89,8 +89,12 @@ def main():
              "--seed", str(4321 + 97 * i + int(os.environ.get("RANK", "0")))] + (["--greedy"] if args.greedy else []),
             stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, cwd=ROOT) for i in range(nc)]
 
-    from llmss_amd.parallel.dist import TPGroup, initialize_distributed
+    from llmss_amd.models.config import get_preset
+    from llmss_amd.parallel.dist import RCCL_TUNE_INFO, TPGroup, initialize_distributed
 
+    if args.gpus > 1:  # the start-up RCCL setting probe times the decode all-reduce of THIS run: rows x hidden bf16
+        os.environ.setdefault("LLMSS_RCCL_TUNE_BYTES", str(args.batch_per_gpu * args.gpus *
+                                                           get_preset(args.model).hidden_size * 2))
     tp, rank, world = initialize_distributed()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
@@ -112,6 +116,8 @@ def main():
     res = run_config(args, args.model, tp, args.batch_per_gpu * max(world, args.simulate_tp), progress)
     if comm is not None:
         res["comm_probe"] = comm
+    if RCCL_TUNE_INFO:
+        res["rccl_setting_probe"] = dict(RCCL_TUNE_INFO)
     if args.secondary not in ("", "none") and args.simulate_tp <= 1 and args.secondary != args.model:
         # second BASELINE headline config (GPT-2-XL TP=1, 25 heads: no TP split), driver-timed in the same run;
         # with N GPUs every rank serves its own TP=1 replica (data parallel) and the node total is reported

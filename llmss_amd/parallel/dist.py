@@ -363,6 +363,107 @@ def _native_comm(rank: int, dp: int, tp: int):
     return comm
 
 
+# RCCL settings the decode all-reduce is timed under at start-up (LLMSS_RCCL_TUNE): the library's choice, then
+# each protocol forced (RCCL reads NCCL_PROTO / NCCL_ALGO while it builds a communicator's tuning tables, so a
+# communicator created under the variable keeps it). Each entry: (name, env overrides).
+RCCL_CANDIDATES = [("default", {}), ("LL", {"NCCL_PROTO": "LL"}), ("LL128", {"NCCL_PROTO": "LL128"}),
+                   ("Simple", {"NCCL_PROTO": "Simple"}), ("Tree", {"NCCL_ALGO": "Tree"})]
+RCCL_TUNE_INFO: dict = {}  # what the start-up probe measured and kept (bench.py's runtime record)
+
+
+def _time_all_reduce(comm, nbytes: int, reps: int = 20) -> float:
+    """Microseconds per bf16 all-reduce of ``nbytes``, replayed from a HIP graph (as the decode graphs run it)."""
+    from .. import _native
+
+    code = _native().rccl_dtypes["bfloat16"]
+    x = torch.ones(nbytes // 2, dtype=torch.bfloat16, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            comm.all_reduce(x.data_ptr(), x.data_ptr(), x.numel(), code, s.cuda_stream)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        for _ in range(reps):
+            comm.all_reduce(x.data_ptr(), x.data_ptr(), x.numel(), code, torch.cuda.current_stream().cuda_stream)
+    g.replay()
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        b.synchronize()
+        best = min(best, a.elapsed_time(b) * 1e3 / reps)
+    del g
+    return best
+
+
+def _tune_native_comm(comm, rank: int, tp: int, nbytes: int, group=None):
+    """Start-up probe of the RCCL protocol / algorithm for the decode all-reduce (``nbytes``, the bench's 64
+    sequences per GPU x hidden 4096 x bf16 at TP=8 = 4 MiB by default, LLMSS_RCCL_TUNE_BYTES). Every candidate
+    of RCCL_CANDIDATES gets a communicator built under its environment, its graph-replayed all-reduce is timed
+    on every rank, and the max over ranks decides (all ranks keep the same setting, so every later collective
+    pairs up); a candidate must beat the library default by 5 %. Returns the communicator to keep (the default
+    one, or the winner's) and records the table in RCCL_TUNE_INFO. Single replica (dp == 1) only: the unique
+    id of each probe communicator goes over the world group."""
+    from .. import _native
+
+    C = _native()
+    times, comms = {"default": _time_all_reduce(comm, nbytes)}, {"default": comm}
+    saved = {k: os.environ.get(k) for _, env in RCCL_CANDIDATES for k in env}
+    try:
+        for name, env in RCCL_CANDIDATES[1:]:
+            os.environ.update(env)
+            box = [C.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(box, src=0, group=group)
+            c, err = None, ""
+            try:
+                c = C.RcclComm(box[0], tp, rank, torch.cuda.current_device())
+                t = _time_all_reduce(c, nbytes)
+            except Exception as e:  # noqa: BLE001 - decided collectively below
+                err, t = str(e), float("inf")
+            for k in env:
+                if saved[k] is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = saved[k]
+            ok = torch.tensor([0 if err else 1], dtype=torch.int32)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+            if not int(ok[0]):
+                if c is not None:
+                    c.abort()
+                times[name] = None
+                continue
+            times[name], comms[name] = t, c
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    allt = [None] * dist.get_world_size(group)
+    dist.all_gather_object(allt, times, group=group)
+    worst = {n: (None if any(t[n] is None for t in allt) else max(t[n] for t in allt)) for n in times}
+    ok = {n: v for n, v in worst.items() if v is not None}
+    best = min(ok, key=lambda n: ok[n] if n == "default" else ok[n] / 0.95)
+    for n, c in comms.items():
+        if n != best:
+            c.destroy()
+    RCCL_TUNE_INFO.clear()
+    RCCL_TUNE_INFO.update({"bytes": nbytes, "us": {n: (round(v, 2) if v is not None else None)
+                                                   for n, v in worst.items()}, "kept": best,
+                           "env": dict(dict(RCCL_CANDIDATES)[best])})
+    if best != "default":  # later communicators of this process (none today) inherit the setting too
+        os.environ.update(dict(RCCL_CANDIDATES)[best])
+    log.info("rank %d: RCCL all-reduce %d KiB per setting (us, max over ranks): %s -> keeping %s", rank,
+             nbytes >> 10, RCCL_TUNE_INFO["us"], best)
+    return comms[best]
+
+
 def initialize_distributed(timeout_s: Optional[int] = None, backend: Optional[str] = None, dp: Optional[int] = None):
     """Initialise torch.distributed from torchrun env vars.
 
@@ -419,6 +520,11 @@ def initialize_distributed(timeout_s: Optional[int] = None, backend: Optional[st
             err = str(e)
         ok = torch.tensor([0 if err else 1], dtype=torch.int32)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # CPU (gloo) world group: every rank takes the same path
+        if int(ok[0]) and dp == 1 and os.environ.get("LLMSS_RCCL_TUNE", "1") != "0":
+            try:
+                comm = _tune_native_comm(comm, rank, tp, _env_int("LLMSS_RCCL_TUNE_BYTES", 4 << 20))
+            except Exception as e:  # noqa: BLE001 - a failed probe keeps the library default
+                log.warning("rank %d: RCCL setting probe failed (%s); keeping the default", rank, e)
         if not int(ok[0]):
             if comm is not None:
                 comm.abort()

@@ -198,3 +198,45 @@ def test_captured_collectives_are_graph_nodes(comm):
         g.replay()
         torch.cuda.synchronize()
         assert all(bool((o == v).all()) for o in outs)
+
+
+def test_rccl_setting_probe_one_rank(monkeypatch):
+    """The start-up probe of RCCL protocol / algorithm settings (parallel/dist.py _tune_native_comm) builds a
+    communicator per candidate environment, times the graph-replayed all-reduce on each, keeps one communicator
+    that still works and restores the environment (one rank: the mechanism; the multi-rank timing runs in the
+    driver's multi-GPU bench and lands in its runtime record)."""
+    import os
+    import socket
+
+    import torch.distributed as dist
+
+    from llmss_amd import _native
+    from llmss_amd.parallel import dist as D
+
+    C = _native()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(port))
+    monkeypatch.delenv("NCCL_PROTO", raising=False)
+    monkeypatch.delenv("NCCL_ALGO", raising=False)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        c0 = C.RcclComm(C.rccl_unique_id(), 1, 0, torch.cuda.current_device())
+        kept = D._tune_native_comm(c0, 0, 1, 1 << 20)
+        info = D.RCCL_TUNE_INFO
+        assert info["bytes"] == 1 << 20 and set(info["us"]) == {n for n, _ in D.RCCL_CANDIDATES}
+        assert info["kept"] in info["us"] and info["us"]["default"] > 0
+        assert os.environ.get("NCCL_PROTO") == info["env"].get("NCCL_PROTO")
+        x = torch.arange(64, dtype=torch.float32, device="cuda")
+        out = torch.empty_like(x)
+        kept.all_gather(x.data_ptr(), out.data_ptr(), x.numel(), C.rccl_dtypes["float32"], _st())
+        torch.cuda.synchronize()
+        assert torch.equal(out, x)
+        kept.destroy()
+    finally:
+        dist.destroy_process_group()
+        os.environ.pop("NCCL_PROTO", None)
+        os.environ.pop("NCCL_ALGO", None)
