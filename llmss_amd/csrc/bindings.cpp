@@ -39,11 +39,6 @@ void launch_attn_extend(const void* q, int64_t q_stride, const void* k_cache, co
                         const void* block_tables, int max_blocks, const void* cu_q, const void* ctx_lens, void* out,
                         int64_t out_stride, int B, int max_qlen, int nh, int nkv, int D, int bs, float scale,
                         hipStream_t st, bool kv8);
-bool fused_mlp_plan(int M, int H, int N1, int F, bool glu, int* grid, int* ub, int* s2);
-void launch_fused_mlp(const void* dpart, int dS, const void* dbias, const void* delta, void* resid, const void* nw,
-                      const void* nb, float eps, bool rms, void* y, const void* wu, const void* bu, void* h,
-                      const void* wd, void* out, int M, int H, int N1, int F, bool glu, int act, int grid, int ub,
-                      int s2, int* cnt, int* err, hipStream_t st);
 int launch_gemm_qkv_args(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y, int64_t ldy,
                          int M, int N, int K, void* workspace, int64_t ws_bytes, int nt_hint, int split_hint,
                          const void* pos, const void* cos_t, const void* sin_t, void* kc, void* vc, const void* slot,
@@ -154,19 +149,6 @@ PYBIND11_MODULE(_C, m) {
      pybind11::arg("pos"), pybind11::arg("cos_t"), pybind11::arg("sin_t"), pybind11::arg("kc"), pybind11::arg("vc"),
      pybind11::arg("slot"), pybind11::arg("nh"), pybind11::arg("nkv"), pybind11::arg("D"), pybind11::arg("rot"),
      pybind11::arg("bs"), pybind11::arg("style"), pybind11::arg("do_rope"), pybind11::arg("st"));
-  m.def("fused_mlp_plan", [](int M, int H, int N1, int F, bool glu) -> py::object {
-    int g, u, s;
-    if (!fused_mlp_plan(M, H, N1, F, glu, &g, &u, &s)) return py::none();
-    return py::make_tuple(g, u, s);
-  });
-  m.def("fused_mlp", [](uintptr_t dpart, int dS, uintptr_t dbias, uintptr_t delta, uintptr_t resid, uintptr_t nw,
-                        uintptr_t nb, float eps, bool rms, uintptr_t y, uintptr_t wu, uintptr_t bu, uintptr_t h,
-                        uintptr_t wd, uintptr_t out, int M, int H, int N1, int F, bool glu, int act, int grid, int ub,
-                        int s2, uintptr_t cnt, uintptr_t err, uintptr_t st) {
-    launch_fused_mlp(CP(dpart), dS, CP(dbias), CP(delta), P(resid), CP(nw), CP(nb), eps, rms, P(y), CP(wu), CP(bu),
-                     P(h), CP(wd), P(out), M, H, N1, F, glu, act, grid, ub, s2, reinterpret_cast<int*>(P(cnt)),
-                     reinterpret_cast<int*>(P(err)), S(st));
-  });
   m.def("gemm_plan", [](int M, int N, int K, bool fp8) {
     int nt, s;
     gemm_plan(M, N, K, fp8, &nt, &s);

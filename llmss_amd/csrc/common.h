@@ -172,12 +172,40 @@ struct QkvEpi {
   int nh, nkv, D, rot, block_size, style, do_rope;
 };
 
+// fp32 epilogue image of a tile with BN columns in LDS. The C-layout writes (lane li, g -> row 4g + i,
+// column li: ds_write_b32, banks mod 32 per 32-lane half) and the row-piece reads (ds_read_b128, banks
+// mod 64 per 16-lane group) are both conflict-free when rows are unpadded and the 16-B slot of a float
+// is XOR-ed with 4 on rows with bit 2 set (BN % 32 == 0); other widths pad rows by 4 floats. The
+// previous padded image with 4-byte reads cost 4-8x the ideal LDS cycles on the read side
+// (SQ_LDS_BANK_CONFLICT 21 % of gemm_big's LDS-active cycles, all in the epilogue).
+template <int BN>
+struct EpiImg {
+  static constexpr bool SWZ = BN % 32 == 0;
+  static constexpr int LDW = SWZ ? BN : BN + 4;
+  __device__ static __forceinline__ int at(int r, int c) { return r * LDW + (SWZ ? (c ^ (((r >> 2) & 1) << 4)) : c); }
+  __device__ static __forceinline__ f32x4 ld4(const float* ct, int r, int c) {  // c % 4 == 0
+    return *reinterpret_cast<const f32x4*>(ct + at(r, c));
+  }
+  // 8 floats of row r from column c (c % 8 == 0) as two ds_read_b128. Lanes whose bit 3 is set take
+  // the upper half first, so the lanes of a 16-lane group that hit the same slot pair split across
+  // the two instructions.
+  __device__ static __forceinline__ void ld8(const float* ct, int r, int c, float (&x)[8]) {
+    const int key = (threadIdx.x >> 3) & 1;
+    const f32x4 a = ld4(ct, r, c + 4 * key), b = ld4(ct, r, c + 4 * (key ^ 1));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      x[i] = key ? b[i] : a[i];
+      x[4 + i] = key ? a[i] : b[i];
+    }
+  }
+};
+
 // One LDS row chunk of the QKV epilogue: each thread owns ITEMS (row, 8-column) groups of the chunk and
 // processes them G at a time in three phases - (1) every group's position and cache slot, (2) every
 // group's cos / sin rows, (3) rotate, round, store - so each thread pays two dependent memory round trips
 // per G groups instead of per group (the loads sit behind no per-group branch: addresses are clamped).
 template <int BN, int NTHR, int R>
-__device__ __forceinline__ void qkv_store_chunk(const QkvEpi& e, const float* ct, int ldw, int rows, int r0, int m0,
+__device__ __forceinline__ void qkv_store_chunk(const QkvEpi& e, const float* ct, int rows, int r0, int m0,
                                                 int n0, int M, int N, bf16_t* __restrict__ Y, int64_t ldy,
                                                 const bf16_t* __restrict__ bias) {
   constexpr int VPR = BN / 8, ITEMS = (R * VPR + NTHR - 1) / NTHR, G = ITEMS < 4 ? ITEMS : 4;
@@ -221,11 +249,11 @@ __device__ __forceinline__ void qkv_store_chunk(const QkvEpi& e, const float* ct
     for (int j = 0; j < G; ++j) {  // phase 3: bias, bf16 rounding, rotation, stores
       if (!ok[j]) continue;
       const int c = cc[j], n = n0 + c, d = n % D, m = mm[j];
-      const float* crow = ct + rr[j] * ldw;
       float x[8], y[8];
+      EpiImg<BN>::ld8(ct, rr[j], c, x);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        x[i] = bf2f(f2bf(crow[c + i] + (bias ? bf2f(bias[n + i]) : 0.f)));
+        x[i] = bf2f(f2bf(x[i] + (bias ? bf2f(bias[n + i]) : 0.f)));
         y[i] = x[i];
       }
       const bool is_v = n >= nq + nk;
@@ -239,9 +267,11 @@ __device__ __forceinline__ void qkv_store_chunk(const QkvEpi& e, const float* ct
         } else {  // neox: halves [0, rh) and [rh, rot) rotate against each other
           const bool lo = d < rh;
           const int sh = lo ? rh : -rh;
+          float xs[8];
+          EpiImg<BN>::ld8(ct, rr[j], c + sh, xs);
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
-            const float xp = bf2f(f2bf(crow[c + sh + i] + (bias ? bf2f(bias[n + sh + i]) : 0.f)));
+            const float xp = bf2f(f2bf(xs[i] + (bias ? bf2f(bias[n + sh + i]) : 0.f)));
             const float cv = cs[j][i >> 2][i & 3], sv = sn[j][i >> 2][i & 3];
             y[i] = lo ? x[i] * cv - xp * sv : x[i] * cv + xp * sv;
           }
@@ -273,8 +303,8 @@ __device__ __forceinline__ void tile_store_lds(const f32x4 (&acc)[MT][NT], char*
                                                int n0, int M, int N, float* __restrict__ part,
                                                bf16_t* __restrict__ Y, int64_t ldy, const bf16_t* __restrict__ bias,
                                                int act, int glu, const QkvEpi& qe = QkvEpi{}) {
-  constexpr int LDW = BN + 4;  // padded row: the 4 rows a wave-instruction writes hit different banks
-  constexpr int RMAX = LDSB / (LDW * 4);
+  using Img = EpiImg<BN>;
+  constexpr int RMAX = LDSB / (Img::LDW * 4);
   constexpr int R = (RMAX >= BM ? BM : RMAX) / 16 * 16;
   static_assert(R >= 16, "LDS too small for a 16-row epilogue chunk");
   float* ct = reinterpret_cast<float*>(lds);
@@ -290,21 +320,21 @@ __device__ __forceinline__ void tile_store_lds(const f32x4 (&acc)[MT][NT], char*
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) ct[(rb - r0 + 4 * g + i) * LDW + wcol0 + nt * 16 + li] = acc[mt][nt][i];
+        for (int nt = 0; nt < NT; ++nt) ct[Img::at(rb - r0 + 4 * g + i, wcol0 + nt * 16 + li)] = acc[mt][nt][i];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const int rows = BM - r0 < R ? BM - r0 : R;  // the last chunk may be shorter
     if (qe.D) {  // QKV projection: RoPE + paged KV write (N % 8 == 0, ldy % 8 == 0: host-checked)
-      qkv_store_chunk<BN, NTHR, R>(qe, ct, LDW, rows, r0, m0, n0, M, N, Y, ldy, bias);
+      qkv_store_chunk<BN, NTHR, R>(qe, ct, rows, r0, m0, n0, M, N, Y, ldy, bias);
     } else if (part) {  // fp32 slab rows: 4 floats (16 B) per thread-step
       constexpr int VPR = BN / 4;
       for (int v = threadIdx.x; v < rows * VPR; v += NTHR) {
         const int r = v / VPR, c = (v - r * VPR) * 4;
         const int m = m0 + r0 + r, n = n0 + c;
         if (m >= M || n >= N) continue;
-        const f32x4 val = *reinterpret_cast<const f32x4*>(&ct[r * LDW + c]);
+        const f32x4 val = Img::ld4(ct, r, c);
         float* dst = part + (int64_t)m * N + n;
         if (n + 3 < N && (N & 3) == 0) *reinterpret_cast<f32x4*>(dst) = val;
         else
@@ -318,9 +348,12 @@ __device__ __forceinline__ void tile_store_lds(const f32x4 (&acc)[MT][NT], char*
         const int cg = 32 * p + j, m = m0 + r0 + r, ng = n0 + cg;
         if (m >= M || ng >= N) continue;  // N % 32 == 0: the whole gate|up pair exists
         u16x8 o;
+        float gx[8], ux[8];
+        Img::ld8(ct, r, cg, gx);
+        Img::ld8(ct, r, cg + 16, ux);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float gv = ct[r * LDW + cg + e], uv = ct[r * LDW + cg + 16 + e];
+          float gv = gx[e], uv = ux[e];
           if (bias) { gv += bf2f(bias[ng + e]); uv += bf2f(bias[ng + 16 + e]); }
           o[e] = f2bf(silu(gv) * uv);
         }
@@ -336,9 +369,11 @@ __device__ __forceinline__ void tile_store_lds(const f32x4 (&acc)[MT][NT], char*
         const int m = m0 + r0 + r, n = n0 + c;
         if (m >= M || n >= N) continue;
         u16x8 o;
+        float xv[8];
+        Img::ld8(ct, r, c, xv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float x = ct[r * LDW + c + e];
+          float x = xv[e];
           if (bias && n + e < N) x += bf2f(bias[n + e]);
           o[e] = f2bf(apply_act(x, act));
         }

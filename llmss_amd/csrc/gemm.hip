@@ -535,7 +535,11 @@ __device__ __forceinline__ void wait_vmcnt_upto(int younger) {
 // Barrier that lets global_load_lds stay in flight across it: __syncthreads()' release fence
 // would emit vmcnt(0) and drain the prefetch (guide: "Pipelining across barriers").
 __device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // lgkmcnt(0) through the builtin (vmcnt / expcnt at their maxima), which the compiler's wait-count
+  // pass accounts for: after an inline-asm wait it still believes earlier LDS reads are pending and
+  // adds an lgkmcnt(0) in front of the next MFMA that uses their registers
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
@@ -704,6 +708,9 @@ __device__ __forceinline__ f32x4 mfma_f8x2(s16x8 a0, s16x8 a1, s16x8 b0, s16x8 b
 // 64-element bf16 one, so staging / LDS image / fragment addresses are shared; each (m, n) takes one
 // MX-fp8 16x16x128 MFMA per K-tile (the two 16-B chunks 2g, 2g+1 of the lane's row), and the
 // per-token x per-channel scales are applied in the epilogue.
+// K-loop schedules measured against this one (profiles/r4_gemm_big): hiding one k-half's fragment reads under
+// the other k-half's MFMAs inside the K-tile changes nothing; doing it across K-tiles (prefetch distance 1
+// K-tile instead of 1.5) is 6 % slower - the loop waits on the LDS-DMA stream, not on LDS reads.
 template <bool F8>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict__ A, int64_t lda,
                                                           const void* __restrict__ B, int64_t ldb,

@@ -216,8 +216,6 @@ class LLMEngine:
             self.tuned = tune_model(model, self.decode_batch_sizes())
         if self.is_gpu and autotune:
             self._tune_gqa_attention()
-        if self.is_gpu:
-            self._tune_fused_mlp(autotune)
         if self.use_graphs and os.environ.get("LLMSS_GRAPHS", "1") == "0":
             self.use_graphs = False
         self._capture_agreed()
@@ -259,7 +257,6 @@ class LLMEngine:
                 "dist_sampling": self.dist_sampling, "kv_fp8": bool(self.model.kv_fp8),
                 "overlap_rows": self.model.overlap_rows, "bucket_bytes": self.model.bucket_bytes,
                 "tbo_min": self.model.tbo_min, "graph_keys": sorted(self.graphs),
-                "fused_mlp": sorted(self.model.fused_mlp_rows),
                 "decode_schedule": sorted(self.decode_schedule.items()), "rsag_mode": self.model.rsag_mode,
                 "fp8": any(L.qkv.w_scale is not None for L in self.model.w.layers[:1])}
 
@@ -342,49 +339,6 @@ class LLMEngine:
             del kc, vc
         self.stats["gqa_attn_us"] = {str(b): v for b, v in res.items()}
         log.info("GQA decode attention (us VALU split-K / MFMA extend): %s; MFMA for %s", res, sorted(m.gqa_mfma))
-
-    def _tune_fused_mlp(self, timed: bool):
-        """Decode buckets whose MLP block runs as the persistent fused launch (csrc/fused_mlp.hip) instead of
-        add_norm + up GEMM + down GEMM: LLMSS_FUSED_MLP=auto (default) times both on layer 0's weights per
-        bucket (graph-replayed, like the GEMM autotuner) and keeps the fused one where it is faster by 2 %;
-        1 takes it for every bucket it supports (and auto without the autotuner), 0 never. TP = 1 only."""
-        m = self.model
-        mode = m.fused_mlp_mode
-        if mode == "0" or not m.fused_mlp_ok():
-            return
-        from ..ops.autotune import _time
-
-        L, cfg, dev = m.w.layers[0], self.cfg, self.device
-        H = cfg.hidden_size
-        res = {}
-        for b in self.decode_batch_sizes():
-            if b > 64 or _hip_ops.fused_mlp_plan(b, H, L.up.N, L.down.K, L.up.glu) is None:
-                continue
-            if mode == "1" or not timed:
-                m.fused_mlp_rows.add(b)
-                continue
-            g = torch.Generator(device=dev)
-            g.manual_seed(7)
-            o = (torch.randn(b, H, device=dev, generator=g) * 0.5).to(m.dtype)
-            resid = (torch.randn(b, H, device=dev, generator=g)).to(m.dtype)
-
-            def unfused(i):
-                y2, _ = ops.add_norm(o, L.ln2_w, L.ln2_b, cfg.norm_eps, m.rms, resid)
-                L.down(L.up(y2, m.act), partial_ok=True)
-
-            def fused(i):
-                m.fused_mlp(L, o, resid)
-            unfused(0)
-            fused(0)
-            torch.cuda.synchronize()
-            tu, tf = _time(unfused, 8), _time(fused, 8)
-            if tf < 0.98 * tu:
-                m.fused_mlp_rows.add(b)
-            res[b] = (round(tu, 1), round(tf, 1))
-        if _hip_ops.fused_mlp_error(dev):
-            raise RuntimeError("fused MLP: a hand-off wait timed out (workgroups not co-resident)")
-        self.stats["fused_mlp_us"] = {str(b): v for b, v in res.items()}
-        log.info("fused MLP block (us unfused / fused): %s; fused for %s", res, sorted(m.fused_mlp_rows))
 
     def _tbo_candidates(self) -> List[int]:
         """Decode buckets whose two-micro-batch schedule is timed against the single-batch one at capture

@@ -115,11 +115,6 @@ class DecoderLM:
         # the engine's capture-time A/B picks on the real communicator, 0 never
         self.rsag_mode = os.environ.get("LLMSS_TP_RSAG", "auto")
         self.rsag: set = set()
-        # decode batch sizes whose MLP block (add + norm -> up -> down) runs as ONE persistent launch
-        # (csrc/fused_mlp.hip); TP = 1, bf16 weights, M <= 64. LLMSS_FUSED_MLP=auto (default: the engine times
-        # both forms per decode bucket at start-up and keeps the faster), 1 (every supported batch), 0 (never)
-        self.fused_mlp_mode = os.environ.get("LLMSS_FUSED_MLP", "0")
-        self.fused_mlp_rows: set = set()
         self._cu_decode = {}
         self._comm_stream = None
 
@@ -370,27 +365,6 @@ class DecoderLM:
             ops.add_norm(delta[j], w.lnf_w, w.lnf_b, eps, rms, res[j], out=out[r0:r1])
         return out
 
-    def fused_mlp_ok(self) -> bool:
-        """Can this model's MLP blocks run as the persistent fused launch (csrc/fused_mlp.hip)?"""
-        L = self.w.layers[0]
-        return (self.w.wte.is_cuda and self.tp.size == 1 and not self.cfg.parallel_block
-                and all(lin.w.dim() == 2 and lin.w_scale is None and lin.w.dtype == torch.bfloat16
-                        for lin in (L.up, L.down)))
-
-    def fused_mlp_wanted(self, M: int) -> bool:
-        if self.fused_mlp_mode == "0" or M > 64:
-            return False
-        return self.fused_mlp_mode == "1" or M in self.fused_mlp_rows
-
-    def fused_mlp(self, L, o, residual):
-        """The MLP block of a decode layer as one launch: residual += o (in place), y = norm2(residual), then
-        up / activation / down; returns the down projection's split-K slabs (summed by the next add_norm), or
-        None when the shape has no fused plan."""
-        if residual is None or not self.fused_mlp_ok():
-            return None
-        return _hip_ops().fused_mlp(o, residual, L.ln2_w, L.ln2_b, self.cfg.norm_eps, self.rms, L.up.w, L.up.b,
-                                    L.down.w, L.down.b, self.act, L.up.glu)
-
     def rsag_ok(self, M: int) -> bool:
         """Can an M-row decode step run the row-sharded (reduce-scatter / all-gather) schedule?"""
         return self.tp.comm_active and self.tp.size > 1 and M % self.tp.size == 0 and M >= self.tp.size
@@ -452,11 +426,6 @@ class DecoderLM:
             elif fuse:
                 # TP=1: the split-K partials of o / down are reduced inside the next add_norm
                 o = L.o(a, partial_ok=True)
-                if inp.kind == "decode" and self.fused_mlp_wanted(o.shape[0]):
-                    d = self.fused_mlp(L, o, residual)
-                    if d is not None:
-                        delta = d
-                        continue
                 y2, residual = ops.add_norm(o, L.ln2_w, L.ln2_b, eps, rms, residual, fp8_out=self._fp8_in(L.up, a))
                 delta = L.down(L.up(y2, self.act), partial_ok=True)
             else:

@@ -605,75 +605,6 @@ def linear_qkv(x, w, bias, positions, cos, sin, k_cache, v_cache, slots, nh, nkv
     return y if rc == 0 else None
 
 
-class _MlpScratch:
-    """Buffers of the fused MLP launch per (device, H, F, S2): normed rows y [64, H] and activated rows h [64, F]
-    (bf16 hand-offs), the down projection's fp32 slabs [S2, 64, H] and the self-resetting counters."""
-
-    def __init__(self):
-        self.bufs = {}
-
-    def get(self, device, H, F, S2):
-        key = (str(device), H, F, S2)
-        b = self.bufs.get(key)
-        if b is None:
-            b = self.bufs[key] = {
-                "y": torch.empty(64, H, dtype=torch.bfloat16, device=device),
-                "h": torch.empty(64, F, dtype=torch.bfloat16, device=device),
-                "out": torch.empty(S2 * 64 * H, dtype=torch.float32, device=device),
-                "cnt": torch.zeros(2 + S2, dtype=torch.int32, device=device),
-                "err": torch.zeros(1, dtype=torch.int32, device=device)}
-        return b
-
-
-_MLP_WS = _Slotted(_MlpScratch)
-
-
-def fused_mlp_plan(M: int, H: int, N1: int, F: int, glu: bool):
-    """(grid, up units per workgroup, down K slices) of a fused MLP launch, or None (shape not supported)."""
-    return lib().fused_mlp_plan(int(M), int(H), int(N1), int(F), bool(glu))
-
-
-def fused_mlp(delta, residual, nw, nb, eps, rms, wu, bu, wd, bd, act="none", glu=False):
-    """ONE persistent launch for  r = delta + residual (in place);  y = norm(r);  h = act(y @ wu^T + bu);
-    slabs = h @ wd^T  (csrc/fused_mlp.hip) - the add_norm + up GEMM + down GEMM of a decode layer. ``delta`` is
-    the o-projection's :class:`PartialSum` or bf16 [M, H] output. Returns the down projection as a
-    :class:`PartialSum` (bias ``bd`` added by its consumer, like the unfused split-K GEMM), or None when the
-    shape has no plan (the caller then runs the three kernels)."""
-    if isinstance(delta, PartialSum):
-        M, H = delta.M, delta.N
-    else:
-        _bf16_rows(delta, "delta")
-        M, H = delta.shape
-    _check(residual is not None and residual.dtype == torch.bfloat16 and residual.is_contiguous()
-           and residual.shape == (M, H), "residual [M, H] bf16")
-    if wu.dim() != 2 or wd.dim() != 2 or wu.dtype != torch.bfloat16 or wd.dtype != torch.bfloat16:
-        return None
-    N1, F = wu.shape[0], wd.shape[1]
-    _check(wu.shape[1] == H and wd.shape[0] == H and wu.is_contiguous() and wd.is_contiguous(), "mlp weights")
-    plan = fused_mlp_plan(M, H, N1, F, glu)
-    if plan is None:
-        return None
-    G, ub, s2 = plan
-    _check(nw.numel() == H and nw.dtype == torch.bfloat16, "norm weight")
-    for b, n in ((nb, H), (bu, N1), (bd, H)):
-        if b is not None:
-            _check(b.dtype == torch.bfloat16 and b.is_contiguous() and b.numel() == n, "bias")
-    ws = _MLP_WS.get(residual.device, H, F, s2)
-    dp = delta if isinstance(delta, PartialSum) else None
-    lib().fused_mlp(dp.buf.data_ptr() if dp else 0, dp.S if dp else 0, _ptr(dp.bias) if dp else 0,
-                    0 if dp else delta.data_ptr(), residual.data_ptr(), nw.data_ptr(), _ptr(nb), float(eps), bool(rms),
-                    ws["y"].data_ptr(), wu.data_ptr(), _ptr(bu), ws["h"].data_ptr(), wd.data_ptr(), ws["out"].data_ptr(),
-                    M, H, N1, F, bool(glu), _ACT[act], G, ub, s2, ws["cnt"].data_ptr(), ws["err"].data_ptr(),
-                    _stream())
-    return PartialSum(ws["out"], s2, M, H, bd, residual.device)
-
-
-def fused_mlp_error(device) -> bool:
-    """Did any fused MLP launch on ``device`` time out in a hand-off wait (a producer workgroup not resident)?"""
-    return any(int(b["err"].item()) for inst in _MLP_WS._items for b in inst.bufs.values()
-               if str(b["err"].device) == str(device))
-
-
 def add_norm_partial(p: PartialSum, weight, bias, eps, rms, residual, out=None, fp8_out=False):
     T, H = p.M, p.N
     _check(residual is not None and residual.is_contiguous() and residual.shape == (T, H), "residual [T, H]")

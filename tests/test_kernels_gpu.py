@@ -210,6 +210,22 @@ def test_gemm(M, N, K):
         close(H.linear(x, w, None, glu=True), R.linear(x.float(), w.float(), None, glu=True), 2e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(700, 1312, 64), (513, 768, 128), (300, 512, 192), (1024, 1536, 4096),
+                                   (2100, 800, 1600)])
+def test_gemm_big_edges(M, N, K):
+    """The 256x256 prefill kernel (gemm.hip gemm_big_kernel) against the fp32 oracle at K-tile counts 1-3
+    (prologue / epilogue edges of its two-buffer pipeline) and ragged M / N, through the swizzled LDS epilogue."""
+    torch.manual_seed(0)
+    x, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
+    b = rnd(N, scale=0.1)
+    y = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=x.device)
+    close(H.linear(x, w, b, act="gelu_tanh", nt_hint=4 << 8, split_hint=1, out=y),
+          R.linear(x.float(), w.float(), b.float(), act="gelu_tanh"), 2e-2)
+    y = torch.full((M, N // 2), float("nan"), dtype=torch.bfloat16, device=x.device)
+    close(H.linear(x, w, None, glu=True, nt_hint=4 << 8, split_hint=1, out=y),
+          R.linear(x.float(), w.float(), None, glu=True), 2e-2)
+
+
 # 128x128, 64x128, 64x64, 256x256, 256x128 / 256x64 (8 waves); gemm_mid (buffer-descriptor staging):
 # 8 = 128x128, 9 = 256x128, 10 = 64x256, 11 = 64x128, 12 = 128x256, 13 = 64x192, 14 = 64x32, 15 = 64x96, 7 = 64x48
 @pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
