@@ -710,7 +710,8 @@ __device__ __forceinline__ f32x4 mfma_f8x2(s16x8 a0, s16x8 a1, s16x8 b0, s16x8 b
 // per-token x per-channel scales are applied in the epilogue.
 // K-loop schedules measured against this one (profiles/r4_gemm_big): hiding one k-half's fragment reads under
 // the other k-half's MFMAs inside the K-tile changes nothing; doing it across K-tiles (prefetch distance 1
-// K-tile instead of 1.5) is 6 % slower - the loop waits on the LDS-DMA stream, not on LDS reads.
+// K-tile instead of 1.5) is 6 % slower; restaging right after the fragment reads (distance ~1.8) is 0-3 %
+// slower. Neither LDS reads nor the DMA prefetch distance alone set its ~1.2 PFLOP/s.
 template <bool F8>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict__ A, int64_t lda,
                                                           const void* __restrict__ B, int64_t ldb,

@@ -210,6 +210,25 @@ def test_gemm(M, N, K):
         close(H.linear(x, w, None, glu=True), R.linear(x.float(), w.float(), None, glu=True), 2e-2)
 
 
+def test_prompt_batch_library_routing():
+    """Plain prompt-batch GEMMs routed to the platform library (ops/hip.py _LIB_PREFILL) give the oracle's result
+    with bias, into a given output; SwiGLU / activation calls and decode-sized M stay on the HIP kernels."""
+    torch.manual_seed(0)
+    M, N, K = 1100, 768, 512
+    x, w, b = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
+    ref = R.linear(x.float(), w.float(), b.float())
+    H._LIB_PREFILL.add((N, K))
+    try:
+        y = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=dev)
+        assert H.linear(x, w, b, out=y) is y
+        close(y, ref, 2e-2)
+        close(H.linear(x, w, b, partial_ok=True), ref, 2e-2)
+        close(H.linear(x, w, None, glu=True), R.linear(x.float(), w.float(), None, glu=True), 2e-2)
+        close(H.linear(x[:64], w, b), ref[:64], 2e-2)
+    finally:
+        H._LIB_PREFILL.discard((N, K))
+
+
 @pytest.mark.parametrize("M,N,K", [(700, 1312, 64), (513, 768, 128), (300, 512, 192), (1024, 1536, 4096),
                                    (2100, 800, 1600)])
 def test_gemm_big_edges(M, N, K):
