@@ -55,13 +55,22 @@ def main():
                 for _ in range(5):
                     f()
                 torch.cuda.synchronize()
-                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                s.record()
-                for _ in range(50):
-                    f()
-                e.record()
+                # 50 calls in one HIP graph (as the decode graphs run it): no host launch cost in the time
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                    for _ in range(50):
+                        f()
+                g.replay()
                 torch.cuda.synchronize()
-                us = s.elapsed_time(e) * 1e3 / 50
+                us = float("inf")
+                for _ in range(3):
+                    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    s.record()
+                    g.replay()
+                    e.record()
+                    torch.cuda.synchronize()
+                    us = min(us, s.elapsed_time(e) * 1e3 / 50)
+                del g
                 tag = f"u{u}" + (f"s{sp}" if sp else "")
                 res[f"{tag}_us"] = round(us, 2)
                 res[f"{tag}_TBps"] = round(kv_bytes / us / 1e6, 2)

@@ -708,10 +708,13 @@ __device__ __forceinline__ f32x4 mfma_f8x2(s16x8 a0, s16x8 a1, s16x8 b0, s16x8 b
 // 64-element bf16 one, so staging / LDS image / fragment addresses are shared; each (m, n) takes one
 // MX-fp8 16x16x128 MFMA per K-tile (the two 16-B chunks 2g, 2g+1 of the lane's row), and the
 // per-token x per-channel scales are applied in the epilogue.
-// K-loop schedules measured against this one (profiles/r4_gemm_big): hiding one k-half's fragment reads under
-// the other k-half's MFMAs inside the K-tile changes nothing; doing it across K-tiles (prefetch distance 1
-// K-tile instead of 1.5) is 6 % slower; restaging right after the fragment reads (distance ~1.8) is 0-3 %
-// slower. Neither LDS reads nor the DMA prefetch distance alone set its ~1.2 PFLOP/s.
+// bf16 K-loop (profiles/r4_gemm_big): the next-but-one K-tile's 8 LDS-DMA loads are issued one per 4 MFMAs
+// of the second k-half instead of as one burst before them (an in-order wave cannot issue MFMAs while its
+// load burst waits on the CU's address path), and the second k-half's fragment reads one or two per 4
+// MFMAs of the first k-half: +3-6 % at M = 2048 / 8192. Measured and not taken: the second k-half's reads
+// as one block under the first k-half's MFMAs (no change), reading the next K-tile's first k-half under
+// this one's second (prefetch distance 1 K-tile instead of 1.5: -6 %), restaging right after the fragment
+// reads (distance ~1.8: 0-3 % slower).
 template <bool F8>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict__ A, int64_t lda,
                                                           const void* __restrict__ B, int64_t ldb,
@@ -719,6 +722,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict
                                                           int64_t ldy, int M, int N, int K, int act, int glu,
                                                           const float* __restrict__ xs, const float* __restrict__ ws,
                                                           int group_m) {
+  constexpr int ILV = F8 ? 0 : 2;
   constexpr int ES = F8 ? 1 : 2;  // operand bytes per element
   constexpr int HALF = 16384, BUF = 4 * HALF;
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
@@ -799,6 +803,26 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict
     else wait_vmcnt<0>();
     lds_barrier();  // stage t landed for every wave
     s16x8 a[8][2], b[4][2];
+    if constexpr (ILV == 2 && !F8) {
+      // k-half 0 fragments, then its MFMAs with the k-half 1 fragment reads interleaved (1-2 per 4 MFMAs)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) b[n][0] = *reinterpret_cast<const s16x8*>(cur + boff[n][0]);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) a[m][0] = *reinterpret_cast<const s16x8*>(cur + aoff[m][0]);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), seen by the wait-count pass: the MFMAs below wait on nothing
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        if (m < 4) b[m][1] = *reinterpret_cast<const s16x8*>(cur + boff[m][1]);
+        a[m][1] = *reinterpret_cast<const s16x8*>(cur + aoff[m][1]);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][0], b[n][0], acc[m][n], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMAs, then the next fragment reads
+        if (m < 4) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        else __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+    } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
 #pragma unroll
@@ -819,7 +843,24 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict
         for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][0], b[n][0], acc[m][n], 0, 0, 0);
     }
     __builtin_amdgcn_s_setprio(0);
+    }
     lds_barrier();  // every wave's reads of this buffer are complete -> restage it
+    if constexpr (ILV && !F8) {
+      const bool more = t + 2 < nk;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        if (more)
+          __builtin_amdgcn_global_load_lds((const void*)(src[m >> 1] + soff[m >> 1][m & 1] + (int64_t)(t + 2) * 128),
+                                           (LDS_AS void*)(cur + (m >> 1) * HALF + lofs[m & 1]), 16, 0, 0);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][1], b[n][1], acc[m][n], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // the load ...
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // ... then its 4 MFMAs
+      }
+      __builtin_amdgcn_s_setprio(0);
+      continue;
+    }
     if (t + 2 < nk) stage(t + 2, cur);
     __builtin_amdgcn_s_setprio(1);
     if constexpr (F8) {  // second half: n-tiles 2, 3
