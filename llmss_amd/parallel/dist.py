@@ -341,16 +341,38 @@ def comm_mode() -> str:
 def _native_comm(rank: int, dp: int, tp: int):
     """One RCCL communicator per data-parallel replica (ranks r*tp .. r*tp+tp-1). Each replica leader draws a
     unique id; the ids travel over the CPU world group (every rank joins every broadcast), then each rank
-    joins its replica's communicator and checks it with one all-reduce."""
+    joins its replica's communicator and checks it with one all-reduce.
+
+    Everything that can fail before ncclCommInitRank (drawing the id, the device) is agreed over gloo first,
+    so a rank that fails there makes every rank raise instead of leaving its peers blocked inside the init.
+    A failure inside ncclCommInitRank itself is not covered: RCCL's blocking init has no timeout, and the
+    non-blocking form would make every later collective call asynchronous too. The peers
+    then wait until the launcher's (or the driver's) time limit."""
     from .. import _native
 
     C = _native()
-    uids = []
+    uids, err = [], ""
     for r in range(dp):
-        box = [C.rccl_unique_id() if rank == r * tp else None]
+        box = [None]
+        if rank == r * tp:
+            try:
+                box = [C.rccl_unique_id()]
+            except Exception as e:  # noqa: BLE001 - agreed below; the broadcast still runs
+                err = f"ncclGetUniqueId: {e}"
         dist.broadcast_object_list(box, src=r * tp)
         uids.append(box[0])
+    try:
+        torch.cuda.set_device(torch.cuda.current_device())
+        torch.cuda.synchronize()
+    except Exception as e:  # noqa: BLE001
+        err = err or f"device: {e}"
     r = rank // tp
+    if uids[r] is None:
+        err = err or "no unique id from the replica leader"
+    ok = torch.tensor([0 if err else 1], dtype=torch.int32)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if not int(ok[0]):
+        raise RuntimeError(f"rank {rank}: RCCL pre-init check failed ({err or 'on a peer'})")
     comm = C.RcclComm(uids[r], tp, rank - r * tp, torch.cuda.current_device())
     t = torch.full((4,), float(rank - r * tp + 1), dtype=torch.float32, device="cuda")
     comm.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), C.rccl_dtypes["float32"],

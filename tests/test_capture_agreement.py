@@ -63,3 +63,57 @@ def test_capture_failure_on_one_rank_is_agreed(tmp_path):
                 p.kill()
     assert isinstance(got[0], list) and got[0] == got[1], got
     assert [p.exitcode for p in procs] == [0, 0]
+
+
+def _preinit_worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    try:
+        import torch.distributed as dist
+
+        from llmss_amd.parallel import dist as D
+
+        dist.init_process_group("gloo", rank=rank, world_size=2)
+        fail = rank == 1
+        real = torch.cuda.set_device
+        if fail:  # rank 1's device step fails; rank 0's succeeds (stubbed: no GPU here)
+            torch.cuda.set_device = lambda *a: (_ for _ in ()).throw(RuntimeError("no device"))
+        else:
+            torch.cuda.set_device = lambda *a: None
+            torch.cuda.synchronize = lambda *a: None
+        torch.cuda.current_device = lambda: 0
+        try:
+            D._native_comm(rank, 1, 2)
+            q.put((rank, "returned"))
+        except RuntimeError as e:
+            q.put((rank, str(e)))
+        finally:
+            torch.cuda.set_device = real
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, "unexpected " + repr(e)))
+
+
+def test_rccl_preinit_failure_on_one_rank_raises_on_all():
+    """parallel/dist.py _native_comm: a rank whose pre-init step fails (here its device) makes EVERY rank raise
+    before ncclCommInitRank, instead of leaving the healthy rank blocked in the init."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_preinit_worker, args=(i, port, q)) for i in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        got = dict(q.get(timeout=120) for _ in range(2))
+        for p in procs:
+            p.join(60)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    assert "pre-init check failed (device: no device)" in got[1], got
+    assert "pre-init check failed (on a peer)" in got[0], got
