@@ -2,11 +2,12 @@
 // each configuration runs as MODE 0 (the kernel), 1 (staging loads only, no MFMA), 2 (MFMAs only, no loads)
 // and 3 (no epilogue stores), 20 launches per HIP graph, weights rotated over > 512 MB of copies.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../llmss_amd/csrc midm_probe.hip -o midm_probe
-// Run:   ./midm_probe            (one line per shape x tile x depth x split x mode)
+// Run:   ./midm_probe [tp1]      (one line per shape x tile x depth x split x mode; tp1: Llama-2-7B TP=1 at M=64)
 #include "gemm_mid.hip"
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                   \
@@ -47,17 +48,25 @@ struct Cfg {
     }                                                                                                        \
   }
 
-int main() {
-  const Shape shapes[] = {{"qkv", 512, 1536, 4096}, {"o", 512, 4096, 512}, {"up", 512, 2752, 4096},
-                          {"down", 512, 4096, 1376}};
-  const Cfg cfgs[] = {CFG("64x128", 64, 128, 1, 4, 4), CFG("128x128", 128, 128, 2, 2, 3),
-                      CFG("128x128", 128, 128, 2, 2, 5), CFG("256x128", 256, 128, 4, 2, 3),
-                      CFG("128x256", 128, 256, 2, 4, 3)};
-  const int splits[] = {1, 2, 4, 8};
+int main(int argc, char** argv) {
+  // default: the TP=8 shard of Llama-2-7B at M = 512; "tp1": Llama-2-7B TP=1 decode at M = 64
+  const bool tp1 = argc > 1 && std::string(argv[1]) == "tp1";
+  const Shape shapes8[] = {{"qkv", 512, 1536, 4096}, {"o", 512, 4096, 512}, {"up", 512, 2752, 4096},
+                           {"down", 512, 4096, 1376}};
+  const Shape shapes1[] = {{"qkv", 64, 12288, 4096}, {"o", 64, 4096, 4096}, {"up", 64, 22016, 4096},
+                           {"down", 64, 4096, 11008}};
+  const Cfg cfgs8[] = {CFG("64x128", 64, 128, 1, 4, 4), CFG("128x128", 128, 128, 2, 2, 3),
+                       CFG("128x128", 128, 128, 2, 2, 5), CFG("256x128", 256, 128, 4, 2, 3),
+                       CFG("128x256", 128, 256, 2, 4, 3)};
+  const Cfg cfgs1[] = {CFG("64x192", 64, 192, 2, 2, 3), CFG("64x96", 64, 96, 4, 1, 3), CFG("64x96", 64, 96, 4, 1, 4),
+                       CFG("64x128", 64, 128, 1, 4, 3), CFG("64x256", 64, 256, 1, 4, 3), CFG("64x32", 64, 32, 4, 1, 4),
+                       CFG("64x32", 64, 32, 4, 1, 6)};
+  const int splits8[] = {1, 2, 4, 8};
+  const int splits1[] = {1, 2, 4};
   hipStream_t st;
   CK(hipStreamCreate(&st));
-  const size_t maxw = (size_t)4096 * 4096;  // elements of the largest weight
-  const int ncopy = 48;                     // 48 x >= 11 MB > 512 MB for every shape but o (4 MB: 200 MB)
+  const size_t maxw = tp1 ? (size_t)22016 * 4096 : (size_t)4096 * 4096;  // elements of the largest weight
+  const int ncopy = tp1 ? 8 : 48;  // > 512 MB of rotating weight copies for the large shapes
   std::vector<bf16_t*> ws(ncopy);
   for (auto& w : ws) {
     CK(hipMalloc(&w, maxw * 2));
@@ -65,18 +74,22 @@ int main() {
   }
   bf16_t *X, *Y;
   float* part;
-  CK(hipMalloc(&X, (size_t)512 * 4096 * 2));
-  CK(hipMemset(X, 0x3c, (size_t)512 * 4096 * 2));
-  CK(hipMalloc(&Y, (size_t)512 * 4096 * 2));
-  CK(hipMalloc(&part, (size_t)8 * 512 * 4096 * 4));
+  CK(hipMalloc(&X, (size_t)512 * 11008 * 2));
+  CK(hipMemset(X, 0x3c, (size_t)512 * 11008 * 2));
+  CK(hipMalloc(&Y, (size_t)512 * 22016 * 2));
+  CK(hipMalloc(&part, (size_t)8 * 512 * 22016 * 4));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const int iters = 24;
+  std::vector<Shape> shapes(tp1 ? std::begin(shapes1) : std::begin(shapes8), tp1 ? std::end(shapes1) : std::end(shapes8));
+  std::vector<Cfg> cfgs(tp1 ? std::begin(cfgs1) : std::begin(cfgs8), tp1 ? std::end(cfgs1) : std::end(cfgs8));
+  std::vector<int> splits(tp1 ? std::begin(splits1) : std::begin(splits8), tp1 ? std::end(splits1) : std::end(splits8));
   for (const auto& s : shapes) {
     for (const auto& c : cfgs) {
       for (int split : splits) {
         if ((s.K / 64) / split < 2) continue;
+        if ((size_t)s.N * s.K > maxw) continue;
         printf("%-5s M=%d N=%d K=%d %-8s ns=%d split=%d:", s.name, s.M, s.N, s.K, c.tile, c.ns, split);
         for (int mode = 0; mode < 4; ++mode) {
           hipGraph_t g;
