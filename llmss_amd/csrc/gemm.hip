@@ -714,7 +714,8 @@ __device__ __forceinline__ f32x4 mfma_f8x2(s16x8 a0, s16x8 a1, s16x8 b0, s16x8 b
 // MFMAs of the first k-half: +3-6 % at M = 2048 / 8192. Measured and not taken: the second k-half's reads
 // as one block under the first k-half's MFMAs (no change), reading the next K-tile's first k-half under
 // this one's second (prefetch distance 1 K-tile instead of 1.5: -6 %), restaging right after the fragment
-// reads (distance ~1.8: 0-3 % slower).
+// reads (distance ~1.8: 0-3 % slower), reading the next K-tile's first-half fragments under this one's
+// second-half MFMAs with both interleaved (distance 1: equal at M = 8192, -9 % on one shape at 2048).
 template <bool F8>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict__ A, int64_t lda,
                                                           const void* __restrict__ B, int64_t ldb,
