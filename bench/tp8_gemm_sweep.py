@@ -33,6 +33,8 @@ def family(nt: int) -> str:
         tag += "+sk"
     if flags & 256:
         tag += "+comb"
+    if flags & 512:
+        tag += "+ilv"
     return tag
 
 

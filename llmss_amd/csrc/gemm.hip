@@ -1245,8 +1245,9 @@ __global__ __launch_bounds__(256) void gemm_f8f8_kernel(const unsigned char* __r
 bool gemm_mid_dims(int tsel, int* bm, int* bn, int* threads);
 void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
-                     int split, hipStream_t st, bool packed, int* cnt, const QkvEpi* qe, const float* xs,
-                     const float* wsc);
+                     int split, hipStream_t st, bool packed = false, int* cnt = nullptr,
+                     const QkvEpi* qe = nullptr, const float* xs = nullptr, const float* wsc = nullptr,
+                     bool ilv = false);
 
 // tile: 1 = 128x128, 2 = 64x128, 3 = 64x64; ring depth 2-4; split-K over grid.y; 8-13: the gemm_mid tiles
 // (buffer-descriptor staging, csrc/gemm_mid.hip, fp8 MFMA variant; K % 128 == 0)
@@ -1519,10 +1520,6 @@ static int tiles_of(int M, int N, int bm, int bn) { return ((M + bm - 1) / bm) *
 // tsel: 1 = 128x128, 2 = 64x128, 3 = 64x64 (4 waves); 5 = 256x128, 6 = 256x64 (8 waves, 1 WG/CU);
 // 4 = the big-tile kernel
 bool gemm_mid_dims(int tsel, int* bm, int* bn, int* threads);
-void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
-                     const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
-                     int split, hipStream_t st, bool packed = false, int* cnt = nullptr,
-                     const QkvEpi* qe = nullptr, const float* xs = nullptr, const float* wsc = nullptr);
 
 // tsel 8-12: gemm_mid (gemm_mid.hip: buffer-descriptor staging, 128x128 / 256x128 / 64x256 / 64x128 / 128x256)
 static int tile_dims(int tsel, int* bm, int* bn) {
@@ -1694,7 +1691,7 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   dim3 grid(nt, s);
   if (tsel >= 7 && tsel <= 15) {  // gemm_mid tiles (7, 8-15)
     launch_gemm_mid(tsel, ns, wnt_ok(tsel_raw, M, tsel), X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, part, M, N, K,
-                    act_k, glu_k, s, st, false, cnt, qe);
+                    act_k, glu_k, s, st, false, cnt, qe, nullptr, nullptr, (tsel_raw & 512) != 0);
     if (cnt) return 0;
     if (s > 1 && partial_out && !g && act == 0) return s;
     if (s > 1) {

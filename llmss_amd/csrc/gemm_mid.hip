@@ -29,7 +29,13 @@
 // epilogue (or the split-K slabs / combine, which are linear in them).
 // MODE (bench/proto/midm_probe.hip only; the library instantiates 0): 1 = loads without MFMAs, 2 = MFMAs on
 // whatever LDS holds without loads, 3 = no epilogue stores - to take a tile's time apart.
-template <int BM, int BN, int WM, int WN, int NS, bool WNT, bool PK, bool F8 = false, int MODE = 0>
+// ILV (bf16 row-major, >= 3 stages, K % 64 == 0; hint bit 512 of launch_gemm, chosen by the autotuner): the
+// k-steps overlap their LDS traffic with the MFMAs instead of running reads -> MFMAs per k-half behind a
+// barrier - the second k-half's fragment reads are issued between the first k-half's MFMAs, and the next
+// k-step's first-half reads plus the ring stage issue between the second k-half's MFMAs (one barrier per
+// k-step, moved to the middle of it; the stage issue moves half a k-step later). For M >= 128 tiles, where a
+// k-step carries 16-64 MFMAs per wave and the MFMA-only time is 60-80 % of the kernel (profiles/r4_gemm).
+template <int BM, int BN, int WM, int WN, int NS, bool WNT, bool PK, bool F8 = false, int MODE = 0, bool ILV = false>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                               const bf16_t* __restrict__ B, int64_t ldb,
                                                               const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
@@ -170,17 +176,127 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
 #pragma unroll
   for (int j = 0; j < NS - 1; ++j)
     if (t0 + j < t1) MID_STAGE(t0 + j, smem + j * STAGE);
+  // wait until at most `younger` (clamped to NS - 2) stages of LOADS loads are still in flight
+  auto ring_wait = [&](int younger) {
+    if (NS >= 6 && younger >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * LOADS) : "memory");
+    else if (NS >= 5 && younger >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * LOADS) : "memory");
+    else if (NS >= 4 && younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
+    else if (NS >= 3 && younger >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  if constexpr (ILV) {
+    static_assert(NS >= 3 && !F8 && !PK && MODE == 0, "interleaved ring: bf16 row-major weights, >= 3 stages");
+    static_assert((NS - 3) * LOADS <= 63, "vmcnt immediate");
+    constexpr int RPG = (MT + NT + MT - 1) / MT;  // fragment reads per group of NT MFMAs
+    constexpr int LPG = (LOADS + MT - 1) / MT;    // ring loads per group
+    // s_waitcnt vmcnt((NS - 3) * LOADS) lgkmcnt(0) through the builtin (the wait-count pass sees it): stage t+1
+    // landed with stages up to t+NS-2 in flight, and this wave's fragment reads are done
+    constexpr int VN = (NS - 3) * LOADS;
+    constexpr int WAIT_MID = (VN & 15) | (7 << 4) | ((VN >> 4) << 14);
+    // load l (< LOADS) of a ring stage: A rows first, then B rows
+#define MID_LOAD1(L_, T_, SA_)                                                                                   \
+  do {                                                                                                           \
+    const int so_ = (T_) * 128;                                                                                  \
+    if ((L_) < AL)                                                                                               \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)((SA_) + ((L_) * NW + w) * 1024), 16,            \
+                                               (uint32_t)va[(L_) < AL ? (L_) : 0], (uint32_t)so_, 0, 0);         \
+    else                                                                                                         \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (LDS_AS void*)((SA_) + A_BYTES + ((L_) - AL) * NW * 1024 + w * 1024), \
+                                               16, (uint32_t)vb[(L_) < AL ? 0 : (L_) - AL], (uint32_t)so_, 0,    \
+                                               WNT ? 2 : 0);                                                     \
+  } while (0)
+    s16x8 a0[MT], b0[NT], a1[MT], b1[NT];
+    ring_wait(min(t1 - 1 - t0, NS - 2));  // stage t0 landed ...
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // ... for every wave
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < MT; ++i) a0[i] = *reinterpret_cast<const s16x8*>(smem + aoff0 + i * 2048);
+#pragma unroll
+    for (int i = 0; i < NT; ++i) b0[i] = *reinterpret_cast<const s16x8*>(smem + boff0 + i * 2048);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    int cur = 0, t = t0;
+    // steady state: every k-step issues a stage and reads the next k-step's fragments (one basic block, so
+    // the group barriers can interleave loads, reads and MFMAs)
+    // program order pinned per group (sched_barrier): the ring loads set M0 one after another, which the group
+    // barriers alone do not spread
+    for (; t + NS - 1 < t1; ++t) {
+      const char* st = smem + cur * STAGE;
+      const int nx = cur == NS - 1 ? 0 : cur + 1;
+      const char* sn = smem + nx * STAGE;
+      char* sl = smem + (cur == 0 ? NS - 1 : cur - 1) * STAGE;  // stage t-1's slot: receives stage t+NS-1
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {  // first k-half MFMAs, second-half fragment reads between them
+#pragma unroll
+        for (int r = mt * RPG; r < (mt + 1) * RPG && r < MT + NT; ++r) {
+          if (r < MT) a1[r < MT ? r : 0] = *reinterpret_cast<const s16x8*>(st + aoff1 + (r < MT ? r : 0) * 2048);
+          else b1[r < MT ? 0 : r - MT] = *reinterpret_cast<const s16x8*>(st + boff1 + (r < MT ? 0 : r - MT) * 2048);
+        }
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[mt], b0[nt], acc[mt][nt], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_s_waitcnt(WAIT_MID);
+      __builtin_amdgcn_s_barrier();  // stage t+1 visible; every wave is past its reads of stage t-1
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {  // second k-half MFMAs; the ring loads and next-step reads between them
+#pragma unroll
+        for (int l = mt * LPG; l < (mt + 1) * LPG && l < LOADS; ++l) MID_LOAD1(l, t + NS - 1, sl);
+#pragma unroll
+        for (int r = mt * RPG; r < (mt + 1) * RPG && r < MT + NT; ++r) {
+          if (r < MT) a0[r < MT ? r : 0] = *reinterpret_cast<const s16x8*>(sn + aoff0 + (r < MT ? r : 0) * 2048);
+          else b0[r < MT ? 0 : r - MT] = *reinterpret_cast<const s16x8*>(sn + boff0 + (r < MT ? 0 : r - MT) * 2048);
+        }
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[mt], b1[nt], acc[mt][nt], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // the next k-step's first-half fragments are in registers
+      cur = nx;
+    }
+    // the last NS - 1 k-steps: nothing left to stage
+    for (; t < t1; ++t) {
+      const char* st = smem + cur * STAGE;
+      const int nx = cur == NS - 1 ? 0 : cur + 1;
+      const char* sn = smem + nx * STAGE;
+#pragma unroll
+      for (int i = 0; i < MT; ++i) a1[i] = *reinterpret_cast<const s16x8*>(st + aoff1 + i * 2048);
+#pragma unroll
+      for (int i = 0; i < NT; ++i) b1[i] = *reinterpret_cast<const s16x8*>(st + boff1 + i * 2048);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[mt], b0[nt], acc[mt][nt], 0, 0, 0);
+      if (t + 1 < t1) {
+        ring_wait(t1 - 2 - t);  // stage t+1 landed ...
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();  // ... for every wave
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < MT; ++i) a0[i] = *reinterpret_cast<const s16x8*>(sn + aoff0 + i * 2048);
+#pragma unroll
+        for (int i = 0; i < NT; ++i) b0[i] = *reinterpret_cast<const s16x8*>(sn + boff0 + i * 2048);
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[mt], b1[nt], acc[mt][nt], 0, 0, 0);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      cur = nx;
+    }
+#undef MID_LOAD1
+  } else {
   int cur = 0;
   for (int t = t0; t < t1; ++t) {
     // stage t landed for this wave (younger stages stay in flight), then for every wave
     // stages t+1 .. t+NS-2 may still be in flight: LOADS wave-instructions each
-    const int younger = min(t1 - 1 - t, NS - 2);
     static_assert((NS - 2) * LOADS <= 63, "vmcnt immediate");
-    if (NS >= 6 && younger >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * LOADS) : "memory");
-    else if (NS >= 5 && younger == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * LOADS) : "memory");
-    else if (NS >= 4 && younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
-    else if (NS >= 3 && younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ring_wait(min(t1 - 1 - t, NS - 2));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // raw barrier: in-flight loads survive it
     asm volatile("" ::: "memory");
@@ -199,6 +315,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
     }
     compute(st);
     cur = cur == NS - 1 ? 0 : cur + 1;
+  }
   }
 
 #undef MID_STAGE
@@ -280,7 +397,7 @@ static int mid_depth(int bm, int bn, int want) {
 void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
                      int split, hipStream_t st, bool packed, int* cnt, const QkvEpi* qe, const float* xs,
-                     const float* wsc) {
+                     const float* wsc, bool ilv) {
   const bool f8 = xs != nullptr;
   if (f8 && (packed || !wsc || K % 128)) throw std::runtime_error("gemm_mid fp8: row-major weights, K % 128 == 0");
   const QkvEpi qv = qe ? *qe : QkvEpi{};
@@ -293,6 +410,7 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
   if (packed && (N % 16 || (int64_t)ldw * 64 < K || (int64_t)ldw * 64 >= K + 64))
     throw std::runtime_error("gemm_mid: packed weights need N % 16 == 0 and ldw = ceil(K / 64)");
   const int ns = mid_depth(bm, bn, depth);
+  ilv = ilv && !f8 && !packed && ns >= 3 && K % 64 == 0;  // the interleaved ring's preconditions
   const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   dim3 grid(tiles, split);
 #define MID1(BM_, BN_, WM_, WN_, NS_, WNT_, PK_)                                                                   \
@@ -302,10 +420,16 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
 #define MID1F8(BM_, BN_, WM_, WN_, NS_, WNT_)                                                                      \
   gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, WNT_, false, true><<<grid, 64 * WM_ * WN_, 0, st>>>(                    \
       X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, cnt, qv, xs, wsc)
+#define MID1I(BM_, BN_, WM_, WN_, NS_, WNT_)                                                                       \
+  gemm_mid_kernel<BM_, BN_, WM_, WN_, (NS_ < 3 ? 3 : NS_), WNT_, false, false, 0, true>                              \
+      <<<grid, 64 * WM_ * WN_, 0, st>>>(X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, cnt, qv, nullptr,     \
+                                        nullptr)
 #define MID(BM_, BN_, WM_, WN_, NS_)                                                                             \
   do {                                                                                                         \
     if (f8) {                                                                                                  \
       if (wnt) MID1F8(BM_, BN_, WM_, WN_, NS_, true); else MID1F8(BM_, BN_, WM_, WN_, NS_, false);            \
+    } else if (ilv && NS_ >= 3) {                                                                              \
+      if (wnt) MID1I(BM_, BN_, WM_, WN_, NS_, true); else MID1I(BM_, BN_, WM_, WN_, NS_, false);              \
     } else if (packed) {                                                                                       \
       if (wnt) MID1(BM_, BN_, WM_, WN_, NS_, true, true); else MID1(BM_, BN_, WM_, WN_, NS_, false, true);     \
     } else {                                                                                                   \
@@ -339,5 +463,6 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
 #undef MID
 #undef MID1
 #undef MID1F8
+#undef MID1I
   HIP_CHECK_LAUNCH();
 }

@@ -210,6 +210,31 @@ def test_gemm(M, N, K):
         close(H.linear(x, w, None, glu=True), R.linear(x.float(), w.float(), None, glu=True), 2e-2)
 
 
+@pytest.mark.parametrize("tile", [7, 8, 9, 10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("depth", [16, 32, 48])
+@pytest.mark.parametrize("split", [1, 3])
+@pytest.mark.parametrize("M,N,K", [(200, 1536, 4096), (512, 768, 1024), (130, 4800, 1600), (300, 1312, 64 * 5 + 16)])
+def test_gemm_mid_interleaved_ring(tile, depth, split, M, N, K):
+    """gemm_mid's interleaved ring (hint bit 512, csrc/gemm_mid.hip ILV: second-half fragment reads and the ring
+    stage issue between the MFMAs, one mid-k-step barrier) against the fp32 oracle: every tile and ring depth,
+    split-K, NaN-filled outputs, SwiGLU; a K with a partial last k-step takes the plain ring (fallback)."""
+    torch.manual_seed(0)
+    x, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
+    b = rnd(N, scale=0.1)
+    hint = (tile | depth | 512) << 8
+    y = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=x.device)
+    close(H.linear(x, w, b, act="gelu_tanh", nt_hint=hint, split_hint=split, out=y),
+          R.linear(x.float(), w.float(), b.float(), act="gelu_tanh"), 2e-2)
+    if tile not in ODD_NT_TILES and split == 1:
+        y = torch.full((M, N // 2), float("nan"), dtype=torch.bfloat16, device=x.device)
+        close(H.linear(x, w, None, glu=True, nt_hint=hint, split_hint=split, out=y),
+              R.linear(x.float(), w.float(), None, glu=True), 2e-2)
+    if split > 1:  # split-K combined inside the launch (hint bit 256) behind the interleaved ring
+        y = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=x.device)
+        close(H.linear(x, w, b, nt_hint=hint | (256 << 8), split_hint=split, out=y),
+              R.linear(x.float(), w.float(), b.float()), 2e-2)
+
+
 def test_prompt_batch_library_routing():
     """Plain prompt-batch GEMMs routed to the platform library (ops/hip.py _LIB_PREFILL) give the oracle's result
     with bias, into a given output; SwiGLU / activation calls and decode-sized M stay on the HIP kernels."""
