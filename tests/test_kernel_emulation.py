@@ -136,3 +136,97 @@ def test_packed_weight_layout(N, K):
     assert torch.allclose(R.linear(x, wp), R.linear(x, w))
     with pytest.raises(ValueError):
         R.pack_weight(torch.zeros(24, 64))
+
+
+class _RingModel:
+    """Program-order model of one wave of a ring schedule (all waves run the same program; a barrier means every
+    wave has finished everything before it). Records which stage each LDS slot holds and checks the two ring
+    invariants: a fragment read sees a stage that has landed for every wave (a vmcnt wait that covers it, then a
+    barrier), and no slot is restaged before every wave's reads of its previous stage have completed (an lgkmcnt
+    wait, then a barrier)."""
+
+    def __init__(self, ns):
+        self.ns = ns
+        self.slot = [None] * ns        # stage held by each slot
+        self.issued = []               # stages in issue order
+        self.landed = set()            # stages whose loads this wave has waited for
+        self.visible = set()           # ... and that a barrier since made visible to every wave
+        self.reads = {}                # slot -> "pending" | "done" | "synced" (reads of its current stage)
+
+    def issue(self, stage, slot):
+        assert self.reads.get(slot, "synced") == "synced", f"slot {slot} restaged while reads of stage {self.slot[slot]} may be in flight"
+        self.slot[slot] = stage
+        self.reads[slot] = "synced"
+        self.issued.append(stage)
+
+    def vm_wait(self, younger):
+        # s_waitcnt vmcnt(younger * LOADS): every stage but the `younger` newest ones has landed
+        done = self.issued[:len(self.issued) - younger] if younger else list(self.issued)
+        self.landed.update(done)
+
+    def lgkm_wait(self):
+        for s, st in self.reads.items():
+            if st == "pending":
+                self.reads[s] = "done"
+
+    def barrier(self):
+        self.lgkm_wait()  # every barrier of the kernel is preceded by lgkmcnt(0)
+        self.visible |= self.landed
+        for s, st in self.reads.items():
+            if st == "done":
+                self.reads[s] = "synced"
+
+    def read(self, slot, stage):
+        assert self.slot[slot] == stage, f"slot {slot} holds stage {self.slot[slot]}, expected {stage}"
+        assert stage in self.visible, f"stage {stage} read before it landed for every wave"
+        self.reads[slot] = "pending"
+
+
+def _ilv_schedule(ns, t0, t1):
+    """csrc/gemm_mid.hip gemm_mid_kernel, ILV path: the order of stage issues, waits, barriers and reads."""
+    r = _RingModel(ns)
+    for j in range(ns - 1):
+        if t0 + j < t1:
+            r.issue(t0 + j, j)
+    r.vm_wait(min(t1 - 1 - t0, ns - 2))
+    r.barrier()
+    r.read(0, t0)  # first-half fragments of k-step t0
+    r.lgkm_wait()
+    cur, t = 0, t0
+    while t + ns - 1 < t1:  # steady state
+        nx = 0 if cur == ns - 1 else cur + 1
+        r.read(cur, t)  # second-half fragments (under the first-half MFMAs)
+        r.vm_wait(ns - 3)
+        r.barrier()
+        r.issue(t + ns - 1, ns - 1 if cur == 0 else cur - 1)
+        r.read(nx, t + 1)  # next k-step's first half (under the second-half MFMAs)
+        r.lgkm_wait()
+        cur, t = nx, t + 1
+    while t < t1:  # tail: nothing left to stage
+        nx = 0 if cur == ns - 1 else cur + 1
+        r.read(cur, t)
+        if t + 1 < t1:
+            r.vm_wait(t1 - 2 - t)
+            r.barrier()
+            r.read(nx, t + 1)
+        r.lgkm_wait()
+        cur, t = nx, t + 1
+    return r
+
+
+@pytest.mark.parametrize("ns", [3, 4, 5, 6])
+@pytest.mark.parametrize("nk", [1, 2, 3, 4, 5, 6, 7, 16, 64])
+def test_gemm_mid_interleaved_ring_schedule(ns, nk):
+    """The interleaved ring's slot / wait / barrier order (csrc/gemm_mid.hip ILV) keeps both ring invariants for
+    every depth and k-step count, including split-K slices shorter than the ring."""
+    r = _ilv_schedule(ns, 5, 5 + nk)
+    assert sorted(r.issued) == list(range(5, 5 + nk))
+
+
+def test_ring_model_catches_an_early_restage():
+    """The model is not vacuous: restaging stage t-1's slot before the mid-k-step barrier is caught."""
+    r = _RingModel(3)
+    r.issue(0, 0), r.issue(1, 1)
+    r.vm_wait(1), r.barrier(), r.read(0, 0)
+    with pytest.raises(AssertionError):
+        r.issue(2, 0)
