@@ -1,10 +1,6 @@
 # round 4: gemm_mid interleaved ring (numerics, TP=8 shard sweep), decode twins (numerics, bench A/B)
 set -u
 mkdir -p gpurun_out/r4w
-timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -k "interleaved_ring" -x -q --timeout 120 --timeout-method thread > gpurun_out/r4w/ilv_tests.log 2>&1 || { tail -30 gpurun_out/r4w/ilv_tests.log; exit 1; }
-tail -1 gpurun_out/r4w/ilv_tests.log
-LLMSS_MID_ILV=1 timeout -k 10 500 python -u bench/tp8_gemm_sweep.py --m 512 --top 6 > gpurun_out/r4w/sweep512_ilv.log 2>&1 || { tail -20 gpurun_out/r4w/sweep512_ilv.log; exit 1; }
-grep -h "sum of best\|best per family" gpurun_out/r4w/sweep512_ilv.log | cut -c1-240
 timeout -k 10 300 python -u -m pytest tests/test_engine_gpu.py tests/test_kernels_gpu.py -k "twin or packed" -x -q --timeout 120 --timeout-method thread > gpurun_out/r4w/twin_tests.log 2>&1 || { tail -30 gpurun_out/r4w/twin_tests.log; exit 1; }
 tail -1 gpurun_out/r4w/twin_tests.log
 LLMSS_DECODE_TWIN=qkv,up timeout -k 10 400 python bench.py > gpurun_out/r4w/bench_twin.log 2>&1 || { tail -20 gpurun_out/r4w/bench_twin.log; exit 1; }

@@ -450,7 +450,7 @@ def test_decode_twin_matches_row_major_weights():
     wc = random_weights(cfg, device="cpu", dtype=torch.float32, seed=3, std=0.05)
     m_cpu = DecoderLM(cfg, wc)
     wg = _to_gpu(wc)
-    assert make_decode_twins(wg) == 2 * cfg.num_hidden_layers
+    assert make_decode_twins(wg) == 2 * cfg.num_layers
     m = DecoderLM(cfg, wg)
     V, B, P = cfg.vocab_size, 3, 20
     ids = torch.randint(0, V, (B * P,))
