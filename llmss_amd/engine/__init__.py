@@ -8,8 +8,7 @@ import torch
 
 from ..models.config import ModelConfig, get_preset
 from ..models.decoder import DecoderLM
-from ..models.weights import (load_hf_weights, load_shard, make_decode_twins, pack_linears, random_weights, save_shard,
-                              shard_cache_path)
+from ..models.weights import load_hf_weights, load_shard, pack_linears, random_weights, save_shard, shard_cache_path
 from ..parallel.dist import TPGroup
 from ..utils.checkpoint import CheckpointReader, weight_files
 from .engine import LLMEngine, Request, StepEvent
@@ -63,11 +62,6 @@ def build_model(model: str, tp: Optional[TPGroup] = None, dtype: str = "bf16", d
     # than that on the gemm_mid-only path, so whole-run tokens/s drops 2-8 %
     if device.type == "cuda" and os.environ.get("LLMSS_PACK_WEIGHTS", "0") == "1":
         pack_linears(w)
-    # decode twins of the projections where panels stream faster (qkv, gate/up); the autotuner decides per
-    # decode batch size whether a call reads the twin (ops/autotune.py tune_model). LLMSS_DECODE_TWIN=0: none
-    twins = os.environ.get("LLMSS_DECODE_TWIN", "0")  # off until measured on the GPU
-    if device.type == "cuda" and twins not in ("", "0"):
-        make_decode_twins(w, tuple(t for t in twins.split(",") if t))
     return DecoderLM(cfg, w, tp)
 
 

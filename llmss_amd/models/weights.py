@@ -77,14 +77,9 @@ class Linear:
     w_scale: Optional[torch.Tensor] = None
     glu: bool = False
     k: int = 0
-    # decode twin (make_decode_twins): the same weight panel-packed, streamed by calls whose row count is in
-    # twin_rows (the autotuner puts a decode M there when the packed plan beats the row-major one)
-    wp: Optional[torch.Tensor] = None
-    twin_rows: set = field(default_factory=set)
 
     def __call__(self, x, act="none", partial_ok=False):
-        w = self.wp if self.wp is not None and x.shape[0] in self.twin_rows else self.w
-        return ops.linear(x, w, self.b, act, self.glu, self.w_scale, partial_ok=partial_ok)
+        return ops.linear(x, self.w, self.b, act, self.glu, self.w_scale, partial_ok=partial_ok)
 
     @property
     def packed(self) -> bool:
@@ -105,25 +100,6 @@ class Linear:
     @property
     def out_features(self):
         return self.N // (2 if self.glu else 1)
-
-
-def make_decode_twins(mw: "ModelWeights", names=("qkv", "up")) -> int:
-    """Give the named bf16 projections of every layer a panel-packed twin next to the row-major weight (the
-    HBM cost of one more copy of those weights: ~9 GB for Llama-2-7B's qkv + gate/up, against 288 GB). Prompt
-    batches (hipBLASLt / the 256x256 kernel) keep reading the row-major copy; decode steps stream the twin,
-    whose k-steps are contiguous 2-KiB panel blocks, where the autotuner measures it faster (round 2: the
-    row-major decode pattern streams at 4.7-5.4 TB/s, panels at 6.1-6.25, profiles/r2_packed). Returns the
-    number of twins made."""
-    n = 0
-    for L in mw.layers:
-        for name in names:
-            lin = getattr(L, name)
-            if lin.packed or lin.wp is not None or lin.w_scale is not None or not lin.w.is_cuda \
-                    or lin.w.dtype != torch.bfloat16 or lin.w.shape[0] % 16:
-                continue
-            lin.wp = ref.pack_weight(lin.w)
-            n += 1
-    return n
 
 
 def pack_linears(mw: "ModelWeights") -> int:

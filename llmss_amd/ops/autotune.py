@@ -13,7 +13,6 @@ timed without its reduce and charged the consumer's extra slab reads instead.
 """
 from __future__ import annotations
 
-import dataclasses
 import itertools
 import math
 import os
@@ -28,7 +27,6 @@ from ..utils.logging import get_logger
 log = get_logger(__name__)
 
 _SLAB_READ_BPS = 4.0e12  # consumer-side fp32 partial reads (add_norm / rope), bytes/s
-TWIN_MAX_M = 64  # decode batch sizes up to which a projection's panel-packed twin is timed against its rows
 
 
 @dataclass(frozen=True)
@@ -373,8 +371,6 @@ def tune_model(model, ms: Sequence[int], native=None) -> Dict[Tuple[str, int], T
     res = {}
     done = _DONE
     for name, shp in model_shapes(model).items():
-        lins = [getattr(L, name) for L in model.w.layers] if name != "head" else [model.w.head]
-        twin = lins[0].wp is not None
         for M in sorted(set(int(m) for m in ms)):
             key = (M, shp, str(dev))
             if key not in done:
@@ -383,21 +379,6 @@ def tune_model(model, ms: Sequence[int], native=None) -> Dict[Tuple[str, int], T
             if nt:
                 lib.gemm_tuned_set(M, shp.N, shp.K, shp.glu, 2 if shp.packed else int(shp.fp8), nt, s)
             res[(name, M)] = done[key]
-            if twin and M <= TWIN_MAX_M:  # decode twin (models/weights.py make_decode_twins): panels vs rows
-                pshp = dataclasses.replace(shp, packed=True)
-                pkey = (M, pshp, str(dev))
-                if pkey not in done:
-                    done[pkey] = tune_shape(M, pshp, dev)
-                pnt, ps, pt, _ = done[pkey]
-                if pt < 0.98 * t:
-                    if pnt:
-                        lib.gemm_tuned_set(M, shp.N, shp.K, shp.glu, 2, pnt, ps)
-                    for lin in lins:
-                        lin.twin_rows.add(M)
-                    res[(name + "_twin", M)] = (pnt, ps, pt, t)
-                else:
-                    for lin in lins:
-                        lin.twin_rows.discard(M)
     if os.environ.get("LLMSS_QKV_EPI", "1") != "0":
         key = ("qkv_epi", tuple(sorted(set(int(m) for m in ms))), model_shapes(model)["qkv"], str(dev),
                model.cfg.head_dim, model.cfg.rotary_dim, model.cfg.rope_style, model.cfg.position)

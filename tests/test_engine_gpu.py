@@ -438,40 +438,3 @@ def test_pipelined_decode_across_kv_block_boundaries():
             assert eng.stats.get("spec_block_reserves", 0) > 0
     assert outs[0] == outs[1]
 
-
-def test_decode_twin_matches_row_major_weights():
-    """Decode twins (models/weights.py make_decode_twins): a decode step whose qkv / gate-up calls stream the
-    panel-packed twin gives the logits of the row-major weights (and the fp32 reference), and prompt-batch calls
-    keep the row-major copy."""
-    from llmss_amd.models.weights import make_decode_twins
-
-    cfg = get_preset("tiny-llama", hidden_size=256, num_heads=4, num_kv_heads=2, head_dim=64, rotary_dim=64,
-                     intermediate_size=512, max_position_embeddings=256)
-    wc = random_weights(cfg, device="cpu", dtype=torch.float32, seed=3, std=0.05)
-    m_cpu = DecoderLM(cfg, wc)
-    wg = _to_gpu(wc)
-    assert make_decode_twins(wg) == 2 * cfg.num_layers
-    m = DecoderLM(cfg, wg)
-    V, B, P = cfg.vocab_size, 3, 20
-    ids = torch.randint(0, V, (B * P,))
-    cu = torch.arange(B + 1, dtype=torch.int32) * P
-    pos = torch.arange(P).repeat(B)
-    slots = torch.cat([torch.arange(P) + 32 * b for b in range(B)])
-    pre = dict(kind="prefill", input_ids=ids, positions=pos, slots=slots, cu_seqlens=cu, max_seqlen=P)
-    bt = torch.tensor([[2 * b, 2 * b + 1] for b in range(B)], dtype=torch.int32)
-    dec = dict(kind="decode", input_ids=torch.randint(0, V, (B,)), positions=torch.full((B,), P),
-               slots=torch.tensor([32 * b + P for b in range(B)]), block_tables=bt,
-               ctx_lens=torch.full((B,), P + 1, dtype=torch.int32), max_ctx=32)
-    kv_c = m_cpu.allocate_kv_cache(8, 16)
-    m_cpu(StepInput(**pre), kv_c)
-    ref = m_cpu(StepInput(**dec), kv_c)[:, :V]
-    outs = {}
-    for use in (False, True):
-        for L in wg.layers:
-            for lin in (L.qkv, L.up):
-                lin.twin_rows = {B} if use else set()
-        kv = m.allocate_kv_cache(8, 16)
-        m(StepInput(**{k: (v.cuda() if torch.is_tensor(v) else v) for k, v in pre.items()}), kv)
-        outs[use] = m(StepInput(**{k: (v.cuda() if torch.is_tensor(v) else v) for k, v in dec.items()}), kv)[:, :V]
-    _assert_logits_close(outs[True].float().cpu(), ref)
-    _assert_logits_close(outs[True].float().cpu(), outs[False].float().cpu())
