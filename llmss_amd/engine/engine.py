@@ -20,7 +20,6 @@ from __future__ import annotations
 
 import collections
 import contextlib
-import gc
 import math
 import os
 import time
@@ -227,12 +226,6 @@ class LLMEngine:
         if self.use_graphs and os.environ.get("LLMSS_GRAPHS", "1") == "0":
             self.use_graphs = False
         self._capture_agreed()
-        if self.is_gpu and os.environ.get("LLMSS_GC_FREEZE", "1") != "0":
-            # the model, KV pool, plans and graphs live as long as the process: move them out of the cyclic
-            # collector's generations, so a full collection during serving scans only per-request objects
-            # (served GPT-2-XL steps showed ~110-130 ms stalls on 2 of 20 steps without it)
-            gc.collect()
-            gc.freeze()
 
     def _capture_agreed(self):
         """Capture the decode graphs, agreeing on the outcome across TP ranks: if capture fails on ANY rank

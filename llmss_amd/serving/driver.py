@@ -28,6 +28,7 @@ ranks on several hosts fall back to it automatically.
 """
 from __future__ import annotations
 
+import gc
 import os
 import queue
 import threading
@@ -300,6 +301,12 @@ class EngineDriver:
         raise RuntimeError(f"injected fault at step {step}")
 
     def run(self):
+        if self.engine.is_gpu and os.environ.get("LLMSS_GC_FREEZE", "1") != "0":
+            # a serving process keeps its model, KV pool, plans and graphs for its lifetime: move them out of
+            # the cyclic collector's generations so a full collection while serving scans only per-request
+            # objects (served GPT-2-XL steps showed ~110-130 ms stalls on 2 of 20 steps)
+            gc.collect()
+            gc.freeze()
         try:
             self._run()
         except Exception as e:  # noqa: BLE001 - a dead peer, a collective timeout, a kernel error
