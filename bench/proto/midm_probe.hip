@@ -2,7 +2,8 @@
 // each configuration runs as MODE 0 (the kernel), 1 (staging loads only, no MFMA), 2 (MFMAs only, no loads)
 // and 3 (no epilogue stores), 20 launches per HIP graph, weights rotated over > 512 MB of copies.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../llmss_amd/csrc midm_probe.hip -o midm_probe
-// Run:   ./midm_probe [tp1]      (one line per shape x tile x depth x split x mode; tp1: Llama-2-7B TP=1 at M=64)
+// Run:   ./midm_probe [tp1|gpt2] (one line per shape x tile x depth x split x mode; tp1: Llama-2-7B TP=1 at
+//        M=64; gpt2: GPT-2-XL at M=64)
 #include "gemm_mid.hip"
 
 #include <cstdio>
@@ -51,6 +52,7 @@ struct Cfg {
 int main(int argc, char** argv) {
   // default: the TP=8 shard of Llama-2-7B at M = 512; "tp1": Llama-2-7B TP=1 decode at M = 64
   const bool tp1 = argc > 1 && std::string(argv[1]) == "tp1";
+  const bool gpt2 = argc > 1 && std::string(argv[1]) == "gpt2";  // GPT-2-XL TP=1 decode at M = 64
   const Shape shapes8[] = {{"qkv", 512, 1536, 4096}, {"o", 512, 4096, 512}, {"up", 512, 2752, 4096},
                            {"down", 512, 4096, 1376}};
   const Shape shapes1[] = {{"qkv", 64, 12288, 4096}, {"o", 64, 4096, 4096}, {"up", 64, 22016, 4096},
@@ -65,7 +67,7 @@ int main(int argc, char** argv) {
   const int splits1[] = {1, 2, 4};
   hipStream_t st;
   CK(hipStreamCreate(&st));
-  const size_t maxw = tp1 ? (size_t)22016 * 4096 : (size_t)4096 * 4096;  // elements of the largest weight
+  const size_t maxw = tp1 ? (size_t)22016 * 4096 : (size_t)6400 * 1600 > (size_t)4096 * 4096 ? (size_t)6400 * 1600 : (size_t)4096 * 4096;
   const int ncopy = tp1 ? 8 : 48;  // > 512 MB of rotating weight copies for the large shapes
   std::vector<bf16_t*> ws(ncopy);
   for (auto& w : ws) {
@@ -82,9 +84,19 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const int iters = 24;
+  const Shape shapesg[] = {{"qkv", 64, 4800, 1600}, {"o", 64, 1600, 1600}, {"up", 64, 6400, 1600},
+                           {"down", 64, 1600, 6400}};
+  const Cfg cfgsg[] = {CFG("64x32", 64, 32, 4, 1, 3), CFG("64x32", 64, 32, 4, 1, 4), CFG("64x32", 64, 32, 4, 1, 6),
+                       CFG("64x48", 64, 48, 2, 1, 4), CFG("64x48", 64, 48, 2, 1, 6), CFG("64x96", 64, 96, 4, 1, 4)};
+  const int splitsg[] = {1, 2, 3, 4, 6, 8};
   std::vector<Shape> shapes(tp1 ? std::begin(shapes1) : std::begin(shapes8), tp1 ? std::end(shapes1) : std::end(shapes8));
   std::vector<Cfg> cfgs(tp1 ? std::begin(cfgs1) : std::begin(cfgs8), tp1 ? std::end(cfgs1) : std::end(cfgs8));
   std::vector<int> splits(tp1 ? std::begin(splits1) : std::begin(splits8), tp1 ? std::end(splits1) : std::end(splits8));
+  if (gpt2) {
+    shapes.assign(std::begin(shapesg), std::end(shapesg));
+    cfgs.assign(std::begin(cfgsg), std::end(cfgsg));
+    splits.assign(std::begin(splitsg), std::end(splitsg));
+  }
   for (const auto& s : shapes) {
     for (const auto& c : cfgs) {
       for (int split : splits) {
