@@ -44,8 +44,7 @@ __device__ __forceinline__ float token_sum(float s) {
 // KV8: the paged cache holds fp8 rows (D e4m3 bytes + fp32 scale at byte D, 16-B tail; reference.py
 // kv_rows_quant): each lane loads 8 bytes per token instead of 16 and the row scales multiply the score
 // (K) and the probability (V) instead of every element.
-// NT: K / V rows are read non-temporally (read once per step); false: default cache policy (unroll codes 21 / 22)
-template <int D, int GB, int UNROLL, bool PIPE = false, bool KV8 = false, bool NT = true>
+template <int D, int GB, int UNROLL, bool PIPE = false, bool KV8 = false>
 __global__ __launch_bounds__(256, GB == 1 ? 8 : 1) void attn_decode_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, void* __restrict__ kcv, void* __restrict__ vcv,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, bf16_t* __restrict__ out,
@@ -133,13 +132,8 @@ __global__ __launch_bounds__(256, GB == 1 ? 8 : 1) void attn_decode_kernel(
         r.ks[u] = *reinterpret_cast<const float*>(kc8 + a - sub * 8 + D);
         r.vs[u] = *reinterpret_cast<const float*>(vc8 + a - sub * 8 + D);
       } else {
-        if constexpr (NT) {
-          r.k[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(kc + a));
-          r.v[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(vc + a));
-        } else {
-          r.k[u] = *reinterpret_cast<const u16x8*>(kc + a);
-          r.v[u] = *reinterpret_cast<const u16x8*>(vc + a);
-        }
+        r.k[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(kc + a));
+        r.v[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(vc + a));
       }
     }
   };
@@ -281,9 +275,7 @@ __global__ __launch_bounds__(256) void attn_decode_reduce_kernel(const float* __
 // default 11 (measured, bench/attn_bench.py, cold KV, B = 64: best or within 1% of best for MHA at
 // 192 / 1024 tokens and 12-17% ahead for GQA groups of 4)
 static int g_decode_unroll = 11;
-void attn_decode_set_unroll(int u) {
-  g_decode_unroll = (u == 1 || u == 2 || u == 4 || u == 11 || u == 12 || u == 14 || u == 21 || u == 22) ? u : 11;
-}
+void attn_decode_set_unroll(int u) { g_decode_unroll = (u == 1 || u == 2 || u == 4 || u == 11 || u == 12 || u == 14) ? u : 11; }
 
 template <int D, int GB>
 static void launch_decode_t(const bf16_t* q, int64_t qs, bf16_t* kc, bf16_t* vc, const int* bt, int bts,
@@ -293,10 +285,9 @@ static void launch_decode_t(const bf16_t* q, int64_t qs, bf16_t* kc, bf16_t* vc,
   const int ngroups = (G + GB - 1) / GB;
   dim3 grid(B, nkv * ngroups, nsplit);
   const float sl2 = scale * kLog2e;
-#define AD(U_, PIPE_, KV8_, ...)                                                                                 \
-  attn_decode_kernel<D, GB, U_, PIPE_, KV8_, ##__VA_ARGS__><<<grid, 256, 0, st>>>(q, qs, kc, vc, bt, bts, cl, out, os, \
-                                                                                 po, pml, nh, nkv, G, ngroups, bs, \
-                                                                                 psize, sl2)
+#define AD(U_, PIPE_, KV8_)                                                                                      \
+  attn_decode_kernel<D, GB, U_, PIPE_, KV8_><<<grid, 256, 0, st>>>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, nh, \
+                                                                  nkv, G, ngroups, bs, psize, sl2)
   if (kv8) {
     switch (g_decode_unroll) {
       case 2: AD(2, false, true); break;
@@ -310,8 +301,6 @@ static void launch_decode_t(const bf16_t* q, int64_t qs, bf16_t* kc, bf16_t* vc,
       case 4: AD(4, false, false); break;
       case 12: AD(2, true, false); break;
       case 14: AD(4, true, false); break;
-      case 21: AD(1, true, false, false); break;  // 11 with default-policy K / V loads
-      case 22: AD(2, false, false, false); break;  // 2 with default-policy K / V loads
       default: AD(1, true, false); break;
     }
   }

@@ -291,15 +291,7 @@ def decode_splits(B: int, nkv: int, max_ctx: int, block_size: int) -> tuple:
     return nsplit, psize
 
 
-_ATTN_UNROLL_SET = False
-
-
 def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale, max_ctx, out=None, splits=None):
-    global _ATTN_UNROLL_SET
-    if not _ATTN_UNROLL_SET:  # LLMSS_ATTN_UNROLL: the decode kernel's token-loop variant (csrc attn_decode_set_unroll)
-        _ATTN_UNROLL_SET = True
-        if os.environ.get("LLMSS_ATTN_UNROLL"):
-            lib().attn_decode_set_unroll(int(os.environ["LLMSS_ATTN_UNROLL"]))
     B = q.shape[0]
     _check(q.is_cuda and q.dtype == torch.bfloat16 and q.stride(-1) == 1 and q.dim() == 2, "q [B, >=nh*D]")
     _check(q.shape[1] >= nh * D, "q too narrow")

@@ -189,7 +189,7 @@ def test_attn_decode(D, nh, nkv, B, maxctx):
     out1 = H.attn_decode(q, kc, vc, perm, ctx, nh, nkv, D, sc, maxctx, splits=(1, maxb * bs))
     close(out1, ref, 2e-2)
     try:  # every token-loop variant (1 / 2 / 4 tokens per slot, single or double register set)
-        for u in (1, 2, 4, 12, 14, 21, 22):
+        for u in (1, 2, 4, 12, 14):
             H.lib().attn_decode_set_unroll(u)
             close(H.attn_decode(q, kc, vc, perm, ctx, nh, nkv, D, sc, maxctx), ref, 2e-2)
             close(H.attn_decode(q, kc, vc, perm, ctx, nh, nkv, D, sc, maxctx, splits=(1, maxb * bs)), ref, 2e-2)
