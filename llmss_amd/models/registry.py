@@ -216,4 +216,36 @@ class Weights:
         return self.get_sharded(f"{prefix}.weight", dim=1)
 
 
-MODEL_REGISTRY = {"gpt2": CausalLM, "gptj": CausalLM, "gpt_bigcode": CausalLM, "llama": CausalLM}
+class _FamilyLM(CausalLM):
+    """A :class:`CausalLM` bound to one checkpoint family: the reference's per-family class names
+    (``custom_modeling/__init__.py:1-2``), rejecting a config of another ``model_type``."""
+
+    model_type = ""
+
+    def __init__(self, config, weights, max_blocks: int = 4096, block_size: int = 16):
+        mt = config.model_type if isinstance(config, ModelConfig) else getattr(config, "model_type", None)
+        if mt != self.model_type:
+            raise ValueError(f"{type(self).__name__} takes model_type {self.model_type!r}, got {mt!r}")
+        super().__init__(config, weights, max_blocks, block_size)
+
+
+class GPTJForCausalLM(_FamilyLM):
+    """Reference ``gptj_modeling.py:514`` (interleaved-pair rotary, parallel attention + MLP block)."""
+    model_type = "gptj"
+
+
+class GPTBigCodeForCausalLM(_FamilyLM):
+    """Reference ``gpt_bigcode_modeling.py:786`` (multi-query attention, fused ``c_attn``)."""
+    model_type = "gpt_bigcode"
+
+
+class GPT2LMHeadModel(_FamilyLM):
+    model_type = "gpt2"
+
+
+class LlamaForCausalLM(_FamilyLM):
+    model_type = "llama"
+
+
+MODEL_REGISTRY = {c.model_type: c for c in (GPT2LMHeadModel, GPTJForCausalLM, GPTBigCodeForCausalLM,
+                                            LlamaForCausalLM)}
