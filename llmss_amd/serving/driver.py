@@ -62,6 +62,11 @@ class Handle:
     # on_token; a unary request just accumulates output_ids (no per-token queue hop)
     stream: bool = False
     on_token: Optional[Callable[["Handle", int], None]] = None
+    # batched delivery (gRPC streams): the step's tokens of every handle sharing a sink go to ONE
+    # sink([(sink_q, token), ...]) call after the step, the finish marker as (sink_q, None) in order after
+    # the handle's last token - one cross-thread wake-up per step instead of one per request
+    sink: Optional[Callable[[list], None]] = None
+    sink_q: object = None
     t_submit: float = field(default_factory=time.perf_counter)
     deadline: Optional[float] = None  # perf_counter time after which the request is aborted
     error: str = ""
@@ -109,6 +114,7 @@ class EngineDriver:
                 dist.new_group(backend="gloo", timeout=timedelta(seconds=leader_timeout_s))
         self.inbox: "queue.Queue" = queue.Queue()
         self.handles: Dict[int, Handle] = {}
+        self._pending: Optional[dict] = None  # sink -> [(sink_q, token | None)] while a step's events are handed out
         self._next = 0
         self._stop = False
         self._thread: Optional[threading.Thread] = None
@@ -177,14 +183,16 @@ class EngineDriver:
     # --------------------------------------------------------------------- leader API
     def submit(self, prompt_ids: List[int], params: SamplingParams,
                on_done: Optional[Callable[[Handle], None]] = None, deadline_s: Optional[float] = None,
-               stream: bool = False, on_token: Optional[Callable[[Handle, int], None]] = None) -> Handle:
+               stream: bool = False, on_token: Optional[Callable[[Handle, int], None]] = None,
+               sink: Optional[Callable[[list], None]] = None, sink_q=None) -> Handle:
         if not self.leader:
             raise RuntimeError("submit() is only valid on rank 0")
         params.resolved_seed()  # fix the seed on the leader so every rank uses the same one
         with self._lock:
             rid = self._next
             self._next += self._rid_stride
-        h = Handle(rid, list(prompt_ids), params, on_done=on_done, stream=stream, on_token=on_token)
+        h = Handle(rid, list(prompt_ids), params, on_done=on_done, stream=stream, on_token=on_token, sink=sink,
+                   sink_q=sink_q)
         if deadline_s is not None:
             h.deadline = h.t_submit + deadline_s
         if self.error is not None:  # the driver already failed: refuse instead of queueing forever
@@ -365,17 +373,25 @@ class EngineDriver:
             events = eng.step()
             steps += 1
             if self.leader:
-                for ev in events:
-                    h = self.handles.get(ev.req_id)
-                    if h is None:
-                        continue
-                    h.output_ids.append(ev.token)
-                    if h.stream:
-                        h.tokens.put(ev.token)
-                    if h.on_token is not None:
-                        h.on_token(h, ev.token)
-                    if ev.finished:
-                        self._complete(h, ev.finish_reason)
+                self._pending = {}
+                try:
+                    for ev in events:
+                        h = self.handles.get(ev.req_id)
+                        if h is None:
+                            continue
+                        h.output_ids.append(ev.token)
+                        if h.stream:
+                            h.tokens.put(ev.token)
+                        if h.on_token is not None:
+                            h.on_token(h, ev.token)
+                        if h.sink is not None:
+                            self._pending.setdefault(h.sink, []).append((h.sink_q, ev.token))
+                        if ev.finished:
+                            self._complete(h, ev.finish_reason)
+                finally:
+                    pending, self._pending = self._pending, None
+                    for sink, items in pending.items():
+                        sink(items)
             for r in eng.pop_finished():
                 pass
 
@@ -386,6 +402,11 @@ class EngineDriver:
             h.metrics = req.metrics()
         if h.stream:
             h.tokens.put(None)
+        if h.sink is not None:
+            if self._pending is not None:  # inside a step: after this handle's last token
+                self._pending.setdefault(h.sink, []).append((h.sink_q, None))
+            else:
+                h.sink([(h.sink_q, None)])
         h.done.set()
         self.handles.pop(h.rid, None)
         if h.on_done is not None:

@@ -180,12 +180,29 @@ def _resolve(fut, value):
         fut.set_result(value)
 
 
+def _fanout(items):
+    for q, t in items:
+        q.put_nowait(t)
+
+
+class _LoopSink:
+    """Driver-thread -> event-loop hand-off of one step's stream tokens in ONE call_soon_threadsafe
+    (``Handle.sink``): 64 streams cost one loop wake-up per step, not 64."""
+
+    def __init__(self, loop):
+        self.loop = loop
+
+    def __call__(self, items):
+        self.loop.call_soon_threadsafe(_fanout, items)
+
+
 class EngineServicer:
     """Direct servicer on the TP leader (coroutine handlers: :func:`serve` runs it on a ``grpc.aio`` server)."""
 
     def __init__(self, driver, tokenizer):
         self.driver = driver
         self.tok = tokenizer
+        self._sinks = {}  # event loop -> _LoopSink
 
     def _prompt_ids(self, req):
         from ..utils.tokenizer import encode
@@ -226,10 +243,11 @@ class EngineServicer:
             await ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, str(e))
         loop = asyncio.get_running_loop()
         q: asyncio.Queue = asyncio.Queue()
-        # tokens and the final None reach the queue in the driver's order (call_soon_threadsafe is FIFO)
-        h = self.driver.submit(self._prompt_ids(req), params, deadline_s=ctx.time_remaining(),
-                               on_token=lambda h_, t: loop.call_soon_threadsafe(q.put_nowait, t),
-                               on_done=lambda h_: loop.call_soon_threadsafe(q.put_nowait, None))
+        sink = self._sinks.get(loop)
+        if sink is None:
+            sink = self._sinks[loop] = _LoopSink(loop)
+        # tokens and the final None reach the queue in the driver's order (one batch per step, batches FIFO)
+        h = self.driver.submit(self._prompt_ids(req), params, deadline_s=ctx.time_remaining(), sink=sink, sink_q=q)
         from ..utils.tokenizer import StreamDecoder
 
         dec = StreamDecoder(self.tok)  # one short-window decode per token, not the whole prefix again

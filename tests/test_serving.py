@@ -267,3 +267,35 @@ def test_grpc_burst_lands_in_one_admission_step(model_dir):
     finally:
         server.stop(0).wait(10)
         drv.stop()
+
+
+def test_stream_sink_batches_one_call_per_step(driver):
+    """Handle.sink: the tokens of all streams sharing a sink arrive as ONE call per engine step, each stream's
+    tokens in order and its end marker (None) after its last token (the gRPC stream servicer's hand-off)."""
+    import threading
+
+    from llmss_amd.utils.tokenizer import encode
+
+    drv, tok, m = driver
+    calls, lock = [], threading.Lock()
+
+    def sink(items):
+        with lock:
+            calls.append(list(items))
+
+    prompts = ["hello world", "this is", "tiny corpus for"]
+    qs = [f"q{i}" for i in range(len(prompts))]
+    hs = [drv.submit(encode(tok, p), SamplingParams(max_new_tokens=4 + i, is_greedy=True), sink=sink, sink_q=q)
+          for i, (p, q) in enumerate(zip(prompts, qs))]
+    for h in hs:
+        assert h.wait(60)
+    per_q = {q: [] for q in qs}
+    for items in calls:
+        for q, t in items:
+            assert not per_q[q] or per_q[q][-1] is not None, "token after the end marker"
+            per_q[q].append(t)
+    for h, q, p, i in zip(hs, qs, prompts, range(len(prompts))):
+        assert per_q[q][-1] is None and per_q[q][:-1] == h.output_ids
+        assert tok.decode(h.output_ids) == _offline(m, tok, p, 4 + i)
+    # fewer hand-offs than tokens: steps batch the streams together
+    assert len(calls) < sum(len(v) for v in per_q.values())
