@@ -14,6 +14,7 @@ Open loop compares scheduling policies: LLMSS_PREFILL_CHUNK=-1 (whole prompts) v
 """
 import argparse
 import concurrent.futures as cf
+import faulthandler
 import json
 import os
 import random
@@ -187,9 +188,11 @@ def main():
     res.update(mode=a.mode, model=a.model, fp8=a.fp8, data="synthetic prompts, random-init weights",
                prefill_chunk=eng.prefill_chunk, engine_stats=eng.stats)
     print(json.dumps(res), flush=True)
-    # orderly shutdown: front-ends first, then the engine thread, then device state
+    # orderly shutdown: front-ends first, then the engine thread, then device state. A teardown that takes
+    # over a minute dumps every thread's stack (a run once went silent here after printing its result)
+    faulthandler.dump_traceback_later(60, exit=False)
     for s in servers:
-        s.stop(0).wait()
+        s.stop(0).wait(60)
     if consumer is not None:
         consumer.stop()
     if mini is not None:
@@ -197,6 +200,7 @@ def main():
     drv.stop()
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    faulthandler.cancel_dump_traceback_later()
 
 
 if __name__ == "__main__":
