@@ -121,8 +121,8 @@ class EngineDriver:
         self._lock = threading.Lock()
         self.idle_wait_s = 0.05
         # admission window: an idle leader that wakes on a request keeps collecting arrivals until none
-        # came for `batch_window_s` (at most 10 windows), so a burst of concurrent clients is admitted in
-        # one prefill step instead of trickling in one by one
+        # came for `batch_window_s` (at most 10 windows) or the arrivals fill the free sequence slots, so a
+        # burst of concurrent clients is admitted in one prefill step instead of trickling in one by one
         self.batch_window_s = float(os.environ.get("LLMSS_ADMIT_WINDOW_S", "0.003"))
         self.batch_window_max = int(os.environ.get("LLMSS_ADMIT_WINDOW_MAX", "10"))
         self.fault = fault if fault is not None else FaultSpec.from_env()
@@ -269,6 +269,10 @@ class EngineDriver:
             item = self.inbox.get(timeout=self.idle_wait_s) if block else self.inbox.get_nowait()
             t_start = time.perf_counter()
             t_end = t_start + self.batch_window_max * self.batch_window_s
+            # a burst that fills every free sequence slot closes the window at once: a later arrival could not
+            # join this prefill step anyway
+            sch = self.engine.sched
+            cap = self.engine.max_num_seqs - sch.num_waiting() - sch.num_running()
             while True:
                 kind, v = item
                 if kind == "new":
@@ -280,7 +284,8 @@ class EngineDriver:
                 try:
                     item = self.inbox.get_nowait()
                 except queue.Empty:
-                    if not (block and self.batch_window_s > 0 and new and not stop) or time.perf_counter() > t_end:
+                    if not (block and self.batch_window_s > 0 and new and not stop) or time.perf_counter() > t_end \
+                            or len(new) >= cap:
                         raise
                     item = self.inbox.get(timeout=self.batch_window_s)
         except queue.Empty:

@@ -299,3 +299,22 @@ def test_stream_sink_batches_one_call_per_step(driver):
         assert tok.decode(h.output_ids) == _offline(m, tok, p, 4 + i)
     # fewer hand-offs than tokens: steps batch the streams together
     assert len(calls) < sum(len(v) for v in per_q.values())
+
+
+def test_admission_window_closes_when_slots_are_full(model_dir):
+    """A burst that fills every free sequence slot is admitted without waiting out the quiet period: nothing that
+    arrives later could join that prefill step."""
+    m = build_model(model_dir, None, "fp32", "cpu")
+    tok = load_tokenizer(model_dir, m.cfg.vocab_size)
+    eng = LLMEngine(m, max_num_seqs=4, block_size=4, num_blocks=128, eos_token_id=None)
+    drv = EngineDriver(eng)
+    drv.batch_window_s = 0.5  # a full burst must not wait this long for more arrivals
+    hs = [drv.submit(encode(tok, f"full {i}"), SamplingParams(max_new_tokens=3, is_greedy=True)) for i in range(4)]
+    drv.start()
+    try:
+        assert all(h.wait(60) for h in hs)
+        assert drv.stats["admit_windows"] == 1 and drv.stats["admit_window_reqs"] == 4
+        assert drv.stats["admit_window_s"] < 0.25
+        assert eng.stats["prefill_steps"] == 1
+    finally:
+        drv.stop()
