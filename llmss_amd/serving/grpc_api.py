@@ -21,6 +21,7 @@ from __future__ import annotations
 import asyncio
 import inspect
 import json
+import logging
 import threading
 import time
 from concurrent import futures
@@ -28,6 +29,8 @@ from typing import Optional
 
 import grpc
 from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+
+log = logging.getLogger(__name__)
 
 _F = descriptor_pb2.FieldDescriptorProto
 
@@ -119,6 +122,8 @@ class AioServer:
         self._server = None
         self._err: Optional[BaseException] = None
         self._ready = threading.Event()
+        self._stop_lock = threading.Lock()
+        self._stopping = False
         self._thread = threading.Thread(target=self._run, args=(servicer, port, host), daemon=True,
                                         name="grpc-aio-server")
         self._thread.start()
@@ -141,17 +146,32 @@ class AioServer:
 
         try:
             self.loop.run_until_complete(main())
-        except BaseException as e:  # noqa: BLE001 - reported to the constructor
+            if not self._stopping:
+                log.warning("gRPC aio server terminated without stop()")
+        except BaseException as e:  # noqa: BLE001 - reported to the constructor / stop()
             self._err = e
             self._ready.set()
+            log.error("gRPC aio server loop ended with %r", e)
+        finally:
+            self._stopped = True
 
     def stop(self, grace: Optional[float] = None):
-        fut = asyncio.run_coroutine_threadsafe(self._server.stop(grace), self.loop)
+        """Stop serving; ``.wait(timeout)`` joins the loop thread. A loop that already ended (its server
+        terminated or failed) has nothing to stop: scheduling onto it would never complete."""
         th = self._thread
+        self._stopping = True
+        with self._stop_lock:
+            live = not getattr(self, "_stopped", False) and th.is_alive() and self.loop.is_running()
+            fut = asyncio.run_coroutine_threadsafe(self._server.stop(grace), self.loop) if live else None
 
         class _Done:
             def wait(self, timeout: Optional[float] = None) -> bool:
-                fut.result(timeout)
+                if fut is not None:
+                    t0 = time.perf_counter()
+                    while not fut.done():  # polled: the loop may end (and drop the callback) meanwhile
+                        if not th.is_alive() or (timeout is not None and time.perf_counter() - t0 > timeout):
+                            break
+                        time.sleep(0.01)
                 th.join(timeout)
                 return not th.is_alive()
         return _Done()

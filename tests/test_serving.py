@@ -318,3 +318,18 @@ def test_admission_window_closes_when_slots_are_full(model_dir):
         assert eng.stats["prefill_steps"] == 1
     finally:
         drv.stop()
+
+
+def test_aio_server_stop_after_its_loop_ended(driver):
+    """stop().wait() returns when the server's loop already ended (it used to schedule the stop onto the dead
+    loop and wait forever)."""
+    drv, tok, m = driver
+    server = serve(EngineServicer(drv, tok), port=0, host="127.0.0.1")
+    server.loop.call_soon_threadsafe(server.loop.stop)  # the loop ends without a server stop
+    server._thread.join(10)
+    assert not server._thread.is_alive()
+    t0 = time.perf_counter()
+    assert server.stop(0).wait(5)
+    assert time.perf_counter() - t0 < 5
+    ok = serve(EngineServicer(drv, tok), port=0, host="127.0.0.1")  # the normal path still stops cleanly
+    assert ok.stop(0).wait(30)
