@@ -678,13 +678,14 @@ __global__ __launch_bounds__(64 * NW) void gemm_tiled_kernel(const bf16_t* __res
 }
 
 // -------------------------------------------------------------------------------------------
-// big-tile GEMM (prefill, M >= ~1024): 256x256x64 tile, 8 waves (2 x 4), each wave 128x64 =
-// 8x4 mfma_f32_16x16x32 accumulators (AGPRs). LDS = 2 buffers x {A rows 0-127, A rows 128-255,
-// B rows 0-127, B rows 128-255} of 16 KiB = 128 KiB -> one workgroup per CU.
+// W8A8 big-tile GEMM (fp8 prefill, M >= ~1024; bf16 prompt batches take gemm_pp_kernel below):
+// 256x256 tile of 128-element fp8 K-tiles, 8 waves (2 x 4), each wave 128x64 = 8x4 accumulators on the
+// MX-fp8 16x16x128 MFMA. LDS = 2 buffers x {A rows 0-127, A rows 128-255, B rows 0-127, B rows 128-255}
+// of 16 KiB = 128 KiB -> one workgroup per CU.
 // Per K-tile t: (1) counted vmcnt(8) retires stage t while stage t+1 stays in flight, raw
 // barrier; (2) every wave reads ALL its fragments of tile t into VGPRs (24 ds_read_b128) and
-// runs the first k-half of its MFMAs; (3) barrier (lgkmcnt(0): all reads of buffer t&1 done) and
-// stage t+2 is issued into that same buffer, then the second k-half of MFMAs. Prefetch distance
+// runs the first half of its MFMAs; (3) barrier (lgkmcnt(0): all reads of buffer t&1 done) and
+// stage t+2 is issued into that same buffer, then the second half of MFMAs. Prefetch distance
 // is therefore ~1.5 K-tiles of MFMA time and no barrier ever drains the DMA queue (guide:
 // "Pipelining across barriers", 3-buffer-equivalent depth in 2 buffers).
 // Requires K % 64 == 0; rows beyond M / N are clamped on load and masked on store.
@@ -708,14 +709,6 @@ __device__ __forceinline__ f32x4 mfma_f8x2(s16x8 a0, s16x8 a1, s16x8 b0, s16x8 b
 // 64-element bf16 one, so staging / LDS image / fragment addresses are shared; each (m, n) takes one
 // MX-fp8 16x16x128 MFMA per K-tile (the two 16-B chunks 2g, 2g+1 of the lane's row), and the
 // per-token x per-channel scales are applied in the epilogue.
-// bf16 K-loop (profiles/r4_gemm_big): the next-but-one K-tile's 8 LDS-DMA loads are issued one per 4 MFMAs
-// of the second k-half instead of as one burst before them (an in-order wave cannot issue MFMAs while its
-// load burst waits on the CU's address path), and the second k-half's fragment reads one or two per 4
-// MFMAs of the first k-half: +3-6 % at M = 2048 / 8192. Measured and not taken: the second k-half's reads
-// as one block under the first k-half's MFMAs (no change), reading the next K-tile's first k-half under
-// this one's second (prefetch distance 1 K-tile instead of 1.5: -6 %), restaging right after the fragment
-// reads (distance ~1.8: 0-3 % slower), reading the next K-tile's first-half fragments under this one's
-// second-half MFMAs with both interleaved (distance 1: equal at M = 8192, -9 % on one shape at 2048).
 template <bool F8>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict__ A, int64_t lda,
                                                           const void* __restrict__ B, int64_t ldb,
@@ -723,7 +716,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict
                                                           int64_t ldy, int M, int N, int K, int act, int glu,
                                                           const float* __restrict__ xs, const float* __restrict__ ws,
                                                           int group_m) {
-  constexpr int ILV = F8 ? 0 : 2;
   constexpr int ES = F8 ? 1 : 2;  // operand bytes per element
   constexpr int HALF = 16384, BUF = 4 * HALF;
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
@@ -804,26 +796,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict
     else wait_vmcnt<0>();
     lds_barrier();  // stage t landed for every wave
     s16x8 a[8][2], b[4][2];
-    if constexpr (ILV == 2 && !F8) {
-      // k-half 0 fragments, then its MFMAs with the k-half 1 fragment reads interleaved (1-2 per 4 MFMAs)
-#pragma unroll
-      for (int n = 0; n < 4; ++n) b[n][0] = *reinterpret_cast<const s16x8*>(cur + boff[n][0]);
-#pragma unroll
-      for (int m = 0; m < 8; ++m) a[m][0] = *reinterpret_cast<const s16x8*>(cur + aoff[m][0]);
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), seen by the wait-count pass: the MFMAs below wait on nothing
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        if (m < 4) b[m][1] = *reinterpret_cast<const s16x8*>(cur + boff[m][1]);
-        a[m][1] = *reinterpret_cast<const s16x8*>(cur + aoff[m][1]);
-#pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][0], b[n][0], acc[m][n], 0, 0, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMAs, then the next fragment reads
-        if (m < 4) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        else __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_s_setprio(0);
-    } else {
+    {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
 #pragma unroll
@@ -846,22 +819,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict
     __builtin_amdgcn_s_setprio(0);
     }
     lds_barrier();  // every wave's reads of this buffer are complete -> restage it
-    if constexpr (ILV && !F8) {
-      const bool more = t + 2 < nk;
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        if (more)
-          __builtin_amdgcn_global_load_lds((const void*)(src[m >> 1] + soff[m >> 1][m & 1] + (int64_t)(t + 2) * 128),
-                                           (LDS_AS void*)(cur + (m >> 1) * HALF + lofs[m & 1]), 16, 0, 0);
-#pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m][1], b[n][1], acc[m][n], 0, 0, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // the load ...
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // ... then its 4 MFMAs
-      }
-      __builtin_amdgcn_s_setprio(0);
-      continue;
-    }
     if (t + 2 < nk) stage(t + 2, cur);
     __builtin_amdgcn_s_setprio(1);
     if constexpr (F8) {  // second half: n-tiles 2, 3
@@ -878,12 +835,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict
     __builtin_amdgcn_s_setprio(0);
   }
 
-  if constexpr (!F8) {
-    // bf16: through LDS in row chunks, 16-B row stores (the 128 KiB ring is free after the last tile)
-    tile_store_lds<256, 256, 8, 4, 512, 2 * BUF>(acc, smem, wr * 128, wc * 64, m0, n0, M, N, nullptr, Y, ldy, bias,
-                                                 act, glu);
-    return;
-  }
   // epilogue (C layout: col = lane&15 -> n, row = 4*(lane>>4)+i -> m)
   const int wn0 = n0 + wc * 64;
 #pragma unroll
@@ -918,6 +869,163 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict
       }
     }
   }
+}
+
+// -------------------------------------------------------------------------------------------
+// Ping-pong prefill GEMM (bf16, M >= ~1024): the shipped bf16 big-tile kernel (profiles/r5_gemm_pp).
+// 256x256x64 tile, 8 waves = two groups of 4 (waves 0-3 / 4-7; one wave of each group per SIMD). Waves
+// 4-7 pass one extra barrier before the K-loop, so on every SIMD one wave's compute segment runs beside
+// its partner's load segment (guide "The 256^2 8-phase template", MI355X_MICROARCH "Two waves per SIMD").
+//   * LDS = 2 buffers x 4 slots of 16 KiB: slot 0 = A half 0, 1 = B half 0, 2 = B half 1, 3 = A half 1.
+//     A half h holds block rows {128 r + 64 h + i}, B half h block columns {64 c + 32 h + j}, so each
+//     wave's contiguous 128x64 output splits into four 64x32 quadrants Q(mq, nq) reading A slot mq and
+//     B slot nq. Rows are 128 B (one K-tile), chunk-XOR swizzled on the source address (rule 21).
+//   * 4 phases per K-tile: Q(0,0) [reads A0 + B0: 12 ds_read_b128], Q(0,1) [B1: 4], Q(1,1) [A1: 8],
+//     Q(1,0) [B0 still in registers]. Phase = load segment (2 LDS-DMA of slot p of the NEXT K-tile, then
+//     the fragment reads, then a counted vmcnt) | barrier | 16 MFMA 16x16x32 | barrier.
+//   * RAW: a slot is read one phase after the vmcnt that retires it (vmcnt 4/4/6/4 in steady state,
+//     2/0 on the last K-tile); WAR: a slot is restaged >= 4 phases after its last read.
+//   * waves 4-7 run at s_setprio 1 (the arbitration loser of each pair, MI355X_MICROARCH item 4).
+// Measured vs the previous 2-barrier kernel at M = 8192 (Llama-2-7B shapes, random data, one process):
+// +4-13 %; the no-stagger control equals the old kernel. Ablations (profiles/r5_gemm_pp/README.md): the
+// LDS-DMA + fragment-read traffic through the LDS costs ~25 % each on top of the MFMA/barrier skeleton.
+// Requires K % 64 == 0; rows beyond M / N are clamped on load and masked on store.
+// -------------------------------------------------------------------------------------------
+__device__ __forceinline__ void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                         const bf16_t* __restrict__ B, int64_t ldb,
+                                                         const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
+                                                         int64_t ldy, int M, int N, int K, int act, int glu,
+                                                         int group_m) {
+  constexpr int SLOT = 16384, BUF = 4 * SLOT;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  const int wr = w >> 2, wc = w & 3;
+  const int ntn = (N + 255) / 256, ntm = (M + 255) / 256;
+  const int GM = group_m;  // XCD-contiguous tile ranges, GM M-tiles per group (as gemm_big)
+  const int tile = xcd_remap(blockIdx.x, ntn * ntm);
+  const int grp = tile / (GM * ntn), gidx = tile - grp * (GM * ntn);
+  const int gm = min(GM, ntm - grp * GM);
+  const int m0 = (grp * GM + gidx % gm) * 256, n0 = (gidx / gm) * 256;
+  const int nk = K / 64;
+
+  // staging: slot h, instruction i (0, 1) = 8 local rows x 128 B, local row lr = (8 i + w) * 8 + lane / 8;
+  // LDS chunk lane & 7 holds global chunk (lane & 7) ^ (lr & 7)
+  const char* src[4] = {(const char*)A, (const char*)B, (const char*)B, (const char*)A};
+  int64_t soff[4][2];
+  int lofs[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int inst = i * 8 + w;
+    const int lr = inst * 8 + (lane >> 3);
+    const int gc = (lane & 7) ^ (lr & 7);
+    lofs[i] = inst * 1024;
+    const int ar0 = min(m0 + (lr >> 6) * 128 + (lr & 63), M - 1);
+    const int ar1 = min(m0 + (lr >> 6) * 128 + 64 + (lr & 63), M - 1);
+    const int bc0 = min(n0 + (lr >> 5) * 64 + (lr & 31), N - 1);
+    const int bc1 = min(n0 + (lr >> 5) * 64 + 32 + (lr & 31), N - 1);
+    soff[0][i] = (int64_t)ar0 * lda * 2 + gc * 16;
+    soff[3][i] = (int64_t)ar1 * lda * 2 + gc * 16;
+    soff[1][i] = (int64_t)bc0 * ldb * 2 + gc * 16;
+    soff[2][i] = (int64_t)bc1 * ldb * 2 + gc * 16;
+  }
+  auto stage = [&](int t, int h, char* buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src[h] + soff[h][i] + (int64_t)t * 128),
+                                       (LDS_AS void*)(buf + h * SLOT + lofs[i]), 16, 0, 0);
+  };
+  // fragment offsets inside a slot: A rows wr*64 + mt*16 + li, B rows wc*32 + nt*16 + li; k-half s -> chunk 4s+g
+  // (the conflict-free ds_read_b128 image of gemm_big)
+  int aoff[4][2], boff[2][2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int c = 4 * s + g;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int r = wr * 64 + mt * 16 + li;
+      aoff[mt][s] = r * 128 + ((c ^ (r & 7)) << 4);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int r = wc * 32 + nt * 16 + li;
+      boff[nt][s] = r * 128 + ((c ^ (r & 7)) << 4);
+    }
+  }
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s16x8 fa[4][2], fb0[2][2], fb1[2][2];
+  auto rdA = [&](const char* slot) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fa[mt][s] = *reinterpret_cast<const s16x8*>(slot + aoff[mt][s]);
+  };
+  auto rdB = [&](const char* slot, s16x8 (&fb)[2][2]) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fb[nt][s] = *reinterpret_cast<const s16x8*>(slot + boff[nt][s]);
+  };
+  auto quad = [&](int mq, int nq, const s16x8 (&fb)[2][2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          acc[mq * 4 + mt][nq * 2 + nt] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt][s], fb[nt][s], acc[mq * 4 + mt][nq * 2 + nt], 0, 0, 0);
+  };
+  // one phase: LDS-DMA of slot h of the next K-tile, fragment reads, vmcnt(n) retiring what the next phase
+  // reads, barrier, the quadrant's 16 MFMAs, barrier
+  auto phase = [&](auto rd, int t, int h, bool more, int n_more, int n_last, int mq, int nq,
+                   const s16x8 (&fb)[2][2]) {
+    if (more) stage(t + 1, h, smem + ((t + 1) & 1) * BUF);
+    rd();
+    switch (more ? n_more : n_last) {
+      case 0: wait_vmcnt<0>(); break;
+      case 2: wait_vmcnt<2>(); break;
+      case 4: wait_vmcnt<4>(); break;
+      case 6: wait_vmcnt<6>(); break;
+      default: break;
+    }
+    pp_barrier();
+    quad(mq, nq, fb);
+    pp_barrier();
+  };
+
+#pragma unroll
+  for (int h = 0; h < 4; ++h) stage(0, h, smem);
+  wait_vmcnt<4>();  // slots 0, 1 (A0, B0) of K-tile 0
+  pp_barrier();
+  if (w >= 4) {
+    __builtin_amdgcn_s_setprio(1);
+    pp_barrier();  // the stagger: waves 4-7 run one barrier behind waves 0-3
+  }
+  for (int t = 0; t < nk; ++t) {
+    const char* cur = smem + (t & 1) * BUF;
+    const bool more = t + 1 < nk;
+    phase([&] { rdA(cur); rdB(cur + SLOT, fb0); }, t, 0, more, 4, 2, 0, 0, fb0);
+    phase([&] { rdB(cur + 2 * SLOT, fb1); }, t, 1, more, 4, 0, 0, 1, fb1);
+    phase([&] { rdA(cur + 3 * SLOT); }, t, 2, more, 6, -1, 1, 1, fb1);
+    phase([&] {}, t, 3, more, 4, -1, 1, 0, fb0);
+  }
+  if (w < 4) pp_barrier();  // balances the stagger barrier
+  __builtin_amdgcn_s_setprio(0);
+  wait_vmcnt<0>();
+  tile_store_lds<256, 256, 8, 4, 512, 2 * BUF>(acc, smem, wr * 128, wc * 64, m0, n0, M, N, nullptr, Y, ldy, bias,
+                                               act, glu);
 }
 
 // -------------------------------------------------------------------------------------------
@@ -1666,8 +1774,8 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   if ((tsel == 2 || tsel == 6) && ns > 4) ns = 4;
   if (f8 && tsel == 4) tsel = 1;
   if (tsel == 4) {
-    gemm_big_kernel<false><<<tiles_of(M, N, 256, 256), 512, 0, st>>>(X, ldx, W, ldw, B, Y, ldy, M, N, K, act, g,
-                                                                     nullptr, nullptr, g_big_group_m);
+    gemm_pp_kernel<<<tiles_of(M, N, 256, 256), 512, 0, st>>>(X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, M, N, K, act, g,
+                                                             g_big_group_m);
     HIP_CHECK_LAUNCH();
     return 0;
   }

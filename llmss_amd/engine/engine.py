@@ -214,13 +214,6 @@ class LLMEngine:
             from ..ops.autotune import tune_model
 
             self.tuned = tune_model(model, self.decode_batch_sizes())
-            if os.environ.get("LLMSS_PREFILL_LIB", "1") != "0":  # prompt-batch plain GEMMs: ours vs hipBLASLt
-                from ..ops.autotune import tune_prefill_library
-
-                lib_us = tune_prefill_library(model, min(self.max_batched_tokens, 8192),
-                                              agree=lambda f: self.tp.all_reduce_int(f, "min"))
-                if lib_us:
-                    self.stats["prefill_gemm_us"] = {k: list(v) for k, v in lib_us.items()}
         if self.is_gpu and autotune:
             self._tune_gqa_attention()
         if self.use_graphs and os.environ.get("LLMSS_GRAPHS", "1") == "0":

@@ -297,61 +297,11 @@ def tune_qkv_epilogue(model, ms: Sequence[int], native=None, iters: int = 16) ->
     return res
 
 
-def tune_prefill_library(model, M: int, agree=None, iters: int = 4) -> Dict[str, Tuple[float, float]]:
-    """Prompt-batch GEMMs: time each plain projection of the model (no activation / SwiGLU epilogue, bf16
-    weights) at M rows on the 256x256 kernel against the platform library (hipBLASLt via torch.matmul) and
-    route the shapes where the library is faster by 3 % to it (ops/hip.py _LIB_PREFILL). ``agree(flag)``
-    (e.g. a min all-reduce over TP ranks) makes every rank take the same decision. Returns
-    {name: (ours us, library us)}."""
-    from . import hip as H
-
-    if M < H.LIB_MIN_M:
-        return {}
-    dev = model.device
-    res = {}
-    for name, shp in model_shapes(model).items():
-        if shp.glu or shp.fp8 or shp.packed or shp.act not in ("none", None) or name == "head":
-            continue
-        key = ("lib", M, shp.N, shp.K, str(dev))
-        if key not in _DONE_LIB:
-            g = torch.Generator(device=dev)
-            g.manual_seed(99)
-            ws = [(torch.randn(shp.N, shp.K, device=dev, generator=g) * shp.K ** -0.5).to(torch.bfloat16)
-                  for _ in range(2)]
-            x = (torch.randn(M, shp.K, device=dev, generator=g) * 0.5).to(torch.bfloat16)
-            y = torch.empty(M, shp.N, dtype=torch.bfloat16, device=dev)
-            H._LIB_PREFILL.discard((shp.N, shp.K))
-
-            def ours(i):
-                H.linear(x, ws[i % 2], None, out=y)
-
-            def lib(i):
-                torch.matmul(x, ws[i % 2].t(), out=y)
-            ours(0)
-            lib(0)
-            torch.cuda.synchronize(dev)
-            _DONE_LIB[key] = (round(_time(ours, iters), 1), round(_time(lib, iters), 1))
-            del ws, x, y
-        t_ours, t_lib = _DONE_LIB[key]
-        win = t_lib < 0.97 * t_ours
-        if agree is not None:
-            win = bool(agree(int(win)))
-        if win:
-            H._LIB_PREFILL.add((shp.N, shp.K))
-        else:
-            H._LIB_PREFILL.discard((shp.N, shp.K))
-        res[name] = (t_ours, t_lib)
-    log.info("prompt-batch GEMMs at M=%d (us ours / library): %s; library for %s", M, res,
-             sorted(H._LIB_PREFILL))
-    return res
-
-
 # process-wide results: a second engine in the same process reuses the first one's plans, so both
 # run bit-identical kernels (and skip the tuning time)
 _DONE: Dict[Tuple[int, GemmShape, str], Tuple[int, int, float, float]] = {}
 _QKV_DONE: Dict[tuple, Dict[int, Tuple[float, float]]] = {}
 _QKV_PLANS: Dict[tuple, Tuple[int, int]] = {}
-_DONE_LIB: Dict[tuple, Tuple[float, float]] = {}
 
 
 def _reinstall_qkv(lib, model, results):

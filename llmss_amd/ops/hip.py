@@ -360,11 +360,6 @@ class PartialSum:
 
 _FP8_PREFILL_M = 128  # untuned fp8 calls above this M run W8A8 (compute-bound); below, W8A16 weight streaming
 
-# Plain bf16 GEMMs (no activation / SwiGLU / fused epilogue) at prompt-batch M that the engine's start-up
-# measurement (autotune.tune_prefill_library) found faster in the platform GEMM library (hipBLASLt through
-# torch.matmul) than the 256x256 kernel: {(N, K)}. Decode shapes never take it (M < LIB_MIN_M).
-LIB_MIN_M = 1024
-_LIB_PREFILL: set = set()
 
 
 # nt_hint flag of a W8A8 plan (the tuned table's fp8 entries or an explicit hint): tile = (nt >> 8) & 15
@@ -557,13 +552,6 @@ def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hi
     if bias is not None:
         _check(bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.numel() == N, "bias [N] bf16")
     nout = N // 2 if glu else N
-    if (M >= LIB_MIN_M and not glu and act in ("none", None) and not nt_hint and not fp8
-            and (N, K) in _LIB_PREFILL):
-        y = out if out is not None else torch.empty(M, N, dtype=x.dtype, device=x.device)
-        torch.matmul(x, w.t(), out=y)
-        if bias is not None:
-            y.add_(bias)
-        return y
     ws = _GEMM_WS.get(64 << 20, x.device)
     partial_ok = partial_ok and not glu and act in ("none", None) and out is None
     y = out if out is not None else (None if partial_ok else torch.empty(M, nout, dtype=x.dtype, device=x.device))

@@ -235,30 +235,12 @@ def test_gemm_mid_interleaved_ring(tile, depth, split, M, N, K):
               R.linear(x.float(), w.float(), b.float()), 2e-2)
 
 
-def test_prompt_batch_library_routing():
-    """Plain prompt-batch GEMMs routed to the platform library (ops/hip.py _LIB_PREFILL) give the oracle's result
-    with bias, into a given output; SwiGLU / activation calls and decode-sized M stay on the HIP kernels."""
-    torch.manual_seed(0)
-    M, N, K = 1100, 768, 512
-    x, w, b = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
-    ref = R.linear(x.float(), w.float(), b.float())
-    H._LIB_PREFILL.add((N, K))
-    try:
-        y = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=dev)
-        assert H.linear(x, w, b, out=y) is y
-        close(y, ref, 2e-2)
-        close(H.linear(x, w, b, partial_ok=True), ref, 2e-2)
-        close(H.linear(x, w, None, glu=True), R.linear(x.float(), w.float(), None, glu=True), 2e-2)
-        close(H.linear(x[:64], w, b), ref[:64], 2e-2)
-    finally:
-        H._LIB_PREFILL.discard((N, K))
-
-
 @pytest.mark.parametrize("M,N,K", [(700, 1312, 64), (513, 768, 128), (300, 512, 192), (1024, 1536, 4096),
-                                   (2100, 800, 1600)])
+                                   (2100, 800, 1600), (257, 288, 256), (600, 544, 320), (1500, 2080, 704)])
 def test_gemm_big_edges(M, N, K):
-    """The 256x256 prefill kernel (gemm.hip gemm_big_kernel) against the fp32 oracle at K-tile counts 1-3
-    (prologue / epilogue edges of its two-buffer pipeline) and ragged M / N, through the swizzled LDS epilogue."""
+    """The 256x256 ping-pong prefill kernel (gemm.hip gemm_pp_kernel) against the fp32 oracle at K-tile counts
+    1-5 and 11 (prologue / last-tile vmcnt edges of its 4-phase, 2-buffer schedule, and the slot reuse of the
+    steady state), ragged M / N, bias + activation and SwiGLU through the swizzled LDS epilogue."""
     torch.manual_seed(0)
     x, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
     b = rnd(N, scale=0.1)

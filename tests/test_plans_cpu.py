@@ -61,48 +61,3 @@ def test_interleaved_ring_candidates_only_where_the_kernel_takes_them():
     assert not ilv(A.candidates(512, 4096, 1376, False, False))  # partial last k-step
 
 
-def test_prompt_batch_library_decision(monkeypatch):
-    """ops/autotune.py tune_prefill_library: only plain projections are timed (no SwiGLU / activation / head),
-    the library takes a shape when it is 3 % faster, and the caller's `agree` (a min over TP ranks) overrules a
-    local win."""
-    import types
-
-    import torch
-
-    from llmss_amd.ops import hip as H
-
-    times = {(12288, 4096): (790.0, 580.0), (4096, 4096): (230.0, 229.0), (4096, 11008): (610.0, 480.0)}
-    cur = {}
-
-    def fake_time(fn, iters):
-        fn(0)
-        return cur.pop("t")
-
-    def fake_linear(x, w, *a, **k):
-        cur["t"] = times[tuple(w.shape)][0]
-
-    def fake_matmul(x, wt, out=None):
-        cur["t"] = times[tuple(wt.t().shape)][1]
-
-    monkeypatch.setattr(A, "_time", fake_time)
-    monkeypatch.setattr(H, "linear", fake_linear)
-    monkeypatch.setattr(torch, "matmul", fake_matmul)
-    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a: None)
-    A._DONE_LIB.clear()
-    lin = lambda n, k, glu=False: types.SimpleNamespace(N=n, K=k, glu=glu, w_scale=None, packed=False)
-    L = types.SimpleNamespace(qkv=lin(12288, 4096), o=lin(4096, 4096), up=lin(22016, 4096, True),
-                              down=lin(4096, 11008))
-    model = types.SimpleNamespace(device=torch.device("cpu"), tp=types.SimpleNamespace(size=1), act="silu",
-                                  cfg=types.SimpleNamespace(parallel_block=False),
-                                  w=types.SimpleNamespace(layers=[L], head=lin(32000, 4096)))
-    H._LIB_PREFILL.clear()
-    try:
-        res = A.tune_prefill_library(model, 4096, iters=1)
-        assert set(res) == {"qkv", "o", "down"}  # up (SwiGLU) and the head are not candidates
-        assert H._LIB_PREFILL == {(12288, 4096), (4096, 11008)}  # o: within 3 %
-        A.tune_prefill_library(model, 4096, agree=lambda f: 0, iters=1)  # a peer rank disagrees
-        assert H._LIB_PREFILL == set()
-        assert A.tune_prefill_library(model, 512) == {}  # decode-sized M: never
-    finally:
-        H._LIB_PREFILL.clear()
-        A._DONE_LIB.clear()
