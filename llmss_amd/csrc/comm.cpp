@@ -17,9 +17,11 @@
 #include <rccl/rccl.h>
 #include <stdint.h>
 
+#include <chrono>
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <thread>
 
 namespace py = pybind11;
 
@@ -36,15 +38,33 @@ ncclDataType_t rccl_dtype(int code) {
 
 hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Bounded communicator set-up (reference: the NCCL process group's 60 s timeout, utils/dist.py:54,71). The
+// communicator is created non-blocking (ncclConfig_t.blocking = 0): ncclCommInitRankConfig returns at once and
+// its state is polled with ncclCommGetAsyncError against a deadline; a peer that never joins (died, hung, or
+// failed before its own init) makes this rank abort the half-built communicator and raise instead of blocking
+// in the init forever. The same poll bounds every later call that reports ncclInProgress (a non-blocking
+// communicator's first collective builds its peer connections asynchronously); collectives whose connections
+// exist return ncclSuccess at once, so captured decode graphs are unaffected.
 class RcclComm {
  public:
-  RcclComm(const std::string& uid, int nranks, int rank, int device) : nranks_(nranks), rank_(rank), device_(device) {
+  RcclComm(const std::string& uid, int nranks, int rank, int device, double timeout_s)
+      : nranks_(nranks), rank_(rank), device_(device), timeout_s_(timeout_s) {
     if (uid.size() != NCCL_UNIQUE_ID_BYTES) throw std::invalid_argument("RcclComm: unique id has the wrong size");
     if (nranks < 1 || rank < 0 || rank >= nranks) throw std::invalid_argument("RcclComm: bad rank / size");
     if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("RcclComm: hipSetDevice failed");
     ncclUniqueId id;
     std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
-    rccl_check(ncclCommInitRank(&comm_, nranks, id, rank), "ncclCommInitRank");
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    const ncclResult_t r = ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+      if (comm_ != nullptr) ncclCommAbort(comm_);
+      comm_ = nullptr;
+      rccl_check(r, "ncclCommInitRankConfig");
+    }
+    settle("ncclCommInitRankConfig", timeout_s);
+    init_s_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
   ~RcclComm() {
     if (comm_ != nullptr) ncclCommDestroy(comm_);
@@ -52,29 +72,29 @@ class RcclComm {
 
   void all_reduce(uintptr_t src, uintptr_t dst, int64_t count, int dtype, uintptr_t stream) {
     live();
-    rccl_check(ncclAllReduce(reinterpret_cast<const void*>(src), reinterpret_cast<void*>(dst), (size_t)count,
-                             rccl_dtype(dtype), ncclSum, comm_, as_stream(stream)),
-               "ncclAllReduce");
+    done(ncclAllReduce(reinterpret_cast<const void*>(src), reinterpret_cast<void*>(dst), (size_t)count,
+                       rccl_dtype(dtype), ncclSum, comm_, as_stream(stream)),
+         "ncclAllReduce");
   }
   // dst holds nranks * count elements, rank r's block at offset r * count
   void all_gather(uintptr_t src, uintptr_t dst, int64_t count, int dtype, uintptr_t stream) {
     live();
-    rccl_check(ncclAllGather(reinterpret_cast<const void*>(src), reinterpret_cast<void*>(dst), (size_t)count,
-                             rccl_dtype(dtype), comm_, as_stream(stream)),
-               "ncclAllGather");
+    done(ncclAllGather(reinterpret_cast<const void*>(src), reinterpret_cast<void*>(dst), (size_t)count,
+                       rccl_dtype(dtype), comm_, as_stream(stream)),
+         "ncclAllGather");
   }
   // src holds nranks * count elements; dst receives the sum of every rank's block `rank`
   void reduce_scatter(uintptr_t src, uintptr_t dst, int64_t count, int dtype, uintptr_t stream) {
     live();
-    rccl_check(ncclReduceScatter(reinterpret_cast<const void*>(src), reinterpret_cast<void*>(dst), (size_t)count,
-                                 rccl_dtype(dtype), ncclSum, comm_, as_stream(stream)),
-               "ncclReduceScatter");
+    done(ncclReduceScatter(reinterpret_cast<const void*>(src), reinterpret_cast<void*>(dst), (size_t)count,
+                           rccl_dtype(dtype), ncclSum, comm_, as_stream(stream)),
+         "ncclReduceScatter");
   }
   void broadcast(uintptr_t buf, int64_t count, int dtype, int root, uintptr_t stream) {
     live();
-    rccl_check(ncclBroadcast(reinterpret_cast<const void*>(buf), reinterpret_cast<void*>(buf), (size_t)count,
-                             rccl_dtype(dtype), root, comm_, as_stream(stream)),
-               "ncclBroadcast");
+    done(ncclBroadcast(reinterpret_cast<const void*>(buf), reinterpret_cast<void*>(buf), (size_t)count,
+                       rccl_dtype(dtype), root, comm_, as_stream(stream)),
+         "ncclBroadcast");
   }
   // Tear down without waiting for peers (a dead or hung rank): pending collectives are cancelled.
   void abort() {
@@ -85,6 +105,13 @@ class RcclComm {
   }
   void destroy() {
     if (comm_ != nullptr) {
+      // non-blocking communicator: flush (finalize, bounded poll), then free
+      const ncclResult_t r = ncclCommFinalize(comm_);
+      if (r != ncclSuccess && r != ncclInProgress) {
+        abort();
+        rccl_check(r, "ncclCommFinalize");
+      }
+      settle("ncclCommFinalize", timeout_s_);
       rccl_check(ncclCommDestroy(comm_), "ncclCommDestroy");
       comm_ = nullptr;
     }
@@ -98,13 +125,41 @@ class RcclComm {
   int rank() const { return rank_; }
   int size() const { return nranks_; }
   int device() const { return device_; }
+  double init_seconds() const { return init_s_; }
 
  private:
   void live() const {
     if (comm_ == nullptr) throw std::runtime_error("RcclComm: communicator was destroyed / aborted");
   }
+  // poll the communicator's state until it leaves ncclInProgress; past the deadline (or on an error) abort it
+  // and raise, so the caller's agreement step (parallel/dist.py) sees a failure instead of a hang
+  void settle(const char* what, double timeout_s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int it = 0;; ++it) {
+      ncclResult_t st = ncclSuccess;
+      const ncclResult_t q = ncclCommGetAsyncError(comm_, &st);
+      if (q != ncclSuccess) st = q;
+      if (st == ncclSuccess) return;
+      if (st != ncclInProgress) {
+        abort();
+        throw std::runtime_error(std::string("RCCL ") + what + ": " + ncclGetErrorString(st));
+      }
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (timeout_s > 0 && el > timeout_s) {
+        abort();
+        throw std::runtime_error(std::string("RCCL ") + what + ": timed out after " + std::to_string(timeout_s) +
+                                 " s waiting for the peer ranks (communicator aborted)");
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(it < 100 ? 20 : 1000));
+    }
+  }
+  void done(ncclResult_t r, const char* what) {
+    if (r == ncclInProgress) settle(what, timeout_s_);
+    else rccl_check(r, what);
+  }
   ncclComm_t comm_ = nullptr;
   int nranks_, rank_, device_;
+  double timeout_s_ = 0, init_s_ = 0;
 };
 
 }  // namespace
@@ -133,7 +188,8 @@ void register_comm(py::module_& m) {
   // init, destroy and a collective's first call (lazy peer connection) block on the peers: release the GIL so
   // other Python threads (the serving heartbeat) keep running
   py::class_<RcclComm>(m, "RcclComm")
-      .def(py::init<const std::string&, int, int, int>(), py::call_guard<py::gil_scoped_release>())
+      .def(py::init<const std::string&, int, int, int, double>(), py::arg("uid"), py::arg("nranks"), py::arg("rank"),
+           py::arg("device"), py::arg("timeout_s") = 120.0, py::call_guard<py::gil_scoped_release>())
       .def("all_reduce", &RcclComm::all_reduce, py::call_guard<py::gil_scoped_release>())
       .def("all_gather", &RcclComm::all_gather, py::call_guard<py::gil_scoped_release>())
       .def("reduce_scatter", &RcclComm::reduce_scatter, py::call_guard<py::gil_scoped_release>())
@@ -143,5 +199,6 @@ void register_comm(py::module_& m) {
       .def("async_error", &RcclComm::async_error)
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("size", &RcclComm::size)
-      .def_property_readonly("device", &RcclComm::device);
+      .def_property_readonly("device", &RcclComm::device)
+      .def_property_readonly("init_seconds", &RcclComm::init_seconds);
 }

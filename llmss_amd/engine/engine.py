@@ -354,9 +354,13 @@ class LLMEngine:
         """Decode buckets whose row-sharded schedule (reduce-scatter -> add + norm on M / tp rows -> all-gather,
         DecoderLM._hidden_states_rsag) is timed against the all-reduce one at capture: real multi-rank
         communicator, LLMSS_TP_RSAG=auto (default), buckets divisible by the TP degree of at least
-        LLMSS_TP_RSAG_MIN (default 8 rows per rank)."""
+        LLMSS_TP_RSAG_MIN (default 8 rows per rank). Not for fp8-weight models: their default schedule feeds the
+        GEMMs the fp8 twin that add_norm writes, which the row-sharded add + norm does not produce, so the A/B would
+        not compare like with like."""
         m = self.model
         if not (self.is_gpu and self.tp.is_real and not self.tp.host_staged and m.rsag_mode == "auto"):
+            return []
+        if any(L.qkv.w_scale is not None for L in m.w.layers[:1]):
             return []
         lo = int(os.environ.get("LLMSS_TP_RSAG_MIN", str(8 * self.tp.size)))
         return [b for b in self.buckets if b >= lo and m.rsag_ok(b)]
@@ -809,29 +813,29 @@ class LLMEngine:
         variants = {b: [n for n, c in (("tbo", self._tbo_cands), ("rsag", self._rsag_cands)) if b in c]
                     for b in self.buckets}
         variants = {b: v for b, v in variants.items() if v}
-        st = torch.cuda.Stream()
-        st.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(st):  # eager warm-up: comm stream, half-batch workspaces, each collective's first use
+        alt, times = {}, {}
+
+        def warm():
+            st = torch.cuda.Stream()
+            st.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(st):  # eager warm-up: comm stream, half-batch workspaces, each collective's first use
+                for b in sorted(variants, reverse=True):
+                    for name in variants[b]:
+                        with self._schedule(b, name):
+                            self._decode_forward(b, buf, dist=modes[0])
+            torch.cuda.current_stream().wait_stream(st)
+            torch.cuda.synchronize()
+
+        def capture():
             for b in sorted(variants, reverse=True):
-                for name in variants[b]:
-                    with self._schedule(b, name):
-                        self._decode_forward(b, buf, dist=modes[0])
-        torch.cuda.current_stream().wait_stream(st)
-        torch.cuda.synchronize()
-        alt = {}
-        for b in sorted(variants, reverse=True):
-            for d in modes:
-                for name in variants[b]:
-                    with self._schedule(b, name):
-                        g = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
-                            self._decode_forward(b, buf, dist=d)
-                    alt[(b, d, name)] = g
-        torch.cuda.synchronize()
-        # realistic rows for timing: every row attends `ctx` cached positions (garbage K/V, no cache writes)
-        buf.ctx.fill_(ctx)
-        buf.bt.zero_()
-        buf.bt[:, :nblk] = torch.arange(nblk, dtype=torch.int32, device=buf.bt.device)
+                for d in modes:
+                    for name in variants[b]:
+                        with self._schedule(b, name):
+                            g = torch.cuda.CUDAGraph()
+                            with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
+                                self._decode_forward(b, buf, dist=d)
+                        alt[(b, d, name)] = g
+            torch.cuda.synchronize()
 
         def timed(g):
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -842,18 +846,36 @@ class LLMEngine:
             e.synchronize()
             return s.elapsed_time(e) / 3
 
-        times = {}
-        for b in sorted(variants, reverse=True):
-            for d in modes:
-                gs = {"one": self.graphs[(b, d)], **{n: alt[(b, d, n)] for n in variants[b]}}
-                for g in gs.values():  # warm every graph
-                    g.replay()
+        def measure():
+            # realistic rows for timing: every row attends `ctx` cached positions (garbage K/V, no cache writes)
+            buf.ctx.fill_(ctx)
+            buf.bt.zero_()
+            buf.bt[:, :nblk] = torch.arange(nblk, dtype=torch.int32, device=buf.bt.device)
+            for b in sorted(variants, reverse=True):
+                for d in modes:
+                    gs = {"one": self.graphs[(b, d)], **{n: alt[(b, d, n)] for n in variants[b]}}
+                    for g in gs.values():  # warm every graph
+                        g.replay()
+                    torch.cuda.synchronize()
+                    res = {n: [] for n in gs}
+                    for _ in range(2):  # interleaved rounds, best of each
+                        for n, g in gs.items():
+                            res[n].append(timed(g))
+                    times[(b, d)] = {n: min(v) for n, v in res.items()}
+
+        # each stage agreed across ranks: a stage that raises on one rank (OOM, a refused
+        # capture) makes every rank keep the all-reduce graphs, instead of one rank leaving while its peers
+        # wait for it in the stages' collectives or in the gather of the times below
+        for stage in (warm, capture, measure):
+            ok, err = self.tp.agree(stage)
+            if not ok:
+                log.warning("decode schedule A/B stopped at %s (%s): every rank keeps the all-reduce schedule",
+                            stage.__name__, err or "on a peer rank")
+                alt.clear()
+                buf.ctx.zero_()
+                buf.bt.zero_()
                 torch.cuda.synchronize()
-                res = {n: [] for n in gs}
-                for _ in range(2):  # interleaved rounds, best of each
-                    for n, g in gs.items():
-                        res[n].append(timed(g))
-                times[(b, d)] = {n: min(v) for n, v in res.items()}
+                return
         allt = self.tp.all_gather_object(times)
         for (b, d), tv in times.items():
             worst = {n: max(t[(b, d)][n] for t in allt) for n in tv}

@@ -338,31 +338,48 @@ def comm_mode() -> str:
     return m
 
 
-def _native_comm(rank: int, dp: int, tp: int):
+def _rccl_comm(uid, nranks: int, rank: int, device: int):
+    """One native communicator, created non-blocking with a deadline (csrc/comm.cpp RcclComm): a peer that never
+    joins makes this rank abort and raise after ``LLMSS_RCCL_INIT_TIMEOUT_S`` (default 120 s) instead of blocking
+    inside ncclCommInitRank forever (reference: the NCCL group's 60 s timeout, ``utils/dist.py:54,71``)."""
+    from .. import _native
+
+    timeout = float(os.environ.get("LLMSS_RCCL_INIT_TIMEOUT_S", "120"))
+    return _native().RcclComm(uid, nranks, rank, device, timeout)
+
+
+def _native_comm(rank: int, dp: int, tp: int, make_comm=None, unique_id=None):
     """One RCCL communicator per data-parallel replica (ranks r*tp .. r*tp+tp-1). Each replica leader draws a
     unique id; the ids travel over the CPU world group (every rank joins every broadcast), then each rank
     joins its replica's communicator and checks it with one all-reduce.
 
-    Everything that can fail before ncclCommInitRank (drawing the id, the device) is agreed over gloo first,
-    so a rank that fails there makes every rank raise instead of leaving its peers blocked inside the init.
-    A failure inside ncclCommInitRank itself is not covered: RCCL's blocking init has no timeout, and the
-    non-blocking form would make every later collective call asynchronous too. The peers
-    then wait until the launcher's (or the driver's) time limit."""
-    from .. import _native
+    Everything that can fail before the communicator init (drawing the id, the device) is agreed over gloo
+    first, so a rank that fails there makes every rank raise instead of leaving its peers inside the init. The
+    init itself is bounded (:func:`_rccl_comm`): a peer that never arrives - it died, or failed after the
+    agreement - makes the waiting ranks abort their half-built communicator and raise at the deadline; the
+    caller then agrees on the failure over gloo. ``make_comm`` / ``unique_id`` replace the native constructor and
+    ncclGetUniqueId (CPU tests of this protocol)."""
+    import time
 
-    C = _native()
+    make_comm = make_comm or _rccl_comm
+    if unique_id is None:
+        from .. import _native
+
+        unique_id = _native().rccl_unique_id
     uids, err = [], ""
     for r in range(dp):
         box = [None]
         if rank == r * tp:
             try:
-                box = [C.rccl_unique_id()]
+                box = [unique_id()]
             except Exception as e:  # noqa: BLE001 - agreed below; the broadcast still runs
                 err = f"ncclGetUniqueId: {e}"
         dist.broadcast_object_list(box, src=r * tp)
         uids.append(box[0])
+    dev = 0
     try:
-        torch.cuda.set_device(torch.cuda.current_device())
+        dev = torch.cuda.current_device()
+        torch.cuda.set_device(dev)
         torch.cuda.synchronize()
     except Exception as e:  # noqa: BLE001
         err = err or f"device: {e}"
@@ -373,7 +390,17 @@ def _native_comm(rank: int, dp: int, tp: int):
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     if not int(ok[0]):
         raise RuntimeError(f"rank {rank}: RCCL pre-init check failed ({err or 'on a peer'})")
-    comm = C.RcclComm(uids[r], tp, rank - r * tp, torch.cuda.current_device())
+    if os.environ.get("LLMSS_FAULT_INJECT", "") == f"{rank}:rccl_init:skip":  # tests: passes the agreement, then
+        raise RuntimeError("injected: rank skipped the communicator init")  # never joins the init (dead peer)
+    t0 = time.perf_counter()
+    comm = make_comm(uids[r], tp, rank - r * tp, dev)
+    COMM_INIT_INFO.update({"init_s": round(time.perf_counter() - t0, 3),
+                           "timeout_s": float(os.environ.get("LLMSS_RCCL_INIT_TIMEOUT_S", "120"))})
+    if not torch.cuda.is_available():  # protocol tests: no device self-check
+        return comm
+    from .. import _native
+
+    C = _native()
     t = torch.full((4,), float(rank - r * tp + 1), dtype=torch.float32, device="cuda")
     comm.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), C.rccl_dtypes["float32"],
                     torch.cuda.current_stream().cuda_stream)
@@ -382,7 +409,11 @@ def _native_comm(rank: int, dp: int, tp: int):
     if not bool((got == want).all()):
         comm.abort()
         raise RuntimeError(f"rank {rank}: RCCL self-check all-reduce returned {got.tolist()}, expected {want}")
+    COMM_INIT_INFO["first_collective_s"] = round(time.perf_counter() - t0 - COMM_INIT_INFO["init_s"], 3)
     return comm
+
+
+COMM_INIT_INFO: dict = {}  # this rank's communicator set-up times (bench.py's runtime record)
 
 
 # RCCL settings the decode all-reduce is timed under at start-up (LLMSS_RCCL_TUNE): the library's choice, then
@@ -424,54 +455,88 @@ def _time_all_reduce(comm, nbytes: int, reps: int = 20) -> float:
     return best
 
 
-def _tune_native_comm(comm, rank: int, tp: int, nbytes: int, group=None):
+def _agreed(fn, group=None):
+    """Run ``fn()`` on every rank of ``group`` and agree on success (min over gloo): ``(True, result)`` only if
+    it raised on no rank, so every rank takes the same branch of the probe below."""
+    out, err = None, ""
+    try:
+        out = fn()
+    except Exception as e:  # noqa: BLE001 - reported collectively
+        err = str(e) or repr(e)
+    ok = torch.tensor([0 if err else 1], dtype=torch.int32)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+    if err:
+        log.warning("rank %d: RCCL probe step failed: %s", dist.get_rank(), err)
+    return bool(int(ok[0])), out
+
+
+def _check_all_reduce(comm, tp: int, rank: int):
+    """A candidate communicator must sum correctly before it may win: rank r contributes r + 1."""
+    from .. import _native
+
+    t = torch.full((1024,), float(rank + 1), dtype=torch.float32, device="cuda")
+    comm.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), _native().rccl_dtypes["float32"],
+                    torch.cuda.current_stream().cuda_stream)
+    want = tp * (tp + 1) / 2
+    if not bool((t.cpu() == want).all()):
+        raise RuntimeError(f"candidate all-reduce returned a wrong sum (expected {want})")
+
+
+def _tune_native_comm(comm, rank: int, tp: int, nbytes: int, group=None, make_comm=None):
     """Start-up probe of the RCCL protocol / algorithm for the decode all-reduce (``nbytes``, the bench's 64
-    sequences per GPU x hidden 4096 x bf16 at TP=8 = 4 MiB by default, LLMSS_RCCL_TUNE_BYTES). Every candidate
-    of RCCL_CANDIDATES gets a communicator built under its environment, its graph-replayed all-reduce is timed
-    on every rank, and the max over ranks decides (all ranks keep the same setting, so every later collective
-    pairs up); a candidate must beat the library default by 5 %. Returns the communicator to keep (the default
-    one, or the winner's) and records the table in RCCL_TUNE_INFO. Single replica (dp == 1) only: the unique
-    id of each probe communicator goes over the world group."""
+    sequences per GPU x hidden 4096 x bf16 at TP=8 = 4 MiB by default, LLMSS_RCCL_TUNE_BYTES). Opt-in
+    (``LLMSS_RCCL_TUNE=1``) until it has run on a multi-GPU node. Every candidate of
+    RCCL_CANDIDATES gets a communicator built under its environment (bounded init), must sum correctly on a
+    fresh buffer, and has its graph-replayed all-reduce timed on every rank; each of these steps is agreed over
+    gloo, so a step that fails on one rank drops the candidate on all of them (no rank leaves the probe's
+    collective sequence alone). The max over ranks decides, all ranks keep the same setting, and a candidate
+    must beat the library default by 5 %. Single replica (dp == 1) only: probe unique ids go over the world
+    group."""
     from .. import _native
 
     C = _native()
-    times, comms = {"default": _time_all_reduce(comm, nbytes)}, {"default": comm}
+    make_comm = make_comm or _rccl_comm
+    dev = torch.cuda.current_device()
+    ok, t = _agreed(lambda: _time_all_reduce(comm, nbytes), group)
+    if not ok:
+        return comm
+    times, comms = {"default": t}, {"default": comm}
     saved = {k: os.environ.get(k) for _, env in RCCL_CANDIDATES for k in env}
+
+    def restore():
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     try:
         for name, env in RCCL_CANDIDATES[1:]:
-            os.environ.update(env)
-            box = [C.rccl_unique_id() if rank == 0 else None]
+            ok, uid = _agreed(lambda: C.rccl_unique_id() if rank == 0 else b"", group)
+            if not ok:
+                times[name] = None
+                continue
+            box = [uid]
             dist.broadcast_object_list(box, src=0, group=group)
-            c, err = None, ""
+            os.environ.update(env)
             try:
-                c = C.RcclComm(box[0], tp, rank, torch.cuda.current_device())
-                t = _time_all_reduce(c, nbytes)
-            except Exception as e:  # noqa: BLE001 - decided collectively below
-                err, t = str(e), float("inf")
-            for k in env:
-                if saved[k] is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = saved[k]
-            ok = torch.tensor([0 if err else 1], dtype=torch.int32)
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
-            if not int(ok[0]):
+                ok, c = _agreed(lambda: make_comm(box[0], tp, rank, dev), group)
+            finally:
+                restore()
+            if ok:
+                ok, t = _agreed(lambda: (_check_all_reduce(c, tp, rank), _time_all_reduce(c, nbytes))[1], group)
+            if not ok:
                 if c is not None:
                     c.abort()
                 times[name] = None
                 continue
             times[name], comms[name] = t, c
     finally:
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        restore()
     allt = [None] * dist.get_world_size(group)
     dist.all_gather_object(allt, times, group=group)
-    worst = {n: (None if any(t[n] is None for t in allt) else max(t[n] for t in allt)) for n in times}
-    ok = {n: v for n, v in worst.items() if v is not None}
-    best = min(ok, key=lambda n: ok[n] if n == "default" else ok[n] / 0.95)
+    worst = {n: (None if any(t.get(n) is None for t in allt) else max(t[n] for t in allt)) for n in times}
+    okt = {n: v for n, v in worst.items() if v is not None}
+    best = min(okt, key=lambda n: okt[n] if n == "default" else okt[n] / 0.95)
     for n, c in comms.items():
         if n != best:
             c.destroy()
@@ -542,7 +607,7 @@ def initialize_distributed(timeout_s: Optional[int] = None, backend: Optional[st
             err = str(e)
         ok = torch.tensor([0 if err else 1], dtype=torch.int32)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # CPU (gloo) world group: every rank takes the same path
-        if int(ok[0]) and dp == 1 and os.environ.get("LLMSS_RCCL_TUNE", "1") != "0":
+        if int(ok[0]) and dp == 1 and os.environ.get("LLMSS_RCCL_TUNE", "0") == "1":
             try:
                 comm = _tune_native_comm(comm, rank, tp, _env_int("LLMSS_RCCL_TUNE_BYTES", 4 << 20))
             except Exception as e:  # noqa: BLE001 - a failed probe keeps the library default
@@ -655,7 +720,14 @@ def initialize_torch_distributed():
     tp, rank, world_size = initialize_distributed()
     if world_size == 1 or tp.fake:
         return FakeGroup(rank, world_size), rank, world_size
-    pg = dist.group.WORLD
-    if tp.dp == 1:
-        _TP_FOR_PG[id(pg)] = (pg, tp)
+    if tp.dp > 1:
+        # data-parallel replicas (LLMSS_DP): this rank's replica, not the world, is the tensor-parallel group -
+        # its CPU control group stands in for the process group (WORLD would shard the model
+        # over every replica's ranks)
+        if tp.size == 1:
+            return FakeGroup(0, 1), rank, world_size
+        pg = tp.ctrl_group
+    else:
+        pg = dist.group.WORLD
+    _TP_FOR_PG[id(pg)] = (pg, tp)
     return pg, rank, world_size

@@ -240,3 +240,25 @@ def test_rccl_setting_probe_one_rank(monkeypatch):
         dist.destroy_process_group()
         os.environ.pop("NCCL_PROTO", None)
         os.environ.pop("NCCL_ALGO", None)
+
+
+def test_rccl_init_deadline_without_peer():
+    """Bounded communicator init (csrc/comm.cpp): a 2-rank communicator whose second rank
+    never arrives raises at the deadline (non-blocking ncclCommInitRankConfig polled, then ncclCommAbort) instead
+    of blocking forever; a 1-rank communicator still initialises and reports its set-up time."""
+    import time
+
+    from llmss_amd import _native
+
+    C = _native()
+    t0 = time.monotonic()
+    with pytest.raises(RuntimeError, match="timed out"):
+        C.RcclComm(C.rccl_unique_id(), 2, 0, torch.cuda.current_device(), 3.0)
+    assert time.monotonic() - t0 < 60
+    c = C.RcclComm(C.rccl_unique_id(), 1, 0, torch.cuda.current_device(), 30.0)
+    assert 0 <= c.init_seconds < 30
+    x = torch.ones(16, device="cuda")
+    c.all_reduce(x.data_ptr(), x.data_ptr(), x.numel(), _code(x), _st())
+    torch.cuda.synchronize()
+    assert bool((x == 1).all())
+    c.destroy()

@@ -137,3 +137,74 @@ def test_leader_loss_detected_by_follower(ckpt, ctrl):
             p.join(30)
             if p.is_alive():
                 p.kill()
+
+
+class _RendezvousComm:
+    """Stand-in for the native RcclComm's bounded init (csrc/comm.cpp): every rank announces itself in a shared
+    directory and waits for all ``nranks`` peers until ``timeout_s``, then raises like the native deadline."""
+
+    def __init__(self, root, timeout_s):
+        self.root, self.timeout_s = root, timeout_s
+
+    def __call__(self, uid, nranks, rank, device):
+        d = os.path.join(self.root, uid.hex()[:16])
+        os.makedirs(d, exist_ok=True)
+        open(os.path.join(d, str(rank)), "w").close()
+        t0 = time.monotonic()
+        while len(os.listdir(d)) < nranks:
+            if time.monotonic() - t0 > self.timeout_s:
+                raise RuntimeError(f"RCCL ncclCommInitRankConfig: timed out after {self.timeout_s} s waiting for "
+                                   "the peer ranks (communicator aborted)")
+            time.sleep(0.01)
+        return object()
+
+
+def _init_worker(rank, port, root, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                      LLMSS_FAULT_INJECT="1:rccl_init:skip")
+    import torch.distributed as dist
+
+    from llmss_amd.parallel.dist import _native_comm
+
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    torch.cuda.set_device = lambda *a: None  # no GPU here: the device step is stubbed (tests/test_capture_agreement.py)
+    torch.cuda.synchronize = lambda *a: None
+    torch.cuda.current_device = lambda: 0
+    t0 = time.monotonic()
+    err = ""
+    try:
+        _native_comm(rank, 1, 2, make_comm=_RendezvousComm(root, 3.0), unique_id=lambda: os.urandom(128))
+    except RuntimeError as e:
+        err = str(e)
+    el = time.monotonic() - t0
+    ok = torch.tensor([0 if err else 1], dtype=torch.int32)  # the caller's agreement (initialize_distributed)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    q.put((rank, el, err, int(ok[0])))
+    dist.destroy_process_group()
+
+
+def test_rccl_init_bounded_when_a_peer_never_joins(tmp_path):
+    """rank 1 passes the pre-init agreement and then never joins the communicator init
+    (fault-injected, as a peer that died). Rank 0's bounded init raises at its deadline instead of blocking, and
+    both ranks then agree on the failure over gloo (the native deadline itself: tests/test_comm_gpu.py)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_init_worker, args=(r, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = {r: (el, err, ok) for r, el, err, ok in (q.get(timeout=120) for _ in range(2))}
+        for p in procs:
+            p.join(30)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
+    el0, err0, ok0 = res[0]
+    assert "timed out" in err0 and 2.5 < el0 < 30, res[0]
+    assert "injected" in res[1][1]
+    assert ok0 == 0 and res[1][2] == 0

@@ -30,8 +30,9 @@ def test_fake_group_reference_api():
     assert (tp1.size, tp1.is_real) == (1, False)
 
 
-def _sequence(d, prompt):
-    """generate.py:42-67 + one cached forward; returns (world_size, rank, logits)."""
+def _sequence(d, prompt, tp_size=None):
+    """generate.py:42-67 + one cached forward; returns (world_size, rank, logits). ``tp_size``: the expected
+    tensor-parallel width of the returned process group (world size unless data-parallel replicas are on)."""
     from llmss.server.models.custom_modeling import MODEL_REGISTRY
     from llmss.server.models.utils.dist import initialize_torch_distributed
     from llmss.server.models.utils.hub import weight_files
@@ -42,7 +43,8 @@ def _sequence(d, prompt):
     device, dtype = torch.device("cpu"), torch.float32
     config = AutoConfig.from_pretrained(d)
     weights = Weights(weight_files(d), device=device, dtype=dtype, process_group=process_group)
-    assert weights.process_group.size() == world_size and weights.process_group.rank() == rank
+    tp_size = tp_size or world_size
+    assert weights.process_group.size() == tp_size and weights.process_group.rank() == rank % tp_size
     model = MODEL_REGISTRY[config.model_type](config, weights)
     model.eval()
     ids = prompt.clone() if rank == 0 else torch.zeros_like(prompt)
@@ -54,11 +56,12 @@ def _sequence(d, prompt):
     return world_size, rank, torch.cat([out.logits, out2.logits], 1)
 
 
-def _worker(rank, port, d, prompt, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2")
+def _worker(rank, port, d, prompt, q, world=2, dp=1):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LLMSS_DP=str(dp))
     torch.set_num_threads(1)
     try:
-        ws, r, logits = _sequence(d, prompt)
+        ws, r, logits = _sequence(d, prompt, world // dp)
         q.put((r, ws, logits.numpy()))
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
@@ -100,3 +103,37 @@ def test_reference_generate_sequence_world1_and_world2(tmp_path, monkeypatch):
         assert ws2 == 2, logits
         torch.testing.assert_close(torch.from_numpy(logits), ref, rtol=1e-4, atol=1e-4)  # TP=2 over gloo == world 1
     assert [p.exitcode for p in procs] == [0, 0]
+
+
+def test_reference_generate_sequence_dp2(tmp_path):
+    """World 4 with two data-parallel replicas (LLMSS_DP=2): initialize_torch_distributed hands each rank its
+    replica's group (TP=2), not the world, so Weights / MODEL_REGISTRY shard over 2 ranks and every replica
+    computes the world-1 logits."""
+    d = str(tmp_path / "llama")
+    save_hf_model("llama", d, vocab=101)
+    prompt = torch.randint(0, 100, (2, 7))
+    with torch.no_grad():
+        from transformers import AutoModelForCausalLM
+
+        full = AutoModelForCausalLM.from_pretrained(d, torch_dtype=torch.float32)(prompt).logits
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(i, port, d, prompt, q, 4, 2)) for i in range(4)]
+    for p in procs:
+        p.start()
+    try:
+        got = [q.get(timeout=300) for _ in range(4)]
+        for p in procs:
+            p.join(60)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
+    for rank, ws, logits in got:
+        assert ws == 4, logits
+        torch.testing.assert_close(torch.from_numpy(logits)[:, :7], full, rtol=1e-4, atol=1e-4)
+    assert [p.exitcode for p in procs] == [0] * 4
