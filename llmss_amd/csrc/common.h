@@ -120,6 +120,19 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// Buffer resource descriptor whose words the compiler can PROVE wave-uniform (guide T20): the base pointer
+// halves and the byte count go through readfirstlane, so the descriptor lives in SGPRs and buffer loads /
+// stores are not wrapped in waterfall loops (one readfirstlane loop per memory op otherwise). `bytes` is
+// clamped to the 32-bit record count; callers keep every per-lane part in voffset.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, int64_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane((int)(bytes < 0x7fffffff ? bytes : 0x7fffffff));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, n,
+                                           0x00020000);
+}
+
 // Reductions over lane pairs (lane, lane ^ 16) / (lane, lane ^ 32) by the gfx950 permlane swaps (VALU,
 // no LDS round trip like ds_bpermute-based __shfl_xor): swapping two copies of x leaves x and its
 // partner's x in the two registers, in some order - symmetric ops need no fix-up. Inline asm (with the

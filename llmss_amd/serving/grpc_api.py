@@ -114,7 +114,17 @@ def serve(servicer, port: int = 50051, host: str = "0.0.0.0", max_workers: int =
 
 
 class AioServer:
-    """``grpc.aio`` server running on a dedicated event-loop thread (the engine driver keeps its own thread)."""
+    """``grpc.aio`` server running on a dedicated event-loop thread (the engine driver keeps its own thread).
+
+    The loop's one task, ``main``, owns the server's whole life: it starts the server, waits for either a stop
+    request or the server terminating on its own, runs ``server.stop(grace)`` ITSELF, and only then returns -
+    after which every task still pending on the loop (servicer coroutines of cancelled calls) is cancelled and
+    drained and the loop is closed. Root cause of round 4's "loop ended early" (profiles/r4_serving): ``stop()``
+    used to schedule ``server.stop()`` onto the loop from another thread while ``main`` awaited
+    ``wait_for_termination()``. The server signals termination part-way through its own ``stop()``, so ``main``
+    returned, ``run_until_complete`` stopped the loop, and the scheduled stop coroutine was left unfinished
+    forever: the thread was gone and the caller's future never resolved (the stack dump's picture). Nothing
+    ended early; the stop raced the loop's own exit (tests/test_serving.py)."""
 
     def __init__(self, servicer, port: int, host: str):
         self.loop = asyncio.new_event_loop()
@@ -122,8 +132,10 @@ class AioServer:
         self._server = None
         self._err: Optional[BaseException] = None
         self._ready = threading.Event()
-        self._stop_lock = threading.Lock()
+        self._stop_ev: Optional[asyncio.Event] = None
+        self._grace: Optional[float] = None
         self._stopping = False
+        self.stop_completed = False  # server.stop() ran to the end on the loop
         self._thread = threading.Thread(target=self._run, args=(servicer, port, host), daemon=True,
                                         name="grpc-aio-server")
         self._thread.start()
@@ -141,37 +153,58 @@ class AioServer:
             add_servicer(self._server, servicer)
             self.bound_port = self._server.add_insecure_port(f"{host}:{port}")
             await self._server.start()
+            self._stop_ev = asyncio.Event()
             self._ready.set()
-            await self._server.wait_for_termination()
+            term = asyncio.ensure_future(self._server.wait_for_termination())
+            req = asyncio.ensure_future(self._stop_ev.wait())
+            done, _ = await asyncio.wait({term, req}, return_when=asyncio.FIRST_COMPLETED)
+            if req in done:
+                await self._server.stop(self._grace)
+                self.stop_completed = True
+            else:
+                log.warning("gRPC aio server terminated without stop()")
+            for t in (term, req):
+                t.cancel()
 
         try:
             self.loop.run_until_complete(main())
-            if not self._stopping:
-                log.warning("gRPC aio server terminated without stop()")
         except BaseException as e:  # noqa: BLE001 - reported to the constructor / stop()
             self._err = e
             self._ready.set()
             log.error("gRPC aio server loop ended with %r", e)
         finally:
+            try:
+                if self._server is not None and not self.stop_completed:  # main did not get to stop it (the loop
+                    # was stopped from outside, or main failed): stop it here, while the loop still runs tasks,
+                    # so grpc's own finaliser never schedules onto a closed loop
+                    self.loop.run_until_complete(asyncio.wait_for(self._server.stop(0), 10))
+                # servicer coroutines of calls the stop cancelled: finish them here, not in a dead loop
+                pending = [t for t in asyncio.all_tasks(self.loop) if not t.done()]
+                for t in pending:
+                    t.cancel()
+                if pending:
+                    self.loop.run_until_complete(asyncio.wait_for(asyncio.gather(*pending, return_exceptions=True),
+                                                                  10))
+            except BaseException as e:  # noqa: BLE001 - best effort; the thread must end
+                log.warning("gRPC aio server loop clean-up: %r", e)
+            if not self.loop.is_running():
+                self.loop.close()
             self._stopped = True
 
     def stop(self, grace: Optional[float] = None):
-        """Stop serving; ``.wait(timeout)`` joins the loop thread. A loop that already ended (its server
-        terminated or failed) has nothing to stop: scheduling onto it would never complete."""
+        """Ask the loop to stop the server (it runs ``server.stop(grace)`` itself); ``.wait(timeout)`` joins the
+        loop thread. A loop that already ended has nothing to stop."""
         th = self._thread
         self._stopping = True
-        with self._stop_lock:
-            live = not getattr(self, "_stopped", False) and th.is_alive() and self.loop.is_running()
-            fut = asyncio.run_coroutine_threadsafe(self._server.stop(grace), self.loop) if live else None
+        self._grace = grace
+        if th.is_alive() and self._stop_ev is not None and not self.loop.is_closed():
+            try:
+                self.loop.call_soon_threadsafe(self._stop_ev.set)
+            except RuntimeError:  # closed between the check and the call
+                pass
 
         class _Done:
             def wait(self, timeout: Optional[float] = None) -> bool:
-                if fut is not None:
-                    t0 = time.perf_counter()
-                    while not fut.done():  # polled: the loop may end (and drop the callback) meanwhile
-                        if not th.is_alive() or (timeout is not None and time.perf_counter() - t0 > timeout):
-                            break
-                        time.sleep(0.01)
                 th.join(timeout)
                 return not th.is_alive()
         return _Done()
@@ -213,7 +246,10 @@ class _LoopSink:
         self.loop = loop
 
     def __call__(self, items):
-        self.loop.call_soon_threadsafe(_fanout, items)
+        try:
+            self.loop.call_soon_threadsafe(_fanout, items)
+        except RuntimeError:  # the server stopped and closed its loop: the streams' receivers are gone
+            pass
 
 
 class EngineServicer:

@@ -333,3 +333,40 @@ def test_aio_server_stop_after_its_loop_ended(driver):
     assert time.perf_counter() - t0 < 5
     ok = serve(EngineServicer(drv, tok), port=0, host="127.0.0.1")  # the normal path still stops cleanly
     assert ok.stop(0).wait(30)
+
+
+def test_aio_server_stop_completes_on_its_own_loop(driver):
+    """Root cause of round 4's stuck stop (profiles/r4_serving): the server signals termination part-way through
+    its own stop(), so a stop coroutine scheduled from outside raced the loop's exit and never finished. Now the
+    loop's main task runs server.stop(grace) itself: with streams in flight, stop().wait() returns, the stop ran
+    to the end (stop_completed), the streams end, pending servicer tasks are drained, the loop is closed and the
+    port refuses new calls - five times in a row."""
+    import threading
+
+    drv, tok, m = driver
+    for _ in range(5):
+        server = serve(EngineServicer(drv, tok), port=0, host="127.0.0.1")
+        ch = grpc.insecure_channel(f"127.0.0.1:{server.bound_port}")
+        stub = Stub(ch)
+        got, errs = [], []
+
+        def stream():
+            try:
+                for t in stub.GenerateStream(GenerateRequest(prompt="hello world", max_new_tokens=400, is_greedy=True,
+                                                             ignore_eos=True), timeout=60):
+                    got.append(t)
+            except grpc.RpcError as e:
+                errs.append(e.code())
+        th = threading.Thread(target=stream)
+        th.start()
+        t0 = time.perf_counter()
+        while not got and time.perf_counter() - t0 < 30:
+            time.sleep(0.01)
+        assert got, "stream never started"
+        assert server.stop(0.2).wait(30)
+        assert server.stop_completed and server.loop.is_closed()
+        th.join(30)
+        assert not th.is_alive()
+        with pytest.raises(grpc.RpcError):
+            stub.Generate(GenerateRequest(prompt="x", max_new_tokens=1), timeout=5)
+        ch.close()
