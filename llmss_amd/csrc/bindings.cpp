@@ -12,7 +12,7 @@ namespace py = pybind11;
 
 void launch_add_norm(const void* x, int64_t x_stride, const void* res_in, void* res_out, const void* w, const void* b,
                      void* y, int64_t y_stride, int T, int H, float eps, bool rms, hipStream_t st, void* q8,
-                     void* s8);
+                     void* s8, int xcw);
 void launch_embed(const void* ids, const void* pos, const void* wte, const void* wpe, void* out, int T, int H,
                   int vocab, hipStream_t st);
 void launch_rope_cache(void* qkv, int64_t row_stride, const void* pos, const void* cos_t, const void* sin_t, void* kc,
@@ -83,12 +83,12 @@ void register_ctrl(py::module_& m);     // shared-memory control ring (ctrl.cpp)
 PYBIND11_MODULE(_C, m) {
   m.doc() = "llmss_amd gfx950 HIP kernels + native runtime";
   m.def("add_norm", [](uintptr_t x, int64_t xs, uintptr_t ri, uintptr_t ro, uintptr_t w, uintptr_t b, uintptr_t y,
-                       int64_t ys, int T, int H, float eps, bool rms, uintptr_t st, uintptr_t q8, uintptr_t s8) {
-    launch_add_norm(CP(x), xs, CP(ri), P(ro), CP(w), CP(b), P(y), ys, T, H, eps, rms, S(st), P(q8), P(s8));
+                       int64_t ys, int T, int H, float eps, bool rms, uintptr_t st, uintptr_t q8, uintptr_t s8, int xcw) {
+    launch_add_norm(CP(x), xs, CP(ri), P(ro), CP(w), CP(b), P(y), ys, T, H, eps, rms, S(st), P(q8), P(s8), xcw);
   }, pybind11::arg("x"), pybind11::arg("xs"), pybind11::arg("ri"), pybind11::arg("ro"), pybind11::arg("w"),
      pybind11::arg("b"), pybind11::arg("y"), pybind11::arg("ys"), pybind11::arg("T"), pybind11::arg("H"),
      pybind11::arg("eps"), pybind11::arg("rms"), pybind11::arg("st"), pybind11::arg("q8") = 0,
-     pybind11::arg("s8") = 0);
+     pybind11::arg("s8") = 0, pybind11::arg("xcw") = 0);
   m.def("embed", [](uintptr_t ids, uintptr_t pos, uintptr_t wte, uintptr_t wpe, uintptr_t out, int T, int H, int V,
                     uintptr_t st) { launch_embed(CP(ids), CP(pos), CP(wte), CP(wpe), P(out), T, H, V, S(st)); });
   m.def("rope_cache", [](uintptr_t qkv, int64_t rs, uintptr_t pos, uintptr_t cos_t, uintptr_t sin_t, uintptr_t kc,

@@ -24,7 +24,7 @@ __global__ __launch_bounds__(256) void add_norm_kernel(const bf16_t* __restrict_
                                                        bf16_t* __restrict__ y, int64_t y_stride, int H, float eps,
                                                        const float* __restrict__ part, int S, int64_t slab,
                                                        const bf16_t* __restrict__ xbias, unsigned char* __restrict__ q8,
-                                                       float* __restrict__ s8) {
+                                                       float* __restrict__ s8, int xcw) {
   __shared__ float red[32];
   __shared__ float red2[32];
   const int row = blockIdx.x;
@@ -74,7 +74,10 @@ __global__ __launch_bounds__(256) void add_norm_kernel(const bf16_t* __restrict_
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[c][j] = bf2f(f2bf(v[c][j]));  // the GEMM output is bf16 in the unfused path
       } else {
-        u16x8 a = *reinterpret_cast<const u16x8*>(xr + ch * 8);
+        // xcw > 0: column-chunked input [C][T][xcw] (the decoder's column-chunked all-reduce schedule)
+        const bf16_t* xp = xcw > 0 ? x + (int64_t)(ch * 8 / xcw) * gridDim.x * xcw + (int64_t)row * xcw + (ch * 8) % xcw
+                                   : xr + ch * 8;
+        u16x8 a = *reinterpret_cast<const u16x8*>(xp);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[c][j] = bf2f(a[j]);
       }
@@ -160,19 +163,19 @@ template <bool RMS, bool HAS_RES, bool HAS_BIAS, int PART = 0>
 static void launch_norm_t(const bf16_t* x, int64_t xs, const bf16_t* ri, bf16_t* ro, const bf16_t* w,
                           const bf16_t* b, bf16_t* y, int64_t ys, int T, int H, float eps, hipStream_t st,
                           const float* part = nullptr, int S = 0, int64_t slab = 0, const bf16_t* xbias = nullptr,
-                          unsigned char* q8 = nullptr, float* s8 = nullptr) {
+                          unsigned char* q8 = nullptr, float* s8 = nullptr, int xcw = 0) {
   const int nchunk = H / 8;
   int threads = nchunk <= 256 ? ((nchunk + 63) / 64) * 64 : 256;
   const int maxc = (nchunk + threads - 1) / threads;
   dim3 grid(T), block(threads);
   if (maxc == 1)
-    add_norm_kernel<1, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias, q8, s8);
+    add_norm_kernel<1, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias, q8, s8, xcw);
   else if (maxc == 2)
-    add_norm_kernel<2, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias, q8, s8);
+    add_norm_kernel<2, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias, q8, s8, xcw);
   else if (maxc <= 4)
-    add_norm_kernel<4, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias, q8, s8);
+    add_norm_kernel<4, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias, q8, s8, xcw);
   else if (maxc <= 8)
-    add_norm_kernel<8, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias, q8, s8);
+    add_norm_kernel<8, RMS, HAS_RES, HAS_BIAS, PART><<<grid, block, 0, st>>>(x, xs, ri, ro, w, b, y, ys, H, eps, part, S, slab, xbias, q8, s8, xcw);
   else
     throw std::runtime_error("add_norm: hidden size too large (max 16384)");
   HIP_CHECK_LAUNCH();
@@ -180,10 +183,11 @@ static void launch_norm_t(const bf16_t* x, int64_t xs, const bf16_t* ri, bf16_t*
 
 void launch_add_norm(const void* x, int64_t x_stride, const void* res_in, void* res_out, const void* w,
                      const void* b, void* y, int64_t y_stride, int T, int H, float eps, bool rms,
-                     hipStream_t st, void* q8v, void* s8v) {
+                     hipStream_t st, void* q8v, void* s8v, int xcw) {
   auto Q8 = (unsigned char*)q8v;
   auto S8 = (float*)s8v;
   if (H % 8 != 0) throw std::runtime_error("add_norm: hidden size must be a multiple of 8");
+  if (xcw < 0 || xcw % 8 || (xcw && H % xcw)) throw std::runtime_error("add_norm: chunk width must divide H, multiple of 8");
   if (T == 0) return;
   auto X = (const bf16_t*)x;
   auto RI = (const bf16_t*)res_in;
@@ -193,15 +197,15 @@ void launch_add_norm(const void* x, int64_t x_stride, const void* res_in, void* 
   auto Y = (bf16_t*)y;
   const bool has_res = res_in != nullptr, has_b = b != nullptr;
   if (rms) {
-    if (has_res) launch_norm_t<true, true, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8);
-    else launch_norm_t<true, false, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8);
+    if (has_res) launch_norm_t<true, true, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8, xcw);
+    else launch_norm_t<true, false, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8, xcw);
   } else {
     if (has_res) {
-      if (has_b) launch_norm_t<false, true, true>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8);
-      else launch_norm_t<false, true, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8);
+      if (has_b) launch_norm_t<false, true, true>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8, xcw);
+      else launch_norm_t<false, true, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8, xcw);
     } else {
-      if (has_b) launch_norm_t<false, false, true>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8);
-      else launch_norm_t<false, false, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8);
+      if (has_b) launch_norm_t<false, false, true>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8, xcw);
+      else launch_norm_t<false, false, false>(X, x_stride, RI, RO, W, B, Y, y_stride, T, H, eps, st, nullptr, 0, 0, nullptr, Q8, S8, xcw);
     }
   }
 }

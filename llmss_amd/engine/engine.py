@@ -196,8 +196,10 @@ class LLMEngine:
             self.buckets.append(max_num_seqs)
         self._tbo_cands = self._tbo_candidates()
         self._rsag_cands = self._rsag_candidates()
+        self._col_cands = self._col_candidates()
         # bucket -> decode schedule the capture-time A/B kept: "one" (all-reduce per row-parallel output),
-        # "tbo" (two interleaved micro-batches) or "rsag" (row-sharded: reduce-scatter / all-gather)
+        # "tbo" (two interleaved micro-batches), "rsag" (row-sharded: reduce-scatter / all-gather) or "col"
+        # (column-chunked all-reduces beside the next chunk's GEMM)
         self.decode_schedule: Dict[int, str] = {}
         self.tp.check_consistent("LLMEngine", self.fingerprint())
         self.buf = _DecodeBuffers(self.buckets[-1], self.max_blocks, self.device) if self.is_gpu else None
@@ -240,7 +242,7 @@ class LLMEngine:
                     torch.cuda.synchronize()
                 self.graphs.clear()
                 self.use_graphs = False
-            elif self._tbo_cands or self._rsag_cands:
+            elif self._tbo_cands or self._rsag_cands or self._col_cands:
                 self._schedule_ab(self._graph_pool, self._graph_modes)
         self.tp.check_consistent("LLMEngine (after graph capture)", self.fingerprint())
 
@@ -258,6 +260,7 @@ class LLMEngine:
                 "overlap_rows": self.model.overlap_rows, "bucket_bytes": self.model.bucket_bytes,
                 "tbo_min": self.model.tbo_min, "graph_keys": sorted(self.graphs),
                 "decode_schedule": sorted(self.decode_schedule.items()), "rsag_mode": self.model.rsag_mode,
+                "col": [self.model.col_mode, self.model.col_chunks, sorted(self.model.col)],
                 "fp8": any(L.qkv.w_scale is not None for L in self.model.w.layers[:1])}
 
     def _default_buckets(self):
@@ -364,6 +367,20 @@ class LLMEngine:
             return []
         lo = int(os.environ.get("LLMSS_TP_RSAG_MIN", str(8 * self.tp.size)))
         return [b for b in self.buckets if b >= lo and m.rsag_ok(b)]
+
+    def _col_candidates(self) -> List[int]:
+        """Decode buckets whose column-chunked schedule (DecoderLM._reduce_cols: each row-parallel projection as
+        LLMSS_TP_COL chunks over disjoint weight-row slices, chunk c's all-reduce on the comm stream beside chunk
+        c + 1's GEMM) is timed against the single all-reduce at capture: real multi-rank communicator, "auto" mode,
+        sequential-block models whose o / down widths split into 8-aligned chunks."""
+        m = self.model
+        if not (self.is_gpu and self.tp.is_real and not self.tp.host_staged and m.col_mode == "auto"):
+            return []
+        L = m.w.layers[0]
+        if self.cfg.parallel_block or not (m.col_ok(L.o) and m.col_ok(L.down)):
+            return []
+        lo = int(os.environ.get("LLMSS_TP_COL_MIN", "1"))
+        return [b for b in self.buckets if b >= lo]
 
     def _tbo_half(self, b: int) -> int:
         if b not in getattr(self, "_tbo_cands", ()):
@@ -783,23 +800,29 @@ class LLMEngine:
     def _schedule(self, b: int, name: str):
         """Decode bucket ``b`` runs schedule ``name`` inside the block (capture / warm-up of an A/B variant)."""
         m = self.model
-        old_tbo, had = m.tbo_min, b in m.rsag
+        old_tbo, had, had_col = m.tbo_min, b in m.rsag, b in m.col
         if name == "tbo":
             m.tbo_min = b
         elif name == "rsag":
             m.rsag.add(b)
+        elif name == "col":
+            m.col.add(b)
         try:
             yield
         finally:
             m.tbo_min = old_tbo
             if name == "rsag" and not had:
                 m.rsag.discard(b)
+            if name == "col" and not had_col:
+                m.col.discard(b)
 
     def _schedule_ab(self, pool, modes):
         """Capture-time A/B of the decode schedules on the real communicator: per candidate bucket the
         all-reduce graph ("one") against the two-micro-batch one ("tbo": each half's all-reduces on the comm
         stream while the other half computes, DecoderLM._hidden_states_overlap) and the row-sharded one ("rsag":
-        reduce-scatter, add + norm on M / tp rows, all-gather, DecoderLM._hidden_states_rsag). Each graph is
+        reduce-scatter, add + norm on M / tp rows, all-gather, DecoderLM._hidden_states_rsag) and the column-chunked
+        one ("col": each row-parallel output as C weight-row slices whose all-reduces run beside the next slice's
+        GEMM, DecoderLM._reduce_cols). Each graph is
         replayed with a realistic context length (the bench's 128 + 64 average), every rank's times are
         gathered and the max over ranks decides, so all ranks keep the same graph; an alternative must beat
         "one" by 3 %. Which wins depends on what collectives cost on the node - hence measured, not assumed
@@ -810,7 +833,8 @@ class LLMEngine:
         nblk = -(-ctx // self.block_size)
         if nblk > self.num_blocks:
             return
-        variants = {b: [n for n, c in (("tbo", self._tbo_cands), ("rsag", self._rsag_cands)) if b in c]
+        variants = {b: [n for n, c in (("tbo", self._tbo_cands), ("rsag", self._rsag_cands), ("col", self._col_cands))
+                        if b in c]
                     for b in self.buckets}
         variants = {b: v for b, v in variants.items() if v}
         alt, times = {}, {}
@@ -884,6 +908,8 @@ class LLMEngine:
                 self.graphs[(b, d)] = alt[(b, d, best)]
             if best == "rsag":  # eager steps of this bucket (none while its graph exists) take it too
                 m.rsag.add(b)
+            if best == "col":
+                m.col.add(b)
             if self.decode_schedule.get(b, "one") == "one":
                 self.decode_schedule[b] = best
             self.stats.setdefault("schedule_ab_ms", {})[f"{b}{'c' if d else 'g'}"] = \

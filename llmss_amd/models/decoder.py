@@ -115,6 +115,15 @@ class DecoderLM:
         # the engine's capture-time A/B picks on the real communicator, 0 never
         self.rsag_mode = os.environ.get("LLMSS_TP_RSAG", "auto")
         self.rsag: set = set()
+        # column-chunked decode schedule (TP > 1, _reduce_cols): each row-parallel projection runs as C GEMMs over
+        # disjoint output-column slices of its weight (no weight byte read twice); chunk c's all-reduce goes to the
+        # priority comm stream while chunk c + 1's GEMM runs, and add_norm reads the chunk-major result. Decode
+        # batch sizes in `col` take it: LLMSS_TP_COL=C (> 1) every decode step with C chunks, "auto" (default) the
+        # buckets the engine's capture-time A/B picks (4 chunks), 0 never
+        col = os.environ.get("LLMSS_TP_COL", "auto")
+        self.col_mode = "auto" if col == "auto" else ("force" if int(col) > 1 else "0")
+        self.col_chunks = int(col) if col not in ("auto", "0", "1") else 4
+        self.col: set = set()
         self._cu_decode = {}
         self._comm_stream = None
 
@@ -257,6 +266,40 @@ class DecoderLM:
             outs.append(y)
         cur.wait_stream(comm)
         return torch.cat(outs)
+
+    def col_ok(self, lin) -> bool:
+        """Can this row-parallel projection run column-chunked (_reduce_cols)?"""
+        C = self.col_chunks
+        return (self.tp.comm_active and C > 1 and not lin.packed and not lin.glu and lin.N % (8 * C) == 0)
+
+    def _reduce_cols(self, lin, x, pre=None) -> torch.Tensor:
+        """``all_reduce(lin(pre(x) if pre else x))`` as C column chunks (the "col" decode schedule): chunk c is the
+        GEMM over output features [c N/C, (c + 1) N/C) - a disjoint slice of the weight rows, so every weight byte is
+        read once - into its own contiguous [M, N/C] block of a chunk-major [C, M, N/C] buffer, and its all-reduce
+        is issued on the priority comm stream at once, while the compute stream already runs chunk c + 1's GEMM.
+        The compute stream waits for the comm stream once, after the last chunk; add_norm reads the chunk-major
+        layout directly. Reference: the synchronous row-parallel all-reduce, ``layers.py:175-179``."""
+        h = pre(x) if pre is not None else x
+        C, N = self.col_chunks, lin.N
+        cw = N // C
+        M = h.shape[0]
+        out = torch.empty(C, M, cw, dtype=h.dtype, device=h.device)
+        if not h.is_cuda:  # gloo / CPU: same chunks and collectives, no streams
+            for c in range(C):
+                out[c].copy_(lin.rows(c * cw, (c + 1) * cw)(h))
+                self.tp.all_reduce(out[c])
+            return out
+        cur = torch.cuda.current_stream()
+        comm = self._comm(h.device)
+        H = _hip_ops()
+        for c in range(C):
+            sl = lin.rows(c * cw, (c + 1) * cw)
+            H.linear(h, sl.w, sl.b, w_scale=sl.w_scale, out=out[c])
+            comm.wait_stream(cur)  # chunk c's GEMM done
+            with torch.cuda.stream(comm):
+                self.tp.all_reduce(out[c])
+        cur.wait_stream(comm)
+        return out
 
     # ------------------------------------------------------- two-micro-batch decode overlap
     def overlap_split(self, B: int) -> int:
@@ -416,6 +459,8 @@ class DecoderLM:
         residual = None
         delta = x
         fuse = self.tp.size == 1  # split-K partials can skip their own reduce only without a TP all-reduce
+        col = (inp.kind == "decode" and not cfg.parallel_block and self.col_ok(w.layers[0].o)
+               and self.col_ok(w.layers[0].down) and (self.col_mode == "force" or inp.input_ids.shape[0] in self.col))
         for i, L in enumerate(w.layers):
             kc, vc = kv_caches[i]
             y, residual = ops.add_norm(delta, L.ln1_w, L.ln1_b, eps, rms, residual, fp8_out=self._fp8_in(L.qkv, delta))
@@ -423,6 +468,10 @@ class DecoderLM:
             a = self._attention(L, y, inp, kc, vc)
             if cfg.parallel_block:  # GPT-J: one all-reduce for attention + MLP
                 delta = self._reduce_rows(lambda a_, y_: L.o(a_).add_(L.down(L.up(y_, self.act))), a, y)
+            elif col:  # column-chunked all-reduces overlapping the next chunk's GEMM (_reduce_cols)
+                o = self._reduce_cols(L.o, a)
+                y2, residual = ops.add_norm(o, L.ln2_w, L.ln2_b, eps, rms, residual, fp8_out=self._fp8_in(L.up, a))
+                delta = self._reduce_cols(L.down, y2, pre=lambda y_: L.up(y_, self.act))
             elif fuse:
                 # TP=1: the split-K partials of o / down are reduced inside the next add_norm
                 o = L.o(a, partial_ok=True)

@@ -93,6 +93,14 @@ class Linear:
     def K(self) -> int:
         return self.k if self.packed else self.w.shape[1]
 
+    def rows(self, r0: int, r1: int) -> "Linear":
+        """Output features [r0, r1) of a row-major linear as a Linear over views (no copy): the weight slice a
+        column chunk of a row-parallel projection reads (DecoderLM._reduce_cols)."""
+        if self.packed or self.glu:
+            raise ValueError("row slices of packed / SwiGLU linears are not supported")
+        return Linear(self.w[r0:r1], None if self.b is None else self.b[r0:r1],
+                      None if self.w_scale is None else self.w_scale[r0:r1], False)
+
     def dense(self) -> torch.Tensor:
         """The [N, K] row-major weight (a copy when packed)."""
         return ref.unpack_weight(self.w, self.k) if self.packed else self.w

@@ -29,6 +29,8 @@ def add_norm(x, weight, bias, eps, rms, residual=None, out=None, fp8_out=False):
     """``fp8_out`` (GPU): also emit the output's per-token fp8 twin for a W8A8 consumer (ops/hip.py)."""
     if x.is_cuda:
         return _hip().add_norm(x, weight, bias, eps, rms, residual, out=out, fp8_out=fp8_out)
+    if x.dim() == 3:  # column-chunked [C, T, CW] -> [T, C * CW]
+        x = x.permute(1, 0, 2).reshape(x.shape[1], -1)
     y, r = ref.add_norm(x, weight, bias, eps, rms, residual)
     if out is not None:
         out.copy_(y)

@@ -78,8 +78,14 @@ def add_norm(x, weight, bias, eps, rms, residual=None, out=None, residual_out=No
     GEMM that consumes it next, which then skips its own quantisation launch."""
     if isinstance(x, PartialSum):
         return add_norm_partial(x, weight, bias, eps, rms, residual, out, fp8_out=fp8_out)
-    T, H = x.shape
-    _bf16_rows(x, "x")
+    xcw = 0
+    if x.dim() == 3:  # column-chunked [C, T, CW] (DecoderLM._reduce_cols): row t is x[:, t, :] concatenated
+        _check(x.is_contiguous() and x.dtype == torch.bfloat16 and x.shape[2] % 8 == 0, "chunked x [C, T, CW]")
+        C, T, xcw = x.shape
+        H = C * xcw
+    else:
+        T, H = x.shape
+        _bf16_rows(x, "x")
     _check(H % 8 == 0, "hidden must be a multiple of 8")
     _check(weight.is_contiguous() and weight.numel() == H and weight.dtype == torch.bfloat16, "norm weight")
     if bias is not None:
@@ -93,8 +99,11 @@ def add_norm(x, weight, bias, eps, rms, residual=None, out=None, residual_out=No
     else:
         ro = None
     q8, s8 = _fp8_twin(y) if fp8_out else (None, None)
-    lib().add_norm(x.data_ptr(), x.stride(0), _ptr(residual), _ptr(ro), weight.data_ptr(), _ptr(bias),
-                   y.data_ptr(), y.stride(0), T, H, float(eps), bool(rms), _stream(), _ptr(q8), _ptr(s8))
+    lib().add_norm(x.data_ptr(), x.stride(0) if not xcw else xcw, _ptr(residual), _ptr(ro), weight.data_ptr(),
+                   _ptr(bias), y.data_ptr(), y.stride(0), T, H, float(eps), bool(rms), _stream(), _ptr(q8), _ptr(s8),
+                   xcw)
+    if residual is None and xcw:
+        raise ValueError("a column-chunked add_norm input needs a residual (its residual output is row-major)")
     return y, (ro if residual is not None else x)
 
 

@@ -134,6 +134,7 @@ def test_decode_overlap_ab_at_capture(comm, monkeypatch):
 
     monkeypatch.setenv("LLMSS_TBO_AUTO_MIN", "16")
     monkeypatch.setenv("LLMSS_TP_RSAG", "0")  # the one-rank stand-in's reduce-scatter is no TP=2 reduce-scatter
+    monkeypatch.setenv("LLMSS_TP_COL", "0")  # A/B of the micro-batch schedule alone (col: its own test below)
     tp = OneRankNative(0, 2, comm=comm)
     cfg = get_preset("tiny-llama", hidden_size=256, num_heads=4, num_kv_heads=2, head_dim=64, rotary_dim=64,
                      intermediate_size=512, max_position_embeddings=256)
@@ -262,3 +263,49 @@ def test_rccl_init_deadline_without_peer():
     torch.cuda.synchronize()
     assert bool((x == 1).all())
     c.destroy()
+
+
+def test_col_schedule_ab_at_capture(comm, monkeypatch):
+    """the column-chunked decode schedule (DecoderLM._reduce_cols: each row-parallel output
+    as weight-row slices whose all-reduces run on the comm stream beside the next slice's GEMM) is a fourth
+    capture-time A/B candidate on a native-comm TP group: both timings recorded, one graph kept per bucket, and
+    what it keeps decodes exactly like eager (one-rank stand-in for TP=2, as the micro-batch A/B test)."""
+    from llmss_amd.engine import LLMEngine, SamplingParams
+    from llmss_amd.models.config import get_preset
+    from llmss_amd.models.decoder import DecoderLM
+    from llmss_amd.models.weights import random_weights
+    from llmss_amd.parallel.dist import TPGroup
+
+    class OneRankNative(TPGroup):
+        def all_gather_last_dim(self, t):
+            t = t.contiguous()
+            out = torch.empty_like(t)
+            self.comm.all_gather(t.data_ptr(), out.data_ptr(), t.numel(), self._code(t), _st())
+            return torch.cat([out, out], -1)
+
+        def all_reduce_int(self, v, op="min"):
+            return int(v)
+
+        def check_consistent(self, what, fp):
+            pass
+
+        def all_gather_object(self, obj):
+            return [obj, obj]
+
+    monkeypatch.setenv("LLMSS_TBO_AUTO", "0")
+    monkeypatch.setenv("LLMSS_TP_RSAG", "0")
+    monkeypatch.setenv("LLMSS_TP_COL", "auto")
+    monkeypatch.setenv("LLMSS_TP_COL_MIN", "8")
+    tp = OneRankNative(0, 2, comm=comm)
+    cfg = get_preset("tiny-llama", hidden_size=256, num_heads=4, num_kv_heads=2, head_dim=64, rotary_dim=64,
+                     intermediate_size=512, max_position_embeddings=256)
+    m = DecoderLM(cfg, random_weights(cfg, 2, 0, device="cuda", dtype=torch.bfloat16, seed=5, std=0.05), tp)
+    prompts = [[int(x) for x in torch.randint(0, cfg.vocab_size, (n,))] for n in range(3, 23)]
+    sp = SamplingParams(max_new_tokens=10, is_greedy=True, ignore_eos=True)
+    e = LLMEngine(m, max_num_seqs=24, block_size=16, use_graphs=True, autotune=False, graph_buckets=[1, 8, 16, 24])
+    assert e._col_cands == [8, 16, 24] and set(e.stats["schedule_ab_ms"]) >= {"8c", "16c", "24c"}
+    assert all(set(v) == {"one", "col"} for v in e.stats["schedule_ab_ms"].values())
+    out_g = e.generate(prompts, sp)
+    del e
+    e2 = LLMEngine(m, max_num_seqs=24, block_size=16, use_graphs=False, autotune=False)
+    assert e2.generate(prompts, sp) == out_g

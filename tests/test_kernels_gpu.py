@@ -50,6 +50,23 @@ def test_add_norm(T, Hd, rms):
     close(y2, y2_ref, 3e-2)
 
 
+@pytest.mark.parametrize("T,Hd,C", [(7, 1600, 2), (33, 4096, 4), (64, 4096, 8), (5, 5120, 5)])
+@pytest.mark.parametrize("rms", [False, True])
+def test_add_norm_column_chunked(T, Hd, C, rms):
+    """add_norm reading the column-chunked [C, T, Hd / C] layout of the "col" decode schedule
+    (DecoderLM._reduce_cols) equals the row-major call on the same values (bitwise: same loads, same order)."""
+    torch.manual_seed(0)
+    x, r = rnd(T, Hd), rnd(T, Hd)
+    w, b = rnd(Hd, scale=0.5) + 1, (None if rms else rnd(Hd, scale=0.1))
+    xc = x.view(T, C, Hd // C).permute(1, 0, 2).contiguous()
+    r1, r2 = r.clone(), r.clone()
+    y, ro = H.add_norm(x, w, b, 1e-5, rms, residual=r1)
+    yc, roc = H.add_norm(xc, w, b, 1e-5, rms, residual=r2)
+    assert torch.equal(y, yc) and torch.equal(ro, roc)
+    y_ref, _ = R.add_norm(x, w, b, 1e-5, rms, r.clone())
+    close(yc, y_ref, 3e-2)
+
+
 def test_embed():
     torch.manual_seed(0)
     wte, wpe = rnd(1000, 256), rnd(64, 256)

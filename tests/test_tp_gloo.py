@@ -38,12 +38,15 @@ def _worker(rank, world, port, ckpt, prompts, q, env=None):
     if (env or {}).get("LLMSS_TP_RSAG") == "1":  # the row-sharded decode schedule really runs
         inner = m._hidden_states_rsag
         m._hidden_states_rsag = lambda *a_, **k_: (calls.__setitem__(0, calls[0] + 1), inner(*a_, **k_))[1]
+    if (env or {}).get("LLMSS_TP_COL"):  # the column-chunked decode schedule really runs
+        inner_c = m._reduce_cols
+        m._reduce_cols = lambda *a_, **k_: (calls.__setitem__(0, calls[0] + 1), inner_c(*a_, **k_))[1]
     eng = LLMEngine(m, max_num_seqs=4, block_size=4, num_blocks=64, check_tokens=True)
     greedy = eng.generate(prompts, SamplingParams(max_new_tokens=8, is_greedy=True, ignore_eos=True))
     sampled = eng.generate(prompts, [SamplingParams(max_new_tokens=8, temperature=0.9, top_k=20, top_p=0.9, seed=5 + i,
                                                     ignore_eos=True) for i in range(len(prompts))])
-    if (env or {}).get("LLMSS_TP_RSAG") == "1":
-        assert calls[0] > 0, "row-sharded decode schedule never ran"
+    if (env or {}).get("LLMSS_TP_RSAG") == "1" or (env or {}).get("LLMSS_TP_COL"):
+        assert calls[0] > 0, "the forced decode schedule never ran"
     if r == 0:
         q.put((greedy, sampled))
     torch.distributed.barrier()
@@ -70,6 +73,7 @@ _ROWS = {"LLMSS_TP_OVERLAP_ROWS": "4"}
 _TBO = {"LLMSS_TP_DECODE_OVERLAP_MIN": "2"}
 _PTBO = {"LLMSS_TP_PREFILL_OVERLAP_MIN": "2"}  # prefill steps as two micro-batches split at a sequence boundary
 _RSAG = {"LLMSS_TP_RSAG": "1"}  # row-sharded decode: reduce-scatter -> add + norm on M / tp rows -> all-gather
+_COL = {"LLMSS_TP_COL": "2"}  # column-chunked decode: row-parallel outputs as 2 weight-row slices, one AR each
 
 
 @pytest.mark.parametrize("name,world,overlap", [("llama", 2, None), ("gptj", 2, None), ("bigcode", 4, None),
@@ -79,7 +83,8 @@ _RSAG = {"LLMSS_TP_RSAG": "1"}  # row-sharded decode: reduce-scatter -> add + no
                                                 ("gptj", 2, _TBO), ("bigcode", 4, _TBO), ("llama", 2, _PTBO),
                                                 ("gptj", 2, _PTBO), ("bigcode", 4, {**_PTBO, **_TBO}),
                                                 ("llama", 2, _RSAG), ("gptj", 2, _RSAG), ("bigcode", 4, _RSAG),
-                                                ("gpt2", 4, _RSAG)])
+                                                ("gpt2", 4, _RSAG), ("llama", 2, _COL), ("gpt2", 2, _COL),
+                                                ("bigcode", 4, {"LLMSS_TP_COL": "4"})])
 def test_tp_matches_single(tmp_path, name, world, overlap):
     d = str(tmp_path / name)
     save_hf_model(name, d, vocab=101)  # 101 % world != 0 -> exercises the padded vocab-parallel head
