@@ -207,6 +207,14 @@ def model_shapes(model) -> Dict[str, GemmShape]:
 
     out = {"qkv": shp(L.qkv, True), "o": shp(L.o, fuse), "up": shp(L.up, False, act), "down": shp(L.down, fuse)}
     out["head"] = shp(model.w.head, False)
+    # the column-chunked decode schedule's slices of o / down (DecoderLM._reduce_cols): whenever it may run - forced,
+    # or a candidate of the engine's capture-time A/B on a real communicator - so the A/B compares tuned plans
+    col_mode = getattr(model, "col_mode", "0")
+    if (not model.cfg.parallel_block and (col_mode == "force" or (col_mode == "auto" and model.tp.is_real))
+            and model.col_ok(L.o) and model.col_ok(L.down)):
+        C = model.col_chunks
+        out["o_col"] = GemmShape(L.o.N // C, L.o.K, False, L.o.w_scale is not None, False, "none", False)
+        out["down_col"] = GemmShape(L.down.N // C, L.down.K, False, L.down.w_scale is not None, False, "none", False)
     return out
 
 
