@@ -413,6 +413,132 @@ __global__ __launch_bounds__(256, 1) void qq_gemm_kernel(const bf16_t* __restric
                                                act, glu);
 }
 
+// 4 waves x 128x128 on the 32x32x16 MFMA (acc 4x4 f32x16 = 256 registers: fewer, larger accumulator objects than
+// qq_gemm_kernel's 8x8 f32x4). LDS rows of 128 B with the chunk swizzle f(row) = (row >> 1) & 7, conflict-free for
+// the 32-row ds_read_b128 fragments. Per K-tile: 4 k-steps of 16, fragments double-buffered across k-steps, the
+// next K-tile's 16 LDS-DMA per wave spread 4 per k-step, one barrier per K-tile. Epilogue: direct bf16 stores.
+template <int VAR>
+__global__ __launch_bounds__(256, 1) void qq2_gemm_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                          const bf16_t* __restrict__ B, int64_t ldb,
+                                                          const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
+                                                          int64_t ldy, int M, int N, int K, int act, int glu,
+                                                          int group_m) {
+  constexpr int HALF = 32768, BUF = 2 * HALF;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r32 = lane & 31, h = lane >> 5;
+  const int wr = w >> 1, wc = w & 1;
+  const int ntn = (N + 255) / 256, ntm = (M + 255) / 256;
+  const int GM = group_m;
+  const int tile = xcd_remap(blockIdx.x, ntn * ntm);
+  const int grp = tile / (GM * ntn), gidx = tile - grp * (GM * ntn);
+  const int gm = min(GM, ntm - grp * GM);
+  const int m0 = (grp * GM + gidx % gm) * 256, n0 = (gidx / gm) * 256;
+  const int nk = K / 64;
+
+  int64_t soff[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int inst = (j & 7) * 4 + w;
+    const int r = inst * 8 + (lane >> 3);
+    const int gc = (lane & 7) ^ ((r >> 1) & 7);
+    const int gr = j < 8 ? min(m0 + r, M - 1) : min(n0 + r, N - 1);
+    soff[j] = (int64_t)gr * (j < 8 ? lda : ldb) * 2 + gc * 16;
+  }
+  auto glds = [&](int j, int t, char* buf) {
+    const char* s = (const char*)(j < 8 ? (const void*)A : (const void*)B);
+    __builtin_amdgcn_global_load_lds((const void*)(s + soff[j] + (int64_t)t * 128),
+                                     (LDS_AS void*)(buf + (j >> 3) * HALF + (j & 7) * 4096 + w * 1024), 16, 0, 0);
+  };
+  int aoff[4][4], boff[4][4];  // [tile][k-step]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int c = 2 * ks + h;
+      const int ra = wr * 128 + i * 32 + r32, rb = wc * 128 + i * 32 + r32;
+      aoff[i][ks] = ra * 128 + ((c ^ ((ra >> 1) & 7)) << 4);
+      boff[i][ks] = HALF + rb * 128 + ((c ^ ((rb >> 1) & 7)) << 4);
+    }
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+  s16x8 fa0[4], fb0[4], fa1[4], fb1[4];
+  auto rd = [&](const char* buf, int ks, s16x8 (&fa)[4], s16x8 (&fb)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fa[i] = *reinterpret_cast<const s16x8*>(buf + aoff[i][ks]);
+      fb[i] = *reinterpret_cast<const s16x8*>(buf + boff[i][ks]);
+    }
+  };
+  auto mm = [&](const s16x8 (&fa)[4], const s16x8 (&fb)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[i][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[n], acc[i][n], 0, 0, 0);
+  };
+
+#pragma unroll
+  for (int j = 0; j < 16; ++j) glds(j, 0, smem);
+  vmc<0>();
+  pbar();
+  rd(smem, 0, fa0, fb0);
+  if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
+  for (int t = 0; t < nk; ++t) {
+    const char* cur = smem + (t & 1) * BUF;
+    char* nxt = smem + ((t + 1) & 1) * BUF;
+    const int t1 = min(t + 1, nk - 1);  // past the last K-tile the DMA reloads tile nk-1 into the free buffer
+    // k-step 0: read 1, DMA 0-3, MFMA 0 ...
+    rd(cur, 1, fa1, fb1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) glds(j, t1, nxt);
+    mm(fa0, fb0);
+    rd(cur, 2, fa0, fb0);
+#pragma unroll
+    for (int j = 4; j < 8; ++j) glds(j, t1, nxt);
+    mm(fa1, fb1);
+    rd(cur, 3, fa1, fb1);
+#pragma unroll
+    for (int j = 8; j < 12; ++j) glds(j, t1, nxt);
+    mm(fa0, fb0);
+#pragma unroll
+    for (int j = 12; j < 16; ++j) glds(j, t1, nxt);
+    mm(fa1, fb1);
+    vmc<0>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    pbar();
+    rd(nxt, 0, fa0, fb0);
+  }
+  if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
+  // epilogue: C layout col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 h
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int col = n0 + wc * 128 + n * 32 + r32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wr * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < M && col < N) Y[(int64_t)row * ldy + col] = f2bf(acc[i][n][r]);
+      }
+    }
+}
+
+template <int VAR>
+static int launch_qq2(const void* A, int64_t lda, const void* B, int64_t ldb, const void* bias, void* Y, int64_t ldy,
+                      int M, int N, int K, int act, int glu, int gm, hipStream_t st) {
+  if (K % 64 || M <= 0 || N <= 0) return -1;
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  hipLaunchKernelGGL(qq2_gemm_kernel<VAR>, dim3(tiles), dim3(256), 0, st, (const bf16_t*)A, lda, (const bf16_t*)B,
+                     ldb, (const bf16_t*)bias, (bf16_t*)Y, ldy, M, N, K, act, glu, gm);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 template <int VAR>
 static int launch_qq(const void* A, int64_t lda, const void* B, int64_t ldb, const void* bias, void* Y, int64_t ldy,
                      int M, int N, int K, int act, int glu, int gm, hipStream_t st) {
@@ -452,6 +578,8 @@ extern "C" int pp_gemm(int var, const void* A, int64_t lda, const void* B, int64
     case 8: return launch<8>(A, lda, B, ldb, bias, Y, ldy, M, N, K, act, glu, gm, st);
     case 10: return launch<10>(A, lda, B, ldb, bias, Y, ldy, M, N, K, act, glu, gm, st);
     case 11: return launch<11>(A, lda, B, ldb, bias, Y, ldy, M, N, K, act, glu, gm, st);
+    case 200: return launch_qq2<0>(A, lda, B, ldb, bias, Y, ldy, M, N, K, act, glu, gm, st);
+    case 201: return launch_qq2<1>(A, lda, B, ldb, bias, Y, ldy, M, N, K, act, glu, gm, st);
     case 100: return launch_qq<0>(A, lda, B, ldb, bias, Y, ldy, M, N, K, act, glu, gm, st);
     case 101: return launch_qq<1>(A, lda, B, ldb, bias, Y, ldy, M, N, K, act, glu, gm, st);
     case 102: return launch_qq<2>(A, lda, B, ldb, bias, Y, ldy, M, N, K, act, glu, gm, st);

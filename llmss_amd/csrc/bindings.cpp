@@ -59,10 +59,6 @@ int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int n
                        int64_t ws_bytes);
 void attn_decode_set_unroll(int u);
 bool gemm_tuned_get(int M, int N, int K, bool glu, int kind, int* nt_hint, int* split);
-int gemm_packed_partial_slabs(int M, int N, int K, bool glu, int act, int nt_hint, int split_hint, int64_t ws_bytes);
-int launch_gemm_packed(const void* x, int64_t ldx, const void* w, int64_t k64, const void* bias, void* y, int64_t ldy,
-                       int M, int N, int K, int act, bool glu, void* workspace, int64_t ws_bytes, int nt_hint,
-                       int split_hint, bool partial_out, hipStream_t st);
 void launch_add_norm_partial(const void* part, int S, int64_t slab, const void* xbias, const void* res_in,
                              void* res_out, const void* w, const void* b, void* y, int64_t y_stride, int T, int H,
                              float eps, bool rms, hipStream_t st, void* q8, void* s8);
@@ -176,13 +172,6 @@ PYBIND11_MODULE(_C, m) {
     if (!gemm_tuned_get(M, N, K, glu, kind, &nt, &s)) return py::none();
     return py::make_tuple(nt, s);
   });
-  m.def("gemm_packed", [](uintptr_t x, int64_t ldx, uintptr_t w, int64_t k64, uintptr_t bias, uintptr_t y, int64_t ldy,
-                          int M, int N, int K, int act, bool glu, uintptr_t work, int64_t wbytes, int nt_hint,
-                          int split_hint, bool partial_out, uintptr_t st) {
-    return launch_gemm_packed(CP(x), ldx, CP(w), k64, CP(bias), P(y), ldy, M, N, K, act, glu, P(work), wbytes, nt_hint,
-                              split_hint, partial_out, S(st));
-  });
-  m.def("gemm_packed_partial_slabs", &gemm_packed_partial_slabs);
   m.def("add_norm_partial", [](uintptr_t part, int S, int64_t slab, uintptr_t xbias, uintptr_t ri, uintptr_t ro,
                                uintptr_t w, uintptr_t b, uintptr_t y, int64_t ys, int T, int H, float eps, bool rms,
                                uintptr_t st, uintptr_t q8, uintptr_t s8) {

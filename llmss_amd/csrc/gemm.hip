@@ -1353,7 +1353,7 @@ __global__ __launch_bounds__(256) void gemm_f8f8_kernel(const unsigned char* __r
 bool gemm_mid_dims(int tsel, int* bm, int* bn, int* threads);
 void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
-                     int split, hipStream_t st, bool packed = false, int* cnt = nullptr,
+                     int split, hipStream_t st, int* cnt = nullptr,
                      const QkvEpi* qe = nullptr, const float* xs = nullptr, const float* wsc = nullptr,
                      bool ilv = false);
 
@@ -1410,7 +1410,7 @@ int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq
   gemm_f8f8_kernel<BM_, BN_, NS_><<<grid, 256, 0, st>>>(A, ldx, XS, Bw, ldw, WSc, Bi, Y, ldy, part, M, N, K, act_k, glu_k)
   if (mid) {
     launch_gemm_mid(tile, depth, M <= bm, (const bf16_t*)xq, ldx, (const bf16_t*)wq, ldw, Bi, Y, ldy, part, M, N, K,
-                    act_k, glu_k, split, st, false, nullptr, nullptr, XS, WSc);
+                    act_k, glu_k, split, st, nullptr, nullptr, XS, WSc);
   } else if (tile == 1) {
     if (depth >= 3) LF(128, 128, 3); else LF(128, 128, 2);
   } else if (tile == 2) {
@@ -1541,7 +1541,7 @@ void gemm_stream_plan(int M, int N, int K, int* nt_out, int* splitk_out);
 namespace {
 std::mutex g_tuned_mu;
 std::unordered_map<uint64_t, std::pair<int, int>> g_tuned;
-// kind: 0 = bf16 [N, K] weights, 1 = fp8 weights, 2 = packed bf16 weights (launch_gemm_packed), 3 = QKV
+// kind: 0 = bf16 [N, K] weights, 1 = fp8 weights, 3 = QKV
 // RoPE / KV-write epilogue (launch_gemm_qkv)
 uint64_t tune_key(int M, int N, int K, bool glu, int kind) {
   return ((uint64_t)(kind & 7) << 61) | ((uint64_t)(M & 0x7FFFF) << 42) | ((uint64_t)N << 22) |
@@ -1799,7 +1799,7 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   dim3 grid(nt, s);
   if (tsel >= 7 && tsel <= 15) {  // gemm_mid tiles (7, 8-15)
     launch_gemm_mid(tsel, ns, wnt_ok(tsel_raw, M, tsel), X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, part, M, N, K,
-                    act_k, glu_k, s, st, false, cnt, qe, nullptr, nullptr, (tsel_raw & 512) != 0);
+                    act_k, glu_k, s, st, cnt, qe, nullptr, nullptr, (tsel_raw & 512) != 0);
     if (cnt) return 0;
     if (s > 1 && partial_out && !g && act == 0) return s;
     if (s > 1) {
@@ -1958,64 +1958,3 @@ void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk) {
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Packed bf16 weights ([N/16][ceil(K/64)][16][64], ops/hip.py pack_weight): every shape runs the
-// gemm_mid kernels (tiles 8-12), whose weight stages are then contiguous 2-KiB panel blocks.
-// Plan: tile by M (64x128 up to 64 rows, 128x128 up to 128, then 256x128 / 128x256), K split until
-// the grid holds ~200 workgroups (>= 4 k-steps per slice); tuned plans (kind 2) override.
-static void packed_plan(int M, int N, int K, bool glu, int nt_hint, int split_hint, int* tsel_out, int* ns_out,
-                        int* split_out) {
-  if (nt_hint == 0 && split_hint == 0) gemm_tuned_get(M, N, K, glu, 2, &nt_hint, &split_hint);
-  int tsel = (nt_hint >> 8) & 15;
-  static constexpr int kDepth[4] = {2, 3, 4, 6};
-  int ns = (nt_hint >> 8) ? kDepth[(nt_hint >> 12) & 3] : 4;
-  if (tsel < 8 || tsel > 12) tsel = M <= 64 ? 11 : (M <= 128 ? 8 : (N >= 4 * M ? 12 : 9));
-  int bm, bn;
-  tile_dims(tsel, &bm, &bn);
-  const int nt = tiles_of(M, N, bm, bn), nk = (K + 63) / 64;
-  int s = split_hint;
-  if (s <= 0) {
-    s = 1;
-    while (nt * s < 200 && s < 8 && nk / (2 * s) >= 4) s *= 2;
-  }
-  *tsel_out = tsel;
-  *ns_out = ns;
-  *split_out = std::max(1, std::min(s, nk));
-}
-
-int gemm_packed_partial_slabs(int M, int N, int K, bool glu, int act, int nt_hint, int split_hint, int64_t ws_bytes) {
-  if (M == 0 || N == 0 || glu || act != 0) return 0;
-  int tsel, ns, s;
-  packed_plan(M, N, K, glu, nt_hint, split_hint, &tsel, &ns, &s);
-  if ((int64_t)s * M * N * 4 > ws_bytes) s = 1;
-  return s > 1 ? s : 0;
-}
-
-int launch_gemm_packed(const void* x, int64_t ldx, const void* w, int64_t k64, const void* bias, void* y, int64_t ldy,
-                       int M, int N, int K, int act, bool glu, void* workspace, int64_t ws_bytes, int nt_hint,
-                       int split_hint, bool partial_out, hipStream_t st) {
-  if (M == 0 || N == 0) return 0;
-  if (K % 16) throw std::runtime_error("gemm_packed: K must be a multiple of 16");
-  if (glu && (N % 32)) throw std::runtime_error("gemm_packed: glu needs N % 32 == 0");
-  int tsel, ns, s;
-  packed_plan(M, N, K, glu, nt_hint, split_hint, &tsel, &ns, &s);
-  if ((int64_t)s * M * N * 4 > ws_bytes) s = 1;
-  const int g = glu ? 1 : 0;
-  const bool keep = s > 1 && partial_out && !g && act == 0;
-  if (!y && !keep) throw std::runtime_error("gemm_packed: this configuration writes the output, but no output buffer");
-  auto Y = (bf16_t*)y;
-  auto B = (const bf16_t*)bias;
-  float* part = s > 1 ? (float*)workspace : nullptr;
-  int bm, bn;
-  tile_dims(tsel, &bm, &bn);
-  launch_gemm_mid(tsel, ns, M <= bm, (const bf16_t*)x, ldx, (const bf16_t*)w, k64, B, Y, ldy, part, M, N, K,
-                  s > 1 ? 0 : act, s > 1 ? 0 : g, s, st, true);
-  if (keep) return s;
-  if (s > 1) {
-    const int nout = g ? N / 2 : N;
-    dim3 rgrid(std::min((nout + 255) / 256, 64), M);
-    splitk_reduce_kernel<<<rgrid, 256, 0, st>>>(part, s, M, N, B, Y, ldy, act, g);
-    HIP_CHECK_LAUNCH();
-  }
-  return 0;
-}

@@ -35,7 +35,7 @@
 // k-step's first-half reads plus the ring stage issue between the second k-half's MFMAs (one barrier per
 // k-step, moved to the middle of it; the stage issue moves half a k-step later). For M >= 128 tiles, where a
 // k-step carries 16-64 MFMAs per wave and the MFMA-only time is 60-80 % of the kernel (profiles/r4_gemm).
-template <int BM, int BN, int WM, int WN, int NS, bool WNT, bool PK, bool F8 = false, int MODE = 0, bool ILV = false>
+template <int BM, int BN, int WM, int WN, int NS, bool WNT, bool F8 = false, int MODE = 0, bool ILV = false>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                               const bf16_t* __restrict__ B, int64_t ldb,
                                                               const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
@@ -44,7 +44,6 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
                                                               const float* __restrict__ xs,
                                                               const float* __restrict__ wsc) {
   constexpr int ES = F8 ? 1 : 2;  // operand bytes per element
-  static_assert(!(F8 && PK), "fp8 weights are row-major");
   constexpr int NW = WM * WN;
   constexpr int MT = BM / WM / 16, NT = BN / WN / 16;  // 16x16 accumulator tiles per wave
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
@@ -67,12 +66,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
   const int t0 = zk * per, t1 = min(nk_all, t0 + per);
 
   // descriptors start at this tile's first row; everything past the matrix end reads as zero
-  // PK: weights packed [N/16][K64][16][64] (ldb = K64, the 64-wide k blocks per row): a k-step of a
-  // 16-row panel is one contiguous 2-KiB block, so a stage streams BN/16 such blocks instead of BN
-  // strided 128-B row pieces (+18 % HBM read rate, bench/stream_ceiling.hip)
   const uint64_t abytes = (uint64_t)(M - m0) * (uint64_t)lda * ES;
-  const uint64_t bbytes = PK ? (uint64_t)((N - n0) / 16) * (uint64_t)ldb * 2048 : (uint64_t)(N - n0) * (uint64_t)ldb * ES;
-  const int64_t boff = PK ? (int64_t)(n0 / 16) * ldb * 2048 : (int64_t)n0 * ldb * ES;  // bytes
+  const uint64_t bbytes = (uint64_t)(N - n0) * (uint64_t)ldb * ES;
+  const int64_t boff = (int64_t)n0 * ldb * ES;  // bytes
   const auto ra = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<char*>(reinterpret_cast<const char*>(A) + (int64_t)m0 * lda * ES), (short)0,
       (int)(abytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)abytes), 0x00020000);
@@ -89,8 +85,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
 #pragma unroll
   for (int i = 0; i < BL; ++i) {
     const int row = (i * NW + w) * 8 + (lane >> 3);
-    vb[i] = PK ? (uint32_t)((row >> 4) * ldb * 2048 + (row & 15) * 128 + (((lane & 7) ^ (row & 7)) << 4))
-               : (uint32_t)(row * ldb * ES + (((lane & 7) ^ (row & 7)) << 4));
+    vb[i] = (uint32_t)(row * ldb * ES + (((lane & 7) ^ (row & 7)) << 4));
   }
   // one ring stage (k-step T_) into LDS slot SA_: AL + BL wave-instructions of 1 KiB (8 rows x 128 B);
   // the k position is the scalar soffset, the per-lane voffsets never change
@@ -98,7 +93,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
   do {                                                                                                           \
     char* sA_ = (SA_);                                                                                           \
     if (MODE == 2) break;                                                                                        \
-    const int soff_ = (T_) * 128, sofb_ = (T_) * (PK ? 2048 : 128);                                             \
+    const int soff_ = (T_) * 128, sofb_ = soff_;                                                                  \
     if (!ktail || (T_) != nk_all - 1) {                                                                          \
       _Pragma("unroll") for (int i_ = 0; i_ < AL; ++i_)                                                           \
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)(sA_ + (i_ * NW + w) * 1024), 16, (uint32_t)va[i_], (uint32_t)soff_, 0, 0); \
@@ -185,7 +180,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
   if constexpr (ILV) {
-    static_assert(NS >= 3 && !F8 && !PK && MODE == 0, "interleaved ring: bf16 row-major weights, >= 3 stages");
+    static_assert(NS >= 3 && !F8 && MODE == 0, "interleaved ring: bf16 row-major weights, >= 3 stages");
     static_assert((NS - 3) * LOADS <= 63, "vmcnt immediate");
     constexpr int RPG = (MT + NT + MT - 1) / MT;  // fragment reads per group of NT MFMAs
     constexpr int LPG = (LOADS + MT - 1) / MT;    // ring loads per group
@@ -396,32 +391,30 @@ static int mid_depth(int bm, int bn, int want) {
 
 void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
-                     int split, hipStream_t st, bool packed, int* cnt, const QkvEpi* qe, const float* xs,
+                     int split, hipStream_t st, int* cnt, const QkvEpi* qe, const float* xs,
                      const float* wsc, bool ilv) {
   const bool f8 = xs != nullptr;
-  if (f8 && (packed || !wsc || K % 128)) throw std::runtime_error("gemm_mid fp8: row-major weights, K % 128 == 0");
+  if (f8 && (!wsc || K % 128)) throw std::runtime_error("gemm_mid fp8: per-row weight scales, K % 128 == 0");
   const QkvEpi qv = qe ? *qe : QkvEpi{};
   int bm, bn, wm, wn;
   if (!mid_layout(tsel, &bm, &bn, &wm, &wn)) throw std::runtime_error("gemm_mid: bad tile code");
   if (glu && (bn / wn / 16) % 2)
     throw std::runtime_error("gemm_mid: SwiGLU needs an even number of 16-column tiles per wave");
-  if ((uint64_t)bm * ldx * 2 >= (1ull << 31) || (uint64_t)bn * ldw * (packed ? 128 : 2) >= (1ull << 31))
+  if ((uint64_t)bm * ldx * 2 >= (1ull << 31) || (uint64_t)bn * ldw * 2 >= (1ull << 31))
     throw std::runtime_error("gemm_mid: row stride too large for 32-bit buffer offsets");
-  if (packed && (N % 16 || (int64_t)ldw * 64 < K || (int64_t)ldw * 64 >= K + 64))
-    throw std::runtime_error("gemm_mid: packed weights need N % 16 == 0 and ldw = ceil(K / 64)");
   const int ns = mid_depth(bm, bn, depth);
-  ilv = ilv && !f8 && !packed && ns >= 3 && K % 64 == 0;  // the interleaved ring's preconditions
+  ilv = ilv && !f8 && ns >= 3 && K % 64 == 0;  // the interleaved ring's preconditions
   const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   dim3 grid(tiles, split);
-#define MID1(BM_, BN_, WM_, WN_, NS_, WNT_, PK_)                                                                   \
-  gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, WNT_, PK_><<<grid, 64 * WM_ * WN_, 0, st>>>(X, ldx, W, ldw, bias, Y, ldy, \
+#define MID1(BM_, BN_, WM_, WN_, NS_, WNT_)                                                                        \
+  gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, WNT_><<<grid, 64 * WM_ * WN_, 0, st>>>(X, ldx, W, ldw, bias, Y, ldy, \
                                                                                       part, M, N, K, act, glu, cnt, qv, \
                                                                                       nullptr, nullptr)
 #define MID1F8(BM_, BN_, WM_, WN_, NS_, WNT_)                                                                      \
-  gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, WNT_, false, true><<<grid, 64 * WM_ * WN_, 0, st>>>(                    \
+  gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, WNT_, true><<<grid, 64 * WM_ * WN_, 0, st>>>(                    \
       X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, cnt, qv, xs, wsc)
 #define MID1I(BM_, BN_, WM_, WN_, NS_, WNT_)                                                                       \
-  gemm_mid_kernel<BM_, BN_, WM_, WN_, (NS_ < 3 ? 3 : NS_), WNT_, false, false, 0, true>                              \
+  gemm_mid_kernel<BM_, BN_, WM_, WN_, (NS_ < 3 ? 3 : NS_), WNT_, false, 0, true>                              \
       <<<grid, 64 * WM_ * WN_, 0, st>>>(X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, cnt, qv, nullptr,     \
                                         nullptr)
 #define MID(BM_, BN_, WM_, WN_, NS_)                                                                             \
@@ -430,10 +423,8 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
       if (wnt) MID1F8(BM_, BN_, WM_, WN_, NS_, true); else MID1F8(BM_, BN_, WM_, WN_, NS_, false);            \
     } else if (ilv && NS_ >= 3) {                                                                              \
       if (wnt) MID1I(BM_, BN_, WM_, WN_, NS_, true); else MID1I(BM_, BN_, WM_, WN_, NS_, false);              \
-    } else if (packed) {                                                                                       \
-      if (wnt) MID1(BM_, BN_, WM_, WN_, NS_, true, true); else MID1(BM_, BN_, WM_, WN_, NS_, false, true);     \
     } else {                                                                                                   \
-      if (wnt) MID1(BM_, BN_, WM_, WN_, NS_, true, false); else MID1(BM_, BN_, WM_, WN_, NS_, false, false);   \
+      if (wnt) MID1(BM_, BN_, WM_, WN_, NS_, true); else MID1(BM_, BN_, WM_, WN_, NS_, false);                 \
     }                                                                                                          \
   } while (0)
 #define MID_NS(BM_, BN_, WM_, WN_)                                               \

@@ -8,7 +8,7 @@ import torch
 
 from ..models.config import ModelConfig, get_preset
 from ..models.decoder import DecoderLM
-from ..models.weights import load_hf_weights, load_shard, pack_linears, random_weights, save_shard, shard_cache_path
+from ..models.weights import load_hf_weights, load_shard, random_weights, save_shard, shard_cache_path
 from ..parallel.dist import TPGroup
 from ..utils.checkpoint import CheckpointReader, weight_files
 from .engine import LLMEngine, Request, StepEvent
@@ -57,11 +57,6 @@ def build_model(model: str, tp: Optional[TPGroup] = None, dtype: str = "bf16", d
             w = load_hf_weights(cfg, CheckpointReader(files), tp.size, tp.rank, device=device, dtype=tdtype, fp8=fp8)
             if cpath:
                 save_shard(w, cpath)
-    # GEMM panel layout (models/weights.py pack_linears): opt-in. Measured on MI355X (profiles/r2_packed):
-    # Llama-2-7B TP=1 decode GEMMs 2-8 % faster, but prefill and GPT-2-XL's small shapes lose more
-    # than that on the gemm_mid-only path, so whole-run tokens/s drops 2-8 %
-    if device.type == "cuda" and os.environ.get("LLMSS_PACK_WEIGHTS", "0") == "1":
-        pack_linears(w)
     return DecoderLM(cfg, w, tp)
 
 

@@ -232,7 +232,7 @@ class DecoderLM:
 
     def _comm(self, device):
         if self._comm_stream is None:
-            self._comm_stream = torch.cuda.Stream(device=device, priority=-1)
+            self._comm_stream = torch.cuda.Stream(device=device, priority=int(os.environ.get("LLMSS_COMM_PRIO", "0")))
         return self._comm_stream
 
     def _reduce_rows(self, fn, *inputs) -> torch.Tensor:
@@ -270,7 +270,7 @@ class DecoderLM:
     def col_ok(self, lin) -> bool:
         """Can this row-parallel projection run column-chunked (_reduce_cols)?"""
         C = self.col_chunks
-        return (self.tp.comm_active and C > 1 and not lin.packed and not lin.glu and lin.N % (8 * C) == 0)
+        return (self.tp.comm_active and C > 1 and not lin.glu and lin.N % (8 * C) == 0)
 
     def _reduce_cols(self, lin, x, pre=None) -> torch.Tensor:
         """``all_reduce(lin(pre(x) if pre else x))`` as C column chunks (the "col" decode schedule): chunk c is the

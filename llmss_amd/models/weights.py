@@ -70,64 +70,38 @@ def shard_plan(cfg: ModelConfig, tp: int, rank: int) -> ShardPlan:
 
 @dataclass
 class Linear:
-    # [N, K] bf16 (or uint8 fp8-e4m3 when w_scale is set), or bf16 panels [N/16, ceil(K/64), 16, 64]
-    # (pack_linears: the layout the decode GEMM streams contiguously) with the logical K in `k`
+    # [N, K] bf16, or uint8 fp8-e4m3 when w_scale is set (per-row scales)
     w: torch.Tensor
     b: Optional[torch.Tensor] = None
     w_scale: Optional[torch.Tensor] = None
     glu: bool = False
-    k: int = 0
 
     def __call__(self, x, act="none", partial_ok=False):
         return ops.linear(x, self.w, self.b, act, self.glu, self.w_scale, partial_ok=partial_ok)
 
     @property
-    def packed(self) -> bool:
-        return self.w.dim() == 4
-
-    @property
     def N(self) -> int:
-        return self.w.shape[0] * 16 if self.packed else self.w.shape[0]
+        return self.w.shape[0]
 
     @property
     def K(self) -> int:
-        return self.k if self.packed else self.w.shape[1]
+        return self.w.shape[1]
 
     def rows(self, r0: int, r1: int) -> "Linear":
-        """Output features [r0, r1) of a row-major linear as a Linear over views (no copy): the weight slice a
-        column chunk of a row-parallel projection reads (DecoderLM._reduce_cols)."""
-        if self.packed or self.glu:
-            raise ValueError("row slices of packed / SwiGLU linears are not supported")
+        """Output features [r0, r1) as a Linear over views (no copy): the weight slice a column chunk of a
+        row-parallel projection reads (DecoderLM._reduce_cols)."""
+        if self.glu:
+            raise ValueError("row slices of SwiGLU linears are not supported")
         return Linear(self.w[r0:r1], None if self.b is None else self.b[r0:r1],
                       None if self.w_scale is None else self.w_scale[r0:r1], False)
 
     def dense(self) -> torch.Tensor:
-        """The [N, K] row-major weight (a copy when packed)."""
-        return ref.unpack_weight(self.w, self.k) if self.packed else self.w
+        """The [N, K] row-major weight."""
+        return self.w
 
     @property
     def out_features(self):
         return self.N // (2 if self.glu else 1)
-
-
-def pack_linears(mw: "ModelWeights") -> int:
-    """Re-lay every bf16 projection (and an untied LM head) of a GPU model as GEMM panels in place
-    (ref.pack_weight; no second copy stays in HBM). The mid-M GEMM then reads each k-step of a
-    16-row panel as one contiguous 2-KiB block instead of 16 strided 128-B row pieces. Returns the
-    number of weights packed."""
-    n = 0
-    lins = [lin for L in mw.layers for lin in (L.qkv, L.o, L.up, L.down)]
-    head = mw.head
-    if head.w.untyped_storage().data_ptr() != mw.wte.untyped_storage().data_ptr():
-        lins.append(head)  # a tied head is a view of the embedding table: stays row-major
-    for lin in lins:
-        if lin.packed or lin.w_scale is not None or not lin.w.is_cuda or lin.w.dtype != torch.bfloat16 \
-                or lin.w.shape[0] % 16:
-            continue
-        K = lin.w.shape[1]
-        lin.w, lin.k = ref.pack_weight(lin.w), K
-        n += 1
-    return n
 
 
 @dataclass

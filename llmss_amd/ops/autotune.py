@@ -38,20 +38,6 @@ class GemmShape:
     fp8: bool = False
     partial: bool = False  # consumer sums split-K slabs itself
     act: str = "none"
-    packed: bool = False  # panel-packed bf16 weights (gemm_mid kernels only)
-
-
-def packed_candidates(M: int, N: int, K: int, glu: bool) -> List[Tuple[int, int]]:
-    """(nt_hint, split) pairs for panel-packed weights: gemm_mid tiles x ring depth x split-K (odd
-    splits too: with one workgroup per CU a grid just over 256 workgroups runs a nearly empty second
-    wave, so the best split is the one whose grid lands just under a multiple of the CU count)."""
-    mids = [(11, 16), (11, 32), (10, 16), (10, 32)]
-    if M > 64:
-        mids += [(8, 16), (8, 32), (12, 16)]
-    if M >= 256:
-        mids += [(9, 16)]
-    nk = -(-K // 64)
-    return [((t | d) << 8, s) for t, d in mids for s in (1, 2, 3, 4, 5, 6, 8) if nk // s >= 2]
 
 
 def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, int]]:
@@ -157,8 +143,6 @@ def tune_shape(M: int, shape: GemmShape, device, weight_budget: int = 600 << 20,
         sc = torch.full((N,), 1e-2, device=device)
     else:
         base = (torch.randn(N, K, device=device, generator=g) * K ** -0.5).to(torch.bfloat16)
-        if shape.packed:
-            base = H.pack_weight(base)
         ws = [base.clone() for _ in range(ncopy)]
         sc = None
     nout = N // 2 if shape.glu else N
@@ -185,7 +169,7 @@ def tune_shape(M: int, shape: GemmShape, device, weight_budget: int = 600 << 20,
     default = cost(0, 0)
     best = (0, 0, default)
     if cands is None:
-        cands = packed_candidates(M, N, K, shape.glu) if shape.packed else candidates(M, N, K, shape.glu, shape.fp8)
+        cands = candidates(M, N, K, shape.glu, shape.fp8)
     for nt, s in cands:
         try:
             t = cost(nt, s)
@@ -203,7 +187,7 @@ def model_shapes(model) -> Dict[str, GemmShape]:
     fuse = model.tp.size == 1 and not model.cfg.parallel_block
     act = model.act if not L.up.glu else "none"
     def shp(lin, partial, act_="none"):
-        return GemmShape(lin.N, lin.K, lin.glu, lin.w_scale is not None, partial, act_, lin.packed)
+        return GemmShape(lin.N, lin.K, lin.glu, lin.w_scale is not None, partial, act_)
 
     out = {"qkv": shp(L.qkv, True), "o": shp(L.o, fuse), "up": shp(L.up, False, act), "down": shp(L.down, fuse)}
     out["head"] = shp(model.w.head, False)
@@ -246,7 +230,7 @@ def tune_qkv_epilogue(model, ms: Sequence[int], native=None, iters: int = 16) ->
 
     lib = native or _native()
     cfg, p, L = model.cfg, model.plan, model.w.layers[0]
-    if L.qkv.packed or L.qkv.w_scale is not None or getattr(model, "kv_fp8", False):
+    if L.qkv.w_scale is not None or getattr(model, "kv_fp8", False):
         return {}
     dev = model.device
     N, K, D = L.qkv.N, L.qkv.K, cfg.head_dim
@@ -336,7 +320,7 @@ def tune_model(model, ms: Sequence[int], native=None) -> Dict[Tuple[str, int], T
                 done[key] = tune_shape(M, shp, dev)
             nt, s, t, t0_us = done[key]
             if nt:
-                lib.gemm_tuned_set(M, shp.N, shp.K, shp.glu, 2 if shp.packed else int(shp.fp8), nt, s)
+                lib.gemm_tuned_set(M, shp.N, shp.K, shp.glu, int(shp.fp8), nt, s)
             res[(name, M)] = done[key]
     if os.environ.get("LLMSS_QKV_EPI", "1") != "0":
         key = ("qkv_epi", tuple(sorted(set(int(m) for m in ms))), model_shapes(model)["qkv"], str(dev),

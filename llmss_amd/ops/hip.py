@@ -493,45 +493,8 @@ def dequant_fp8_rows(q, scale, out=None):
     return w
 
 
-pack_weight = _ref.pack_weight
-unpack_weight = _ref.unpack_weight
-
-
-def linear_packed(x, wp, bias=None, act="none", glu=False, out=None, nt_hint=0, split_hint=0, partial_ok=False):
-    """Y = act(x . W^T + b) for a pack_weight() weight (always the gemm_mid kernels)."""
-    M, K = x.shape
-    _bf16_rows(x, "x")
-    _check(wp.dim() == 4 and wp.shape[2] == 16 and wp.shape[3] == 64 and wp.dtype == torch.bfloat16
-           and wp.is_contiguous() and wp.is_cuda, "packed weight [N/16, K64, 16, 64] bf16")
-    N, k64 = wp.shape[0] * 16, wp.shape[1]
-    _check(k64 * 64 >= K > k64 * 64 - 64 and K % 16 == 0, f"packed weight K blocks {k64} vs x K={K}")
-    if glu:
-        _check(N % 32 == 0, "glu needs N % 32 == 0")
-    if bias is not None:
-        _check(bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.numel() == N, "bias [N] bf16")
-    nout = N // 2 if glu else N
-    ws = _GEMM_WS.get(64 << 20, x.device)
-    partial_ok = partial_ok and not glu and act in ("none", None) and out is None
-    slabs = lib().gemm_packed_partial_slabs(M, N, K, bool(glu), _ACT[act], int(nt_hint), int(split_hint),
-                                            ws.numel() * 4) if partial_ok else 0
-    y = None if slabs else (out if out is not None else torch.empty(M, nout, dtype=x.dtype, device=x.device))
-    if y is not None:
-        _bf16_rows(y, "out", nout)
-    S = lib().gemm_packed(x.data_ptr(), x.stride(0), wp.data_ptr(), k64, _ptr(bias), _ptr(y),
-                          y.stride(0) if y is not None else nout, M, N, K, _ACT[act], bool(glu), ws.data_ptr(),
-                          ws.numel() * 4, int(nt_hint), int(split_hint), bool(y is None), _stream())
-    if y is None:
-        if S <= 1:
-            raise RuntimeError("internal: partial packed GEMM did not produce partial slabs")
-        return PartialSum(ws, S, M, N, bias, x.device)
-    return y
-
-
 def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hint=0, split_hint=0,
            partial_ok=False):
-    if w.dim() == 4:
-        _check(w_scale is None, "packed weights are bf16")
-        return linear_packed(x, w, bias, act, glu, out, nt_hint, split_hint, partial_ok)
     M, K = x.shape
     _bf16_rows(x, "x")
     fp8 = w_scale is not None

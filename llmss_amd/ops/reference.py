@@ -258,28 +258,8 @@ def dequant_fp8(w_q: torch.Tensor, w_scale: torch.Tensor, dtype=torch.float32) -
     return (w_q.view(torch.float8_e4m3fn).float() * w_scale.float()[:, None]).to(dtype)
 
 
-def pack_weight(w: torch.Tensor) -> torch.Tensor:
-    """[N, K] -> the GEMM panel layout [N/16, ceil(K/64), 16, 64] (K zero-padded): 16-row x 64-k blocks
-    of 2 KiB, contiguous in k-block order, which the mid-M GEMM streams (csrc/gemm_mid.hip, PK)."""
-    N, K = w.shape
-    if N % 16:
-        raise ValueError(f"pack_weight: N={N} must be a multiple of 16")
-    k64 = -(-K // 64)
-    if K % 64:
-        w = F.pad(w, (0, k64 * 64 - K))
-    return w.reshape(N // 16, 16, k64, 64).permute(0, 2, 1, 3).contiguous()
-
-
-def unpack_weight(wp: torch.Tensor, K: int) -> torch.Tensor:
-    """Inverse of pack_weight: the [N, K] row-major view (a copy)."""
-    n16, k64 = wp.shape[0], wp.shape[1]
-    return wp.permute(0, 2, 1, 3).reshape(n16 * 16, k64 * 64)[:, :K]
-
-
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act: str = "none", glu: bool = False,
            w_scale: Optional[torch.Tensor] = None) -> torch.Tensor:
-    if w.dim() == 4:  # packed panels
-        w = unpack_weight(w, x.shape[-1])
     wf = dequant_fp8(w, w_scale) if w_scale is not None else w.float()
     y = x.float() @ wf.t()
     if bias is not None:

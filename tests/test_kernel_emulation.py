@@ -112,32 +112,6 @@ def test_stream_gemm_emulation(M, N, K, MT, NT, KC, S):
     np.testing.assert_allclose(Y, X @ W.T, rtol=1e-9, atol=1e-9)
 
 
-@pytest.mark.parametrize("N,K", [(16, 64), (48, 100), (1536, 4096), (32, 1376)])
-def test_packed_weight_layout(N, K):
-    """pack_weight: 16-row x 64-k panels, contiguous in k-block order; element (n, k) sits at
-    ((n // 16) * K64 + k // 64) * 1024 + (n % 16) * 64 + k % 64; unpack inverts; the reference linear
-    accepts the packed form."""
-    import torch
-
-    from llmss_amd.ops import reference as R
-
-    g = torch.Generator().manual_seed(N + K)
-    w = torch.randn(N, K, generator=g)
-    wp = R.pack_weight(w)
-    k64 = -(-K // 64)
-    assert wp.shape == (N // 16, k64, 16, 64) and wp.is_contiguous()
-    flat = wp.reshape(-1)
-    for n, k in [(0, 0), (N - 1, K - 1), (N // 2, K // 3), (min(17, N - 1), min(65, K - 1))]:
-        assert flat[((n // 16) * k64 + k // 64) * 1024 + (n % 16) * 64 + k % 64] == w[n, k]
-    if K % 64:
-        assert wp[:, -1, :, K % 64:].abs().sum() == 0  # zero k padding
-    assert torch.equal(R.unpack_weight(wp, K), w)
-    x = torch.randn(5, K, generator=g)
-    assert torch.allclose(R.linear(x, wp), R.linear(x, w))
-    with pytest.raises(ValueError):
-        R.pack_weight(torch.zeros(24, 64))
-
-
 class _RingModel:
     """Program-order model of one wave of a ring schedule (all waves run the same program; a barrier means every
     wave has finished everything before it). Records which stage each LDS slot holds and checks the two ring

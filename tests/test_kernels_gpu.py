@@ -331,35 +331,6 @@ def test_gemm_splitk_combine_in_launch(tile, split, M, N, K):
     close(p, R.linear(x.float(), w.float(), None), 2e-2)
 
 
-@pytest.mark.parametrize("tile", [0, 8, 9, 10, 11, 12])
-@pytest.mark.parametrize("stages", [2, 4, 6])
-@pytest.mark.parametrize("split", [0, 1, 3])
-@pytest.mark.parametrize("M,N,K", [(64, 1536, 4096), (200, 4800, 1600), (37, 256, 64 * 5 + 16), (130, 384, 208)])
-def test_gemm_packed_weights(tile, stages, split, M, N, K):
-    """Panel-packed weights ([N/16][K64][16][64], K zero-padded) through the gemm_mid kernels."""
-    torch.manual_seed(0)
-    x, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
-    b = rnd(N, scale=0.1)
-    wp = H.pack_weight(w)
-    assert torch.equal(H.unpack_weight(wp, K), w)
-    hint = (tile | ({2: 0, 3: 16, 4: 32, 6: 48}[stages])) << 8 if tile else 0
-    ref = R.linear(x.float(), w.float(), b.float(), act="gelu_tanh")
-    y = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=x.device)
-    close(H.linear(x, wp, b, act="gelu_tanh", nt_hint=hint, split_hint=split, out=y), ref, 2e-2)
-    y = torch.full((M, N // 2), float("nan"), dtype=torch.bfloat16, device=x.device)
-    close(H.linear(x, wp, None, glu=True, nt_hint=hint, split_hint=split, out=y),
-          R.linear(x.float(), w.float(), None, glu=True), 2e-2)
-    # split-K partials left to the consumer (add_norm sums them)
-    p = H.linear(x, wp, None, nt_hint=hint, split_hint=split, partial_ok=True)
-    if isinstance(p, H.PartialSum):
-        res = torch.zeros(M, N, dtype=torch.bfloat16, device=x.device)
-        ones = torch.ones(N, dtype=torch.bfloat16, device=x.device)
-        _, r = H.add_norm_partial(p, ones, None, 1e-5, True, res)
-        close(r, R.linear(x.float(), w.float(), None), 2e-2)
-    else:
-        close(p, R.linear(x.float(), w.float(), None), 2e-2)
-
-
 @pytest.mark.parametrize("tile", [8, 11, 12])
 def test_gemm_mid_k_tail_reads_nothing_past_the_operands(tile):
     """Operands as views at the front of NaN-filled buffers: the partial last k-step of the last rows
