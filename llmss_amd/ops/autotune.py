@@ -197,8 +197,8 @@ def model_shapes(model) -> Dict[str, GemmShape]:
     if (not model.cfg.parallel_block and (col_mode == "force" or (col_mode == "auto" and model.tp.is_real))
             and model.col_ok(L.o) and model.col_ok(L.down)):
         C = model.col_chunks
-        out["o_col"] = GemmShape(L.o.N // C, L.o.K, False, L.o.w_scale is not None, False, "none", False)
-        out["down_col"] = GemmShape(L.down.N // C, L.down.K, False, L.down.w_scale is not None, False, "none", False)
+        out["o_col"] = GemmShape(L.o.N // C, L.o.K, False, L.o.w_scale is not None, False, "none")
+        out["down_col"] = GemmShape(L.down.N // C, L.down.K, False, L.down.w_scale is not None, False, "none")
     return out
 
 

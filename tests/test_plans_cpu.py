@@ -61,3 +61,27 @@ def test_interleaved_ring_candidates_only_where_the_kernel_takes_them():
     assert not ilv(A.candidates(512, 4096, 1376, False, False))  # partial last k-step
 
 
+
+
+@pytest.mark.parametrize("col", ["4", "0"])
+def test_model_shapes_include_the_column_chunks_when_forced(monkeypatch, col):
+    """The autotuner tunes o / down's column slices (DecoderLM._reduce_cols) whenever the column schedule can run."""
+    import torch
+
+    from llmss_amd.models.config import get_preset
+    from llmss_amd.models.decoder import DecoderLM
+    from llmss_amd.models.weights import random_weights
+    from llmss_amd.parallel.dist import TPGroup
+
+    monkeypatch.setenv("LLMSS_TP_COL", col)
+    cfg = get_preset("llama2-7b", num_layers=1, hidden_size=256, intermediate_size=512, num_heads=4, head_dim=64,
+                     num_kv_heads=4, rotary_dim=64, vocab_size=512, max_position_embeddings=64)
+    tp = TPGroup(0, 2, fake=True, sim_comm=(15.0, 150.0))
+    m = DecoderLM(cfg, random_weights(cfg, tp=2, rank=0, dtype=torch.float32, seed=0), tp)
+    shapes = A.model_shapes(m)
+    L = m.w.layers[0]
+    if col == "0":
+        assert "o_col" not in shapes and "down_col" not in shapes
+    else:
+        assert shapes["o_col"] == A.GemmShape(L.o.N // 4, L.o.K)
+        assert shapes["down_col"] == A.GemmShape(L.down.N // 4, L.down.K)
