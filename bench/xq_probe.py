@@ -92,34 +92,7 @@ def main():
                 pend[j] = ev
         cur.wait_stream(side)
 
-    ds = None
-
-    def tbo_devsync():  # the same pattern with device-flag hand-offs (ops.hip.DevSync) instead of graph edges
-        nonlocal ds
-        import sys, os
-        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        from llmss_amd.ops import hip as H
-        if ds is None:
-            ds = H.DevSync(torch.device("cuda"))
-        cur = torch.cuda.current_stream()
-        ds.begin()
-        side.wait_stream(cur)
-        pend = [None, None]
-        for i in range(a.n):
-            for j in (0, 1):
-                if pend[j] is not None:
-                    ds.wait(pend[j])
-                K()
-                tok = ds.signal()
-                with torch.cuda.stream(side):
-                    ds.wait(tok)
-                    C()
-                    pend[j] = ds.signal()
-        for p in pend:
-            ds.wait(p)
-        cur.wait_stream(side)
-
-    arms = {"tbo_devsync": tbo_devsync, "tbo": lambda: tbo(True), "tbo_wait_after_fork": lambda: tbo(False), "serial": serial, "fork_join": lambda: fork_join(0), "fork_join_lag1": lambda: fork_join(1),
+    arms = {"tbo": lambda: tbo(True), "tbo_wait_after_fork": lambda: tbo(False), "serial": serial, "fork_join": lambda: fork_join(0), "fork_join_lag1": lambda: fork_join(1),
             "fork_only": fork_only, "join_done": join_done}
     out = {"kernel_us": a.us, "side_us": a.side_us, "n": a.n}
     if a.arms:
@@ -148,8 +121,6 @@ def main():
             out[f"{name}_{mode}_us"] = round(best, 1)
             nk = 2 * a.n
             out[f"{name}_{mode}_extra_per_kernel_us"] = round((best - nk * a.us) / nk, 2)
-    if ds is not None:
-        out["devsync_error"] = ds.error()
     print(json.dumps(out), flush=True)
 
 

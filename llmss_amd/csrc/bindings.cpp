@@ -58,9 +58,7 @@ int gemm_f8f8_partial_slabs(int M, int N, int K, bool glu, int act, int tile, in
 int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int nt_hint, int split_hint,
                        int64_t ws_bytes);
 void attn_decode_set_unroll(int u);
-void launch_epoch_bump(void* epoch, hipStream_t st);
-void launch_flag_signal(void* flags, int idx, const void* epoch, hipStream_t st);
-void launch_flag_wait(const void* flags, int idx, const void* epoch, void* err, hipStream_t st);
+
 bool gemm_tuned_get(int M, int N, int K, bool glu, int kind, int* nt_hint, int* split);
 void launch_add_norm_partial(const void* part, int S, int64_t slab, const void* xbias, const void* res_in,
                              void* res_out, const void* w, const void* b, void* y, int64_t y_stride, int T, int H,
@@ -81,13 +79,6 @@ void register_ctrl(py::module_& m);     // shared-memory control ring (ctrl.cpp)
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "llmss_amd gfx950 HIP kernels + native runtime";
-  m.def("epoch_bump", [](uintptr_t epoch, uintptr_t st) { launch_epoch_bump(P(epoch), S(st)); });
-  m.def("flag_signal", [](uintptr_t flags, int idx, uintptr_t epoch, uintptr_t st) {
-    launch_flag_signal(P(flags), idx, CP(epoch), S(st));
-  });
-  m.def("flag_wait", [](uintptr_t flags, int idx, uintptr_t epoch, uintptr_t err, uintptr_t st) {
-    launch_flag_wait(CP(flags), idx, CP(epoch), P(err), S(st));
-  });
   m.def("add_norm", [](uintptr_t x, int64_t xs, uintptr_t ri, uintptr_t ro, uintptr_t w, uintptr_t b, uintptr_t y,
                        int64_t ys, int T, int H, float eps, bool rms, uintptr_t st, uintptr_t q8, uintptr_t s8, int xcw) {
     launch_add_norm(CP(x), xs, CP(ri), P(ro), CP(w), CP(b), P(y), ys, T, H, eps, rms, S(st), P(q8), P(s8), xcw);

@@ -126,11 +126,6 @@ class DecoderLM:
         self.col: set = set()
         self._cu_decode = {}
         self._comm_stream = None
-        # overlapped schedules hand off between the compute and comm streams through device flags (ops.hip.DevSync,
-        # csrc/sync.hip) instead of cross-stream events: each such graph edge stalls its source queue ~9 us
-        # (bench/xq_probe.py, profiles/r5_tbo). LLMSS_TP_DEVSYNC=0 = events
-        self.devsync = os.environ.get("LLMSS_TP_DEVSYNC", "1") != "0"
-        self._dsync = None
 
     @property
     def device(self):
@@ -241,15 +236,6 @@ class DecoderLM:
             # comm kernel beside them, ~3x on each overlapped kernel (profiles/r5_tp8sim: TBO 20.9 K vs 60.0 K tok/s)
             self._comm_stream = torch.cuda.Stream(device=device, priority=int(os.environ.get("LLMSS_COMM_PRIO", "0")))
         return self._comm_stream
-
-    def _devsync(self, device):
-        if self._dsync is None:
-            self._dsync = _hip_ops().DevSync(device)
-        return self._dsync
-
-    def sync_error(self) -> bool:
-        """Did a device-flag hand-off time out (a schedule bug; the step computed on stale data)?"""
-        return self._dsync is not None and self._dsync.error()
 
     def _reduce_rows(self, fn, *inputs) -> torch.Tensor:
         """``all_reduce(fn(*inputs))`` for a row-parallel projection (or a whole MLP).
@@ -374,21 +360,11 @@ class DecoderLM:
         on_gpu = inp.input_ids.is_cuda
         cur = torch.cuda.current_stream() if on_gpu else None
         comm = self._comm(inp.input_ids.device) if on_gpu else None
-        ds = self._devsync(inp.input_ids.device) if on_gpu and self.devsync else None
-        if ds is not None:
-            ds.begin()
-            comm.wait_stream(cur)  # the one fork per forward; every later hand-off goes through device flags
 
-        def reduce(t):  # all-reduce t on the comm stream; returns the token (flag or event) to wait on before reading t
+        def reduce(t):  # all-reduce t on the comm stream; returns the event to wait on before reading t
             if not on_gpu:
                 self.tp.all_reduce(t)
                 return None
-            if ds is not None:
-                tok = ds.signal()  # compute -> comm: t is complete
-                with torch.cuda.stream(comm):
-                    ds.wait(tok)
-                    self.tp.all_reduce(t)
-                    return ds.signal()  # comm -> compute: the sum is in t
             comm.wait_stream(cur)
             with torch.cuda.stream(comm):
                 self.tp.all_reduce(t)
@@ -399,11 +375,7 @@ class DecoderLM:
             return ev
 
         def ready(ev):
-            if ev is None:
-                return
-            if ds is not None:
-                ds.wait(ev)
-            else:
+            if ev is not None:
                 cur.wait_event(ev)
 
         x = ops.embed(inp.input_ids, w.wte, inp.positions if w.wpe is not None else None, w.wpe)
@@ -436,8 +408,6 @@ class DecoderLM:
         for j, (r0, r1) in enumerate(rows):
             ready(pend[j])
             ops.add_norm(delta[j], w.lnf_w, w.lnf_b, eps, rms, res[j], out=out[r0:r1])
-        if ds is not None:
-            cur.wait_stream(comm)  # the one join per forward (a captured side stream must rejoin)
         return out
 
     def rsag_ok(self, M: int) -> bool:

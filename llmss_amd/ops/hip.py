@@ -73,44 +73,6 @@ def _fp8_twin(y):
     return q, s
 
 
-class DevSync:
-    """Stream hand-off through device flags instead of cross-stream events (csrc/sync.hip): inside a HIP graph an
-    edge from a kernel on one queue to another queue stalls the source queue ~9 us (bench/xq_probe.py).
-
-    Per forward: ``begin()`` on the compute stream before the side stream forks from it, then pairs of
-    ``signal()`` (on the producing stream; returns a token) and ``wait(token)`` (on the consuming stream). Token
-    indices restart at 0 every forward, so a captured graph replays the same indices; the epoch bumped by
-    ``begin()`` tells this forward's flags from the last one's."""
-
-    CAP = 8192
-
-    def __init__(self, device):
-        self.buf = torch.zeros(self.CAP + 64, dtype=torch.int32, device=device)
-        self.flags = self.buf[: self.CAP]
-        self.epoch = self.buf[self.CAP:self.CAP + 1]
-        self.err = self.buf[self.CAP + 32:self.CAP + 33]
-        self.n = 0
-
-    def begin(self):
-        self.n = 0
-        lib().epoch_bump(self.epoch.data_ptr(), _stream())
-
-    def signal(self) -> int:
-        if self.n >= self.CAP:
-            raise RuntimeError(f"DevSync: more than {self.CAP} hand-offs in one forward")
-        i = self.n
-        self.n += 1
-        lib().flag_signal(self.flags.data_ptr(), i, self.epoch.data_ptr(), _stream())
-        return i
-
-    def wait(self, token: int):
-        lib().flag_wait(self.flags.data_ptr(), int(token), self.epoch.data_ptr(), self.err.data_ptr(), _stream())
-
-    def error(self) -> bool:
-        """A flag_wait timed out (schedule bug): the forward that hit it computed on stale data."""
-        return bool(self.err.item())
-
-
 def add_norm(x, weight, bias, eps, rms, residual=None, out=None, residual_out=None, fp8_out=False):
     """``fp8_out``: also write the per-token fp8-e4m3 twin of the output (== quant_fp8_rows of it) for the W8A8
     GEMM that consumes it next, which then skips its own quantisation launch."""
