@@ -379,8 +379,7 @@ class LLMEngine:
         L = m.w.layers[0]
         if self.cfg.parallel_block or not (m.col_ok(L.o) and m.col_ok(L.down)):
             return []
-        lo = int(os.environ.get("LLMSS_TP_COL_MIN", "1"))
-        return [b for b in self.buckets if b >= lo]
+        return [b for b in self.buckets if b >= m.col_min]
 
     def _tbo_half(self, b: int) -> int:
         if b not in getattr(self, "_tbo_cands", ()):

@@ -123,6 +123,9 @@ class DecoderLM:
         col = os.environ.get("LLMSS_TP_COL", "auto")
         self.col_mode = "auto" if col == "auto" else ("force" if int(col) > 1 else "0")
         self.col_chunks = int(col) if col not in ("auto", "0", "1") else 4
+        # smallest decode bucket the capture-time A/B tries it on (the collectives are small below; and under the
+        # TP=8 comm model it lost at every size, profiles/r5_tp8sim)
+        self.col_min = int(os.environ.get("LLMSS_TP_COL_MIN", "256"))
         self.col: set = set()
         self._cu_decode = {}
         self._comm_stream = None

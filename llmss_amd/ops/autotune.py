@@ -315,6 +315,8 @@ def tune_model(model, ms: Sequence[int], native=None) -> Dict[Tuple[str, int], T
     done = _DONE
     for name, shp in model_shapes(model).items():
         for M in sorted(set(int(m) for m in ms)):
+            if name.endswith("_col") and getattr(model, "col_mode", "0") != "force" and M < model.col_min:
+                continue  # column chunks run only in the buckets the capture-time A/B tries them on
             key = (M, shp, str(dev))
             if key not in done:
                 done[key] = tune_shape(M, shp, dev)
