@@ -237,7 +237,7 @@ class DecoderLM:
         if self._comm_stream is None:
             # normal priority: a higher-priority queue makes the hardware preempt the compute queue's waves for every
             # comm kernel beside them, ~3x on each overlapped kernel (profiles/r5_tp8sim: TBO 20.9 K vs 60.0 K tok/s)
-            self._comm_stream = torch.cuda.Stream(device=device, priority=int(os.environ.get("LLMSS_COMM_PRIO", "0")))
+            self._comm_stream = torch.cuda.Stream(device=device)
         return self._comm_stream
 
     def _reduce_rows(self, fn, *inputs) -> torch.Tensor:

@@ -27,7 +27,7 @@ from ..utils.logging import get_logger
 log = get_logger(__name__)
 
 _SLAB_READ_BPS = 4.0e12  # consumer-side fp32 partial reads (add_norm / rope), bytes/s
-ILV_MIN_M = int(os.environ.get("LLMSS_MID_ILV_MIN_M", "128"))  # smallest M whose plans include the interleaved ring
+ILV_MIN_M = 128  # smallest M whose plans include the interleaved ring (profiles/r4_gemm/sweep512_ilv.log)
 
 
 @dataclass(frozen=True)
@@ -87,8 +87,8 @@ def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, 
     # (64 x 256 tiles of a 12288-column QKV: 48 tiles x 5 = 240 workgroups)
     nk = -(-K // 64)
     out += [((t | d) << 8, s) for t, d in mids for s in (1, 2, 3, 4, 5, 6, 8, 11, 12) if s == 1 or nk // s >= 2]
-    # interleaved ring (hint bit 512, csrc/gemm_mid.hip ILV): >= 3 stages; LLMSS_MID_ILV=0 leaves it out
-    if M >= ILV_MIN_M and K % 64 == 0 and os.environ.get("LLMSS_MID_ILV", "1") != "0":
+    # interleaved ring (hint bit 512, csrc/gemm_mid.hip ILV): >= 3 stages
+    if M >= ILV_MIN_M and K % 64 == 0:
         out += [((t | d | 512) << 8, s) for t, d in mids if d >= 16 for s in (1, 2, 3, 4, 5, 6, 8)
                 if s == 1 or nk // s >= 3]
     # split-K combined inside the launch (hint bit 256, csrc/common.h splitk_combine): finished bf16
