@@ -18,7 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 SHAPES = {"qkv": (12288, 4096), "o": (4096, 4096), "gate_up": (22016, 4096), "down": (4096, 11008),
-          "cube": (8192, 8192), "gpt2_qkv": (4800, 1600), "gpt2_down": (1600, 6400)}
+          "cube": (8192, 8192), "gpt2_qkv": (4800, 1600), "gpt2_down": (1600, 6400),
+          "tp8_qkv": (1536, 4096), "tp8_o": (4096, 512), "tp8_up": (2752, 4096), "tp8_down": (4096, 1376)}
 
 
 def main():

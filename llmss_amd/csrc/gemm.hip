@@ -889,7 +889,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(const void* __restrict
 // Measured vs the previous 2-barrier kernel at M = 8192 (Llama-2-7B shapes, random data, one process):
 // +4-13 %; the no-stagger control equals the old kernel. Ablations (profiles/r5_gemm_pp/README.md): the
 // LDS-DMA + fragment-read traffic through the LDS costs ~25 % each on top of the MFMA/barrier skeleton.
-// Requires K % 64 == 0; rows beyond M / N are clamped on load and masked on store.
+// K % 8 == 0: a partial last K-tile reads zeros (zpage) for the chunks past K; rows beyond M / N are clamped on load
+// and masked on store.
 // -------------------------------------------------------------------------------------------
 __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
@@ -901,7 +902,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const bf16_t* __restric
                                                          const bf16_t* __restrict__ B, int64_t ldb,
                                                          const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
                                                          int64_t ldy, int M, int N, int K, int act, int glu,
-                                                         int group_m) {
+                                                         int group_m, const char* __restrict__ zpage) {
   constexpr int SLOT = 16384, BUF = 4 * SLOT;
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
   const int lane = threadIdx.x & 63;
@@ -914,19 +915,21 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const bf16_t* __restric
   const int grp = tile / (GM * ntn), gidx = tile - grp * (GM * ntn);
   const int gm = min(GM, ntm - grp * GM);
   const int m0 = (grp * GM + gidx % gm) * 256, n0 = (gidx / gm) * 256;
-  const int nk = K / 64;
+  const int nk = (K + 63) / 64;
+  const bool ktail = (K & 63) != 0;  // Llama-2-7B's TP=8 down projection: K = 1376
 
   // staging: slot h, instruction i (0, 1) = 8 local rows x 128 B, local row lr = (8 i + w) * 8 + lane / 8;
   // LDS chunk lane & 7 holds global chunk (lane & 7) ^ (lr & 7)
   const char* src[4] = {(const char*)A, (const char*)B, (const char*)B, (const char*)A};
   int64_t soff[4][2];
-  int lofs[2];
+  int lofs[2], kcol[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int inst = i * 8 + w;
     const int lr = inst * 8 + (lane >> 3);
     const int gc = (lane & 7) ^ (lr & 7);
     lofs[i] = inst * 1024;
+    kcol[i] = gc * 8;
     const int ar0 = min(m0 + (lr >> 6) * 128 + (lr & 63), M - 1);
     const int ar1 = min(m0 + (lr >> 6) * 128 + 64 + (lr & 63), M - 1);
     const int bc0 = min(n0 + (lr >> 5) * 64 + (lr & 31), N - 1);
@@ -937,10 +940,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const bf16_t* __restric
     soff[2][i] = (int64_t)bc1 * ldb * 2 + gc * 16;
   }
   auto stage = [&](int t, int h, char* buf) {
+    const bool last = ktail && t == nk - 1;  // wave-uniform
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(src[h] + soff[h][i] + (int64_t)t * 128),
-                                       (LDS_AS void*)(buf + h * SLOT + lofs[i]), 16, 0, 0);
+    for (int i = 0; i < 2; ++i) {
+      const char* p = src[h] + soff[h][i] + (int64_t)t * 128;
+      if (last) p = t * 64 + kcol[i] >= K ? zpage : p;  // chunks past K (of A and B) land as zeros
+      __builtin_amdgcn_global_load_lds((const void*)p, (LDS_AS void*)(buf + h * SLOT + lofs[i]), 16, 0, 0);
+    }
   };
   // fragment offsets inside a slot: A rows wr*64 + mt*16 + li, B rows wc*32 + nt*16 + li; k-half s -> chunk 4s+g
   // (the conflict-free ds_read_b128 image of gemm_big)
@@ -1647,10 +1653,9 @@ void gemm_tiled_plan(int M, int N, int K, int* tsel_io, int* split_io, bool glu)
     return;
   }
   if (tsel == 0) {
-    if (K % 64 == 0 && tiles_of(M, N, 256, 256) >= 192) tsel = 4;
+    if (tiles_of(M, N, 256, 256) >= 192) tsel = 4;
     else tsel = M <= 64 ? (tiles_of(M, N, 64, 64) > 256 ? 2 : 3) : 1;
   }
-  if (tsel == 4 && K % 64) tsel = 1;
   int hint_bits = tsel & ~15;
   tsel &= 15;
   if (tsel >= 5) hint_bits &= ~128;  // no stream-K variant of the 8-wave tiles
@@ -1718,7 +1723,28 @@ static int* sk_counters(int n) {
   return p + (size_t)g_ws_slot * cap;
 }
 
-void gemm_reserve_streamk(int n) { sk_counters(n); }
+// 4 KiB of zeros per device: the source of the chunks past K in gemm_pp's partial last K-tile
+static const char* g_zero_page[64] = {};
+static const char* zero_page() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) throw std::runtime_error("gemm zero page: bad device");
+  std::lock_guard<std::mutex> lk(g_sk_mu);
+  if (g_zero_page[dev]) return g_zero_page[dev];
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(nullptr, &cs);
+  if (cs != hipStreamCaptureStatusNone) throw std::runtime_error("gemm zero page must be allocated before capture");
+  char* p = nullptr;
+  if (hipMalloc(&p, 4096) != hipSuccess) throw std::runtime_error("gemm zero page: hipMalloc");
+  if (hipMemset(p, 0, 4096) != hipSuccess) throw std::runtime_error("gemm zero page: memset");
+  (void)hipDeviceSynchronize();
+  g_zero_page[dev] = p;
+  return p;
+}
+
+void gemm_reserve_streamk(int n) {
+  sk_counters(n);
+  (void)zero_page();
+}
 
 static bool launch_streamk(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, const bf16_t* B, bf16_t* Y,
                            int64_t ldy, int M, int N, int K, int act, int g, int tsel, int ns, int per_cu,
@@ -1775,7 +1801,7 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   if (f8 && tsel == 4) tsel = 1;
   if (tsel == 4) {
     gemm_pp_kernel<<<tiles_of(M, N, 256, 256), 512, 0, st>>>(X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, M, N, K, act, g,
-                                                             g_big_group_m);
+                                                             g_big_group_m, (K & 63) ? zero_page() : nullptr);
     HIP_CHECK_LAUNCH();
     return 0;
   }

@@ -253,11 +253,14 @@ def test_gemm_mid_interleaved_ring(tile, depth, split, M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(700, 1312, 64), (513, 768, 128), (300, 512, 192), (1024, 1536, 4096),
-                                   (2100, 800, 1600), (257, 288, 256), (600, 544, 320), (1500, 2080, 704)])
+                                   (2100, 800, 1600), (257, 288, 256), (600, 544, 320), (1500, 2080, 704),
+                                   (600, 1024, 1376), (300, 512, 80), (513, 768, 144), (257, 288, 48)])
 def test_gemm_big_edges(M, N, K):
     """The 256x256 ping-pong prefill kernel (gemm.hip gemm_pp_kernel) against the fp32 oracle at K-tile counts
     1-5 and 11 (prologue / last-tile vmcnt edges of its 4-phase, 2-buffer schedule, and the slot reuse of the
-    steady state), ragged M / N, bias + activation and SwiGLU through the swizzled LDS epilogue."""
+    steady state), partial last K-tiles (K % 64 = 16-48: Llama-2-7B's TP=8 down projection has K = 1376; the
+    chunks past K read a zero page), ragged M / N, bias + activation and SwiGLU through the swizzled LDS
+    epilogue."""
     torch.manual_seed(0)
     x, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
     b = rnd(N, scale=0.1)
