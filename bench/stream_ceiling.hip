@@ -116,6 +116,59 @@ __global__ __launch_bounds__(64 * NW) void tile_kernel(const char* __restrict__ 
   if (acc == 0x12345678u) out[blockIdx.x] = acc;
 }
 
+// row-major weight tile with RB bytes of every row per ring slot (RB = 128: gemm_mid's k-step; RB = 256: a 128-element
+// bf16 k-step, each wave-instruction 64 * 16 / RB rows x RB contiguous bytes), plus the 64-row activation tile
+template <int NS, int BN, int NW, int RB>
+__global__ __launch_bounds__(64 * NW) void tile_rb_kernel(const char* __restrict__ src, const char* __restrict__ act,
+                                                          int K, int ksplit, unsigned* out) {
+  constexpr int BBYTES = BN * RB, ABYTES = 64 * RB, SLOT = BBYTES + ABYTES;
+  constexpr int RPI = 1024 / RB;  // rows per wave-instruction
+  constexpr int L = BN / (RPI * NW), LA = 64 / (RPI * NW);
+  static_assert(L >= 1 && LA >= 1, "tile rows must cover the waves");
+  __shared__ __attribute__((aligned(16))) char ring[NS * SLOT];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int rt = blockIdx.x / ksplit, kz = blockIdx.x % ksplit;
+  const size_t rowb = (size_t)K * 2;
+  const int steps = (int)(rowb / RB) / ksplit;
+  const char* base = src + (size_t)rt * BN * rowb + (size_t)kz * steps * RB;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, (int)(BN * rowb), 0x00020000);
+  const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(act + (size_t)kz * steps * RB), (short)0,
+                                                    (int)(64 * rowb), 0x00020000);
+  uint32_t voff[L], aoff[LA];
+#pragma unroll
+  for (int i = 0; i < L; ++i)
+    voff[i] = (uint32_t)(((i * NW + w) * RPI + lane / (RB / 16)) * rowb + (lane % (RB / 16)) * 16);
+#pragma unroll
+  for (int i = 0; i < LA; ++i)
+    aoff[i] = (uint32_t)(((i * NW + w) * RPI + lane / (RB / 16)) * rowb + (lane % (RB / 16)) * 16);
+#define RISSUE(T_)                                                                                           \
+  do {                                                                                                       \
+    char* d_ = ring + ((T_) % NS) * SLOT;                                                                    \
+    _Pragma("unroll") for (int i_ = 0; i_ < LA; ++i_)                                                        \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)(d_ + BBYTES + (i_ * NW + w) * 1024), 16,   \
+                                               (uint32_t)aoff[i_], (uint32_t)((T_) * RB), 0, 0);            \
+    _Pragma("unroll") for (int i_ = 0; i_ < L; ++i_)                                                         \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(d_ + (i_ * NW + w) * 1024), 16, (uint32_t)voff[i_], \
+                                               (uint32_t)((T_) * RB), 0, 2);                                 \
+  } while (0)
+  constexpr int LT = L + LA;
+  for (int j = 0; j < NS - 1 && j < steps; ++j) RISSUE(j);
+  unsigned acc = 0;
+  for (int t = 0; t < steps; ++t) {
+    const int younger = min(steps - 1 - t, NS - 2);
+    if (NS >= 4 && younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LT) : "memory");
+    else if (NS >= 3 && younger >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LT) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + NS - 1 < steps) RISSUE(t + NS - 1);
+    acc += *reinterpret_cast<const unsigned*>(ring + (t % NS) * SLOT + threadIdx.x * 4);
+  }
+#undef RISSUE
+  if (acc == 0x12345678u) out[blockIdx.x] = acc;
+}
+
 template <int U, int NW>
 __global__ __launch_bounds__(64 * NW) void vgpr_kernel(const char* __restrict__ src, size_t chunk, unsigned* out) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -226,5 +279,26 @@ int main() {
   TILEQ(4, 256, 4, 4, true);
   TILEQ(4, 256, 4, 5, true);
   DMA(4, 4, 4, 2, 256);
+  // row bytes per k-step: 128 (gemm_mid today) vs 256, one QKV-sized matrix, activation tile included
+#define TILERB(NS_, BN_, NW_, KS_, RB_)                                                                       \
+  do {                                                                                                     \
+    const int K = 4096, rows = 12288;                                                                      \
+    const int g = rows / BN_ * KS_;                                                                        \
+    const size_t bytes = (size_t)rows * K * 2;                                                             \
+    double us = time_us([&](int i) {                                                                       \
+      tile_rb_kernel<NS_, BN_, NW_, RB_><<<g, 64 * NW_>>>(bufs[i % 3], actbuf, K, KS_, out); }, 20);       \
+    printf("qkv-size rb%d tile ns%d bn%d nw%d ks%d grid %4d  %7.2f us  %5.2f TB/s\n", RB_, NS_, BN_, NW_, KS_, g, us, \
+           bytes / us / 1e6);                                                                              \
+    fflush(stdout);                                                                                        \
+  } while (0)
+  TILERB(4, 64, 4, 1, 128);
+  TILERB(4, 64, 4, 1, 256);
+  TILERB(3, 64, 4, 1, 256);
+  TILERB(4, 128, 4, 2, 128);
+  TILERB(3, 128, 4, 2, 256);
+  TILERB(4, 192, 4, 4, 128);
+  TILERB(2, 192, 4, 4, 256);
+  TILERB(4, 96, 4, 2, 128);
+  TILERB(3, 96, 4, 2, 256);
   return 0;
 }
