@@ -898,6 +898,7 @@ __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+template <bool KTAIL>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                          const bf16_t* __restrict__ B, int64_t ldb,
                                                          const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
@@ -916,7 +917,6 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const bf16_t* __restric
   const int gm = min(GM, ntm - grp * GM);
   const int m0 = (grp * GM + gidx % gm) * 256, n0 = (gidx / gm) * 256;
   const int nk = (K + 63) / 64;
-  const bool ktail = (K & 63) != 0;  // Llama-2-7B's TP=8 down projection: K = 1376
 
   // staging: slot h, instruction i (0, 1) = 8 local rows x 128 B, local row lr = (8 i + w) * 8 + lane / 8;
   // LDS chunk lane & 7 holds global chunk (lane & 7) ^ (lr & 7)
@@ -940,7 +940,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const bf16_t* __restric
     soff[2][i] = (int64_t)bc1 * ldb * 2 + gc * 16;
   }
   auto stage = [&](int t, int h, char* buf) {
-    const bool last = ktail && t == nk - 1;  // wave-uniform
+    const bool last = KTAIL && t == nk - 1;  // wave-uniform; KTAIL: K % 64 != 0 (Llama-2-7B TP=8 down, K = 1376)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const char* p = src[h] + soff[h][i] + (int64_t)t * 128;
@@ -1800,8 +1800,12 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   if ((tsel == 2 || tsel == 6) && ns > 4) ns = 4;
   if (f8 && tsel == 4) tsel = 1;
   if (tsel == 4) {
-    gemm_pp_kernel<<<tiles_of(M, N, 256, 256), 512, 0, st>>>(X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, M, N, K, act, g,
-                                                             g_big_group_m, (K & 63) ? zero_page() : nullptr);
+    if (K & 63)
+      gemm_pp_kernel<true><<<tiles_of(M, N, 256, 256), 512, 0, st>>>(X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, M, N, K,
+                                                                     act, g, g_big_group_m, zero_page());
+    else
+      gemm_pp_kernel<false><<<tiles_of(M, N, 256, 256), 512, 0, st>>>(X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, M, N, K,
+                                                                      act, g, g_big_group_m, nullptr);
     HIP_CHECK_LAUNCH();
     return 0;
   }
