@@ -1,4 +1,4 @@
-# round 5: device-flag stream hand-off (csrc/sync.hip) - probe, GPU tests of the overlapped schedules, TP=8 sim
+# round 5 (historical: csrc/sync.hip and LLMSS_TP_DEVSYNC were removed again, profiles/r5_tbo): device-flag stream hand-off - probe, GPU tests of the overlapped schedules, TP=8 sim
 set -u
 mkdir -p gpurun_out/r5d
 T="--timeout 300 --timeout-method thread"
