@@ -85,3 +85,14 @@ def test_model_shapes_include_the_column_chunks_when_forced(monkeypatch, col):
     else:
         assert shapes["o_col"] == A.GemmShape(L.o.N // 4, L.o.K)
         assert shapes["down_col"] == A.GemmShape(L.down.N // 4, L.down.K)
+
+
+@pytest.mark.parametrize("M,N,K", [(65536, 4096, 1376), (8192, 4096, 4096), (65536, 1536, 4096), (8192, 1600, 1600)])
+def test_prompt_batch_plans_take_the_ping_pong_kernel(M, N, K):
+    """Every prompt-batch projection with enough 256x256 tiles runs the ping-pong kernel (tile code 4), including
+    K % 64 != 0 (Llama-2-7B's TP=8 down projection, K = 1376: its partial last K-tile reads a zero page; before
+    round 5 it fell back to the 128x128 kernel, profiles/r5_prefill_tp8)."""
+    from llmss_amd.ops import hip as H
+
+    nt, split = H.lib().gemm_plan(M, N, K, False)
+    assert (nt >> 8) & 15 == 4 and split == 1, (hex(nt), split)
