@@ -1,4 +1,4 @@
-# round 5: decode-attention pipeline depth in the decode step (headline bench, Llama-2-7B TP=1 + GPT-2-XL)
+# round 5 (historical: LLMSS_ATTN_UNROLL was a temporary hook, removed after this A/B): decode-attention pipeline depth in the decode step
 set -u
 mkdir -p gpurun_out/r5au
 for u in 11 12 2; do
