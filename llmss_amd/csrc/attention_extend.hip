@@ -23,11 +23,16 @@ constexpr float kLog2eX = 1.4426950408889634f;
 
 // KV8: fp8 cache rows (D e4m3 bytes + fp32 scale at byte D; reference.py kv_rows_quant), dequantised to
 // bf16 while the tile is staged into LDS.
+// q8 / s8 (optional): also write the per-token fp8-e4m3 twin of the output rows (== quant_fp8_rows_ld of them, same
+// absmax / 448 scale and clamped conversion) for the W8A8 o-projection that consumes them, which then skips its own
+// quantisation launch. Only when a workgroup holds every head of its rows: one kv head (nkv = 1) whose whole query
+// group fits the slots of a wave (GE = G, a power of two <= 16) - Llama-2-70B at TP=8 (8 query heads per rank).
 template <int D, bool KV8>
 __global__ __launch_bounds__(256) void attn_extend_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ cu_q, const int* __restrict__ ctx_lens,
-    bf16_t* __restrict__ out, int64_t out_stride, int nh, int nkv, int GE, int bs, float scale_log2) {
+    bf16_t* __restrict__ out, int64_t out_stride, int nh, int nkv, int GE, int bs, float scale_log2,
+    unsigned char* __restrict__ q8, float* __restrict__ s8) {
   constexpr int BKV = 64;
   constexpr int LD = D + 16;  // padded LDS row (elements): conflict-free b128 rows and tr_b16 columns
   __shared__ __attribute__((aligned(16))) bf16_t Ks[BKV * LD];
@@ -236,15 +241,41 @@ __global__ __launch_bounds__(256) void attn_extend_kernel(
       }
     }
   }
-  if (!valid) return;
   const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
-  bf16_t* op = out + (int64_t)(t0 + row) * out_stride + (int64_t)h * D + 4 * g;
+  u16x4 res[D / 16];
+  float amax = 0.f;
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      res[dt][i] = f2bf(o[dt][i] * inv);
+      amax = fmaxf(amax, fabsf(bf2f(res[dt][i])));
+    }
+  if (valid) {
+    bf16_t* op = out + (int64_t)(t0 + row) * out_stride + (int64_t)h * D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) *reinterpret_cast<u16x4*>(op + dt * 16) = res[dt];
+  }
+  if (q8 == nullptr) return;  // kernel argument: uniform
+  // a row's slots are GE consecutive lanes of one wave (GE | 16): reduce over them and over the 4 lane groups
+  if (!valid) amax = 0.f;
+  for (int off = 1; off < GE; off <<= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
+  amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+  amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+  if (!valid) return;
+  const float sc = amax > 0.f ? amax / 448.f : 1.f;
+  const float rs = 1.f / sc;
+  const int64_t qrow = (int64_t)(t0 + row) * (nh * D);
+  if (slot % GE == 0 && g == 0) s8[t0 + row] = sc;
 #pragma unroll
   for (int dt = 0; dt < D / 16; ++dt) {
-    u16x4 r;
+    float f[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = f2bf(o[dt][i] * inv);
-    *reinterpret_cast<u16x4*>(op + dt * 16) = r;
+    for (int i = 0; i < 4; ++i) f[i] = fminf(fmaxf(bf2f(res[dt][i]) * rs, -448.f), 448.f);
+    unsigned v = 0;
+    v = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], v, false);
+    v = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], v, true);
+    *reinterpret_cast<unsigned*>(q8 + qrow + (int64_t)h * D + dt * 16 + 4 * g) = v;
   }
 }
 
@@ -258,10 +289,15 @@ static int extend_group(int G) {
 void launch_attn_extend(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
                         const void* block_tables, int max_blocks, const void* cu_q, const void* ctx_lens, void* out,
                         int64_t out_stride, int B, int max_qlen, int nh, int nkv, int D, int bs, float scale,
-                        hipStream_t st, bool kv8) {
+                        hipStream_t st, bool kv8, void* q8v, void* s8v) {
   if (nh % nkv) throw std::runtime_error("attn_extend: nh must be a multiple of nkv");
   if (B == 0 || max_qlen == 0) return;
   const int G = nh / nkv, GE = extend_group(G);
+  auto Q8 = (unsigned char*)q8v;
+  auto S8 = (float*)s8v;
+  if ((Q8 != nullptr) != (S8 != nullptr)) throw std::runtime_error("attn_extend: fp8 twin needs both q8 and s8");
+  if (Q8 && !(nkv == 1 && GE == G && G <= 16 && (G & (G - 1)) == 0))
+    throw std::runtime_error("attn_extend: the fp8 twin needs one kv head and a power-of-two query group <= 16");
   const int rows = 64 / GE;
   dim3 grid((max_qlen + rows - 1) / rows, nkv * (G / GE), B);
   auto Q = (const bf16_t*)q;
@@ -276,10 +312,10 @@ void launch_attn_extend(const void* q, int64_t q_stride, const void* k_cache, co
   do {                                                                                                           \
     if (kv8)                                                                                                     \
       attn_extend_kernel<D_, true><<<grid, 256, 0, st>>>(Q, q_stride, K, V, BT, max_blocks, CU, CL, O, out_stride, nh, \
-                                                         nkv, GE, bs, sl);                                       \
+                                                         nkv, GE, bs, sl, Q8, S8);                               \
     else                                                                                                         \
       attn_extend_kernel<D_, false><<<grid, 256, 0, st>>>(Q, q_stride, K, V, BT, max_blocks, CU, CL, O, out_stride,   \
-                                                          nh, nkv, GE, bs, sl);                                  \
+                                                          nh, nkv, GE, bs, sl, Q8, S8);                          \
   } while (0)
   switch (D) {
     case 64: LX(64); break;

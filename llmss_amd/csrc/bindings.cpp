@@ -38,7 +38,7 @@ void launch_ce_loss(const void* logits, int64_t ld, bool fp32, const void* label
 void launch_attn_extend(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
                         const void* block_tables, int max_blocks, const void* cu_q, const void* ctx_lens, void* out,
                         int64_t out_stride, int B, int max_qlen, int nh, int nkv, int D, int bs, float scale,
-                        hipStream_t st, bool kv8);
+                        hipStream_t st, bool kv8, void* q8, void* s8);
 int launch_gemm_qkv_args(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y, int64_t ldy,
                          int M, int N, int K, void* workspace, int64_t ws_bytes, int nt_hint, int split_hint,
                          const void* pos, const void* cos_t, const void* sin_t, void* kc, void* vc, const void* slot,
@@ -123,10 +123,14 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("attn_extend", [](uintptr_t q, int64_t qs, uintptr_t kc, uintptr_t vc, uintptr_t bt, int maxb, uintptr_t cu,
                           uintptr_t cl, uintptr_t out, int64_t os, int B, int maxq, int nh, int nkv, int D, int bs,
-                          float scale, uintptr_t st, bool kv8) {
+                          float scale, uintptr_t st, bool kv8, uintptr_t q8, uintptr_t s8) {
     launch_attn_extend(CP(q), qs, CP(kc), CP(vc), CP(bt), maxb, CP(cu), CP(cl), P(out), os, B, maxq, nh, nkv, D, bs,
-                       scale, S(st), kv8);
-  });
+                       scale, S(st), kv8, P(q8), P(s8));
+  }, pybind11::arg("q"), pybind11::arg("qs"), pybind11::arg("kc"), pybind11::arg("vc"), pybind11::arg("bt"),
+     pybind11::arg("maxb"), pybind11::arg("cu"), pybind11::arg("cl"), pybind11::arg("out"), pybind11::arg("os"),
+     pybind11::arg("B"), pybind11::arg("maxq"), pybind11::arg("nh"), pybind11::arg("nkv"), pybind11::arg("D"),
+     pybind11::arg("bs"), pybind11::arg("scale"), pybind11::arg("st"), pybind11::arg("kv8"), pybind11::arg("q8") = 0,
+     pybind11::arg("s8") = 0);
   m.def("gemm", [](uintptr_t x, int64_t ldx, uintptr_t w, int64_t ldw, bool fp8, uintptr_t ws, uintptr_t bias,
                    uintptr_t y, int64_t ldy, int M, int N, int K, int act, bool glu, uintptr_t work, int64_t wbytes,
                    int nt_hint, int split_hint, bool partial_out, uintptr_t st) {

@@ -180,8 +180,11 @@ class DecoderLM:
         qkv = self._qkv_rope_cache(L, y, inp, kc, vc)
         if inp.kind == "decode" and qkv.is_cuda and qkv.shape[0] in self.gqa_mfma:
             B = qkv.shape[0]
+            # fp8 models whose rank holds one kv head (Llama-2-70B at TP=8): the attention launch also writes the
+            # o-projection's per-token fp8 input, so the W8A8 GEMM skips its own quantisation launch
+            f8 = self._fp8_in(L.o, qkv) and _hip_ops().extend_fp8_twin_ok(p.nh_l, p.nkv_l)
             return ops.attn_extend(qkv, kc, vc, inp.block_tables, self.decode_cu(B, qkv.device), inp.ctx_lens, 1,
-                                   p.nh_l, p.nkv_l, D, self.scale)
+                                   p.nh_l, p.nkv_l, D, self.scale, fp8_out=f8)
         if inp.kind == "prefill":
             return ops.attn_prefill(qkv, inp.cu_seqlens, inp.max_seqlen, p.nh_l, p.nkv_l, D, self.scale)
         if inp.kind == "extend":

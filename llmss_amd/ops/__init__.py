@@ -72,11 +72,13 @@ def attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale, 
     return _into(ref.attn_decode(q, k_cache, v_cache, block_tables, ctx_lens, nh, nkv, D, scale), out)
 
 
-def attn_extend(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_qlen, nh, nkv, D, scale, out=None):
-    """Chunked-prefill attention over the paged cache (the chunk's K/V already written)."""
+def attn_extend(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_qlen, nh, nkv, D, scale, out=None,
+                fp8_out=False):
+    """Chunked-prefill attention over the paged cache (the chunk's K/V already written). ``fp8_out``: the GPU
+    kernel also writes the per-token fp8 twin for a W8A8 consumer (ops.hip.attn_extend); ignored on the CPU."""
     if q.is_cuda:
         return _hip().attn_extend(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_qlen, nh, nkv, D, scale,
-                                  out=out)
+                                  out=out, fp8_out=fp8_out)
     return _into(ref.attn_extend(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, nh, nkv, D, scale), out)
 
 

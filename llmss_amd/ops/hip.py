@@ -186,10 +186,20 @@ def attn_prefill(qkv, cu_seqlens, max_seqlen, nh, nkv, D, scale, out=None):
     return y
 
 
-def attn_extend(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_qlen, nh, nkv, D, scale, out=None):
+def extend_fp8_twin_ok(nh: int, nkv: int) -> bool:
+    """Can attn_extend write the per-token fp8 twin of its output in the same launch (every head of a row in
+    one workgroup: one kv head, a power-of-two query group <= 16)?"""
+    G = nh // nkv
+    return nkv == 1 and G <= 16 and G & (G - 1) == 0
+
+
+def attn_extend(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_qlen, nh, nkv, D, scale, out=None,
+                fp8_out=False):
     """Chunked-prefill attention: q rows [T, >= nh*D] (query heads first, as in the QKV output) of B
     sequences (``cu_q`` [B+1] int32), each attending its whole paged context ``ctx_lens`` [B] int32 (the
-    chunk's own K/V already written to the cache) causally."""
+    chunk's own K/V already written to the cache) causally. ``fp8_out`` (only where extend_fp8_twin_ok):
+    also write the output's per-token fp8 twin for the W8A8 o-projection, which then skips its quantisation
+    launch."""
     T = q.shape[0]
     _bf16_rows(q, "q")
     _check(q.shape[1] >= nh * D, "q too narrow")
@@ -205,9 +215,13 @@ def attn_extend(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_qlen, nh,
     y = out if out is not None else torch.empty(T, nh * D, dtype=q.dtype, device=q.device)
     _bf16_rows(y, "out")
     _check(y.shape[0] >= T and y.shape[1] >= nh * D, "out shape")
+    q8 = s8 = None
+    if fp8_out:
+        _check(extend_fp8_twin_ok(nh, nkv) and y.shape == (T, nh * D), "fp8 twin: one kv head, group <= 16, dense out")
+        q8, s8 = _fp8_twin(y)
     lib().attn_extend(q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
                       block_tables.shape[1], cu_q.data_ptr(), ctx_lens.data_ptr(), y.data_ptr(), y.stride(0), B,
-                      int(max_qlen), nh, nkv, D, bs, float(scale), _stream(), kv8)
+                      int(max_qlen), nh, nkv, D, bs, float(scale), _stream(), kv8, _ptr(q8), _ptr(s8))
     return y
 
 

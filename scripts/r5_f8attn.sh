@@ -1,0 +1,10 @@
+# round 5: fp8 twin fused into the extend attention (70B TP=8: one kv head per rank) - tests, 70B fp8 TP=8 shard
+set -u
+mkdir -p gpurun_out/r5fa
+T="--timeout 300 --timeout-method thread"
+timeout -k 10 600 python -u -m pytest tests/test_chunked_prefill.py tests/test_kv_fp8.py -q -x -rf -m gpu $T > gpurun_out/r5fa/tests.log 2>&1 || { tail -30 gpurun_out/r5fa/tests.log; exit 1; }
+tail -1 gpurun_out/r5fa/tests.log
+timeout -k 10 600 python -u -m pytest tests/test_hf_parity_gpu.py -q -x -rf -k fp8 $T > gpurun_out/r5fa/parity.log 2>&1 || { tail -30 gpurun_out/r5fa/parity.log; exit 1; }
+tail -1 gpurun_out/r5fa/parity.log
+timeout -k 10 600 python bench.py --model llama2-70b --fp8 --simulate-tp 8 --steps 2 --warmup 1 --secondary none > gpurun_out/r5fa/llama70b_fp8_tp8sim.log 2>&1 || { tail -20 gpurun_out/r5fa/llama70b_fp8_tp8sim.log; exit 1; }
+python3 -c "import json; d=json.loads(open('gpurun_out/r5fa/llama70b_fp8_tp8sim.log').read().strip().splitlines()[-1]); print('70b_fp8_tp8sim', d['value'], d['p50_tpot_ms'], d['p50_ttft_ms'])"

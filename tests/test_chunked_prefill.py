@@ -170,3 +170,48 @@ def test_gpu_chunked_engine_matches_whole_prompt(tmp_path, name):
                                                     name, k, top2.tolist(), got, ref)
             break
     assert compared >= 0.6 * sum(len(x) for x in ref), (compared, got, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nh,D", [(8, 128), (4, 64), (16, 128), (2, 256)])
+def test_extend_kernel_fp8_twin_equals_the_quant_launch(nh, D):
+    """One kv head per rank (Llama-2-70B at TP=8: 8 query heads): the extend kernel's fused per-token fp8 twin of its
+    output equals quant_fp8_rows_ld of that output bit for bit (same absmax / 448 scale, same clamped conversion),
+    for decode rows and multi-token chunks, and the bf16 output is unchanged; the twin is registered for the W8A8
+    o-projection that consumes the tensor next."""
+    from llmss_amd.ops import hip as H
+
+    torch.manual_seed(3)
+    dev = torch.device("cuda")
+    nkv, bs, nb = 1, 16, 96
+    seqs = [(0, 37), (150, 20), (33, 64), (70, 1), (5, 130), (16, 1), (200, 1)]
+    kc = (torch.randn(nb, nkv, bs, D, device=dev) * 0.5).to(torch.bfloat16)
+    vc = torch.randn(nb, nkv, bs, D, device=dev).to(torch.bfloat16)
+    maxb = max((p + q + bs - 1) // bs for p, q in seqs)
+    perm = torch.randperm(nb)
+    bt = torch.zeros(len(seqs), maxb, dtype=torch.int32)
+    k = 0
+    for i, (p, q) in enumerate(seqs):
+        n = (p + q + bs - 1) // bs
+        bt[i, :n] = perm[k:k + n].to(torch.int32)
+        k += n
+    T = sum(q for _, q in seqs)
+    qrows = (torch.randn(T, (nh + 2 * nkv) * D, device=dev)).to(torch.bfloat16)
+    cu = torch.tensor([0] + torch.tensor([q for _, q in seqs]).cumsum(0).tolist(), dtype=torch.int32, device=dev)
+    ctx = torch.tensor([p + q for p, q in seqs], dtype=torch.int32, device=dev)
+    bt = bt.to(dev)
+    mq = max(q for _, q in seqs)
+    assert H.extend_fp8_twin_ok(nh, nkv)
+    plain = H.attn_extend(qrows, kc, vc, bt, cu, ctx, mq, nh, nkv, D, D ** -0.5)
+    got = H.attn_extend(qrows, kc, vc, bt, cu, ctx, mq, nh, nkv, D, D ** -0.5, fp8_out=True)
+    assert torch.equal(got, plain)
+    tq, ts = H._prequant_of(got)
+    K = nh * D
+    rq = torch.empty(T, K, dtype=torch.uint8, device=dev)
+    rs = torch.empty(T, dtype=torch.float32, device=dev)
+    H.lib().quant_fp8_rows_ld(got.data_ptr(), got.stride(0), rq.data_ptr(), rs.data_ptr(), T, K, H._stream())
+    torch.cuda.synchronize()
+    assert torch.equal(ts, rs)
+    assert torch.equal(tq, rq)
+    # heads of a row spread over workgroups / waves: no fused twin
+    assert not H.extend_fp8_twin_ok(8, 2) and not H.extend_fp8_twin_ok(32, 1) and not H.extend_fp8_twin_ok(12, 1)
