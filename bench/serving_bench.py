@@ -3,6 +3,8 @@ one MI355X served over gRPC"; "pubsub producer/consumer under concurrent gRPC cl
 
   --mode grpc    clients -> gRPC Generate service on the engine driver (direct)
   --mode pubsub  clients -> gRPC front-end -> RESP broker (mini Redis) -> consumer -> engine
+                 (front-end and broker in their own process, as a producer server and Redis would be;
+                 --frontend-inproc puts them in the engine process, sharing its interpreter lock)
 
 Random-init weights of the named architecture, random printable prompts (byte tokenizer: one
 token per character). Prints one JSON line: output tokens/s over the timed requests, p50 request
@@ -142,8 +144,23 @@ def main():
     ap.add_argument("--num-requests", type=int, default=256, help="open loop: requests in total")
     ap.add_argument("--long-len", type=int, default=2048, help="open loop: length of the long prompts")
     ap.add_argument("--long-frac", type=float, default=0.1, help="open loop: share of long prompts")
+    ap.add_argument("--frontend-inproc", action="store_true",
+                    help="pubsub: run the broker and the gRPC front-end inside the engine process")
     ap.add_argument("--client-port", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--frontend", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args()
+
+    if a.frontend:  # pub/sub front-end role: broker + gRPC BrokerServicer, no GPU; runs until stdin closes
+        from llmss_amd.serving.broker import MiniRedisServer, RedisBroker
+        from llmss_amd.serving.grpc_api import BrokerServicer, serve
+
+        mini = MiniRedisServer().start()
+        srv = serve(BrokerServicer(RedisBroker(mini.host, mini.port)), port=0, host="127.0.0.1")
+        print(f"{mini.port} {srv.bound_port}", flush=True)
+        sys.stdin.read()
+        srv.stop(0).wait(30)
+        mini.stop()
+        return
 
     if a.client_port:
         if a.client_port < 0:  # spawned before the parent touched the GPU; the port comes on stdin
@@ -156,6 +173,11 @@ def main():
         f"--{k.replace('_', '-')}={v}" for k, v in vars(a).items()
         if k in ("clients", "requests", "prompt_len", "gen_len", "rate", "num_requests", "long_len", "long_frac")]
     child = subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    fe = None
+    if a.mode == "pubsub" and not a.frontend_inproc:  # started before this process touches the GPU
+        fe = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--frontend"], stdin=subprocess.PIPE,
+                              stdout=subprocess.PIPE, text=True)
+        fe_broker_port, fe_grpc_port = map(int, fe.stdout.readline().split())
 
     import torch
 
@@ -176,16 +198,23 @@ def main():
     servers, consumer, mini = [], None, None
     if a.mode == "grpc":
         srv = serve(EngineServicer(drv, tok), port=0, host="127.0.0.1")
+        servers.append(srv)
+        port = srv.bound_port
+    elif fe is not None:
+        consumer = Consumer(drv, tok, RedisBroker("127.0.0.1", fe_broker_port), poll_timeout=0.05).start()
+        port = fe_grpc_port
     else:
         mini = MiniRedisServer().start()
         consumer = Consumer(drv, tok, RedisBroker(mini.host, mini.port), poll_timeout=0.05).start()
         srv = serve(BrokerServicer(RedisBroker(mini.host, mini.port)), port=0, host="127.0.0.1")
-    servers.append(srv)
-    out, _ = child.communicate(f"{srv.bound_port}\n", timeout=1800)
+        servers.append(srv)
+        port = srv.bound_port
+    out, _ = child.communicate(f"{port}\n", timeout=1800)
     if child.returncode:
         raise RuntimeError(f"client process failed with exit code {child.returncode}")
     res = json.loads(out.strip().splitlines()[-1])
     res.update(mode=a.mode, model=a.model, fp8=a.fp8, data="synthetic prompts, random-init weights",
+               frontend=None if a.mode == "grpc" else ("in-process" if fe is None else "own process"),
                prefill_chunk=eng.prefill_chunk, engine_stats=eng.stats)
     print(json.dumps(res), flush=True)
     # orderly shutdown: front-ends first, then the engine thread, then device state. A teardown that takes
@@ -197,6 +226,9 @@ def main():
         consumer.stop()
     if mini is not None:
         mini.stop()
+    if fe is not None:
+        fe.stdin.close()
+        fe.wait(60)
     drv.stop()
     if dev.type == "cuda":
         torch.cuda.synchronize()

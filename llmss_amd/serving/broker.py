@@ -5,8 +5,11 @@
   required); speaks to a real ``redis-server`` or to :class:`MiniRedisServer`.
 * :class:`MemoryBroker` - thread-safe in-process lists (tests, single-process serving).
 * :class:`MiniRedisServer` - a small threaded RESP server implementing the list commands the
-  pub/sub path needs (LPUSH/RPUSH/LPOP/RPOP/LLEN/BRPOP/BLPOP/DEL/PING), so the PoC runs where no
-  ``redis-server`` is installed.
+  pub/sub path needs (LPUSH/RPUSH/LPOP/RPOP/LLEN/BRPOP/BLPOP/RPOPLPUSH/BRPOPLPUSH/LREM/LRANGE/DEL/PING), so the
+  PoC runs where no ``redis-server`` is installed.
+
+:meth:`Broker.pipeline` runs a list of commands in order; the RESP client writes them in one send and reads the
+replies together (Redis pipelining), so a burst of replies or pops costs one round trip instead of one each.
 
 Blocking pops (``brpop``) replace the reference's busy ``while True: if llen: rpop`` loops
 (quirk Q11); replies are correlated by request id (``squeue:<id>``).
@@ -53,6 +56,10 @@ class Broker:
         consumer's in-flight request stays in its processing list until it is acknowledged with lrem."""
         raise NotImplementedError
 
+    def rpoplpush(self, src: str, dst: str) -> Optional[str]:
+        """Non-blocking RPOPLPUSH: None when ``src`` is empty."""
+        raise NotImplementedError
+
     def lrem(self, key: str, count: int, value: str) -> int:
         raise NotImplementedError
 
@@ -61,6 +68,19 @@ class Broker:
 
     def delete(self, key: str) -> int:
         raise NotImplementedError
+
+    def pipeline(self, cmds: List[Tuple]) -> List:
+        """Run ``cmds`` (tuples like ``("LPUSH", key, value)``) in order and return their replies; a command that
+        fails yields its exception object in place of a reply, and the rest still run."""
+        ops = {"LPUSH": self.lpush, "RPUSH": self.rpush, "RPOP": self.rpop, "LPOP": self.lpop, "LLEN": self.llen,
+               "RPOPLPUSH": self.rpoplpush, "LREM": self.lrem, "DEL": self.delete}
+        out = []
+        for c in cmds:
+            try:
+                out.append(ops[c[0].upper()](*c[1:]))
+            except Exception as e:  # noqa: BLE001 - per-command result, like a RESP error reply
+                out.append(e)
+        return out
 
     def close(self):
         pass
@@ -140,6 +160,16 @@ class MemoryBroker(Broker):
                 if rem is not None and rem <= 0:
                     return None
                 self._cv.wait(rem)
+
+    def rpoplpush(self, src, dst):
+        with self._cv:
+            q = self._lists.get(src)
+            if not q:
+                return None
+            v = q.pop()
+            self._lists[dst].appendleft(v)
+            self._cv.notify_all()
+            return v
 
     def lrem(self, key, count, value):
         """Remove up to ``count`` occurrences of ``value`` (0 = all; < 0 = from the tail), like Redis."""
@@ -274,6 +304,26 @@ class RedisBroker(Broker):
     def brpoplpush(self, src, dst, timeout=0):
         return self.execute("BRPOPLPUSH", src, dst, _fmt_timeout(timeout))
 
+    def rpoplpush(self, src, dst):
+        return self.execute("RPOPLPUSH", src, dst)
+
+    def pipeline(self, cmds):
+        if not cmds:
+            return []
+        s, r = self._conn()
+        try:
+            s.sendall(b"".join(_encode(*c) for c in cmds))
+            out = []
+            for _ in cmds:
+                try:
+                    out.append(r.value())
+                except RuntimeError as e:  # an error reply; the stream stays in sync
+                    out.append(e)
+            return out
+        except (ConnectionError, OSError):
+            self._local.conn = None
+            raise
+
     def lrem(self, key, count, value):
         return self.execute("LREM", key, int(count), value)
 
@@ -377,6 +427,8 @@ class MiniRedisServer:
                 v = store.brpoplpush(a[0], a[1], min(rem, 0.05) if rem is not None else 0.05)
                 if v is not None:
                     return ("bulk", v)
+        if op == "RPOPLPUSH":
+            return ("bulk", store.rpoplpush(a[0], a[1]))
         if op == "LREM":
             return store.lrem(a[0], int(a[1]), a[2])
         if op == "LRANGE":

@@ -216,6 +216,52 @@ def test_redis_broker_list_commands():
     srv.stop()
 
 
+@pytest.mark.parametrize("kind", ["memory", "resp"])
+def test_broker_pipeline(kind):
+    """Pipelined commands run in order with one reply each; an error reply sits in its slot and the commands after
+    it still run; RPOPLPUSH on an empty list is None (the consumer's batched intake)."""
+    srv = MiniRedisServer().start() if kind == "resp" else None
+    b = RedisBroker(srv.host, srv.port) if srv else MemoryBroker()
+    try:
+        r = b.pipeline([("LPUSH", "q", "a"), ("LPUSH", "q", "b"), ("RPOPLPUSH", "q", "p"), ("NOPE", "x"),
+                        ("RPOPLPUSH", "q", "p"), ("RPOPLPUSH", "q", "p"), ("LREM", "p", 1, "a"), ("LLEN", "p")])
+        assert r[:3] == [1, 2, "a"] and isinstance(r[3], Exception)
+        assert r[4:] == ["b", None, 1, 1]
+        assert b.lrange("p", 0, -1) == ["b"] and b.pipeline([]) == []
+    finally:
+        if srv:
+            srv.stop()
+
+
+def test_consumer_takes_a_queued_burst_in_one_step(driver):
+    """Requests already queued when the consumer wakes are popped together (one blocking pop plus one pipeline of
+    non-blocking pops) and admitted in a single prefill step; every one is answered and acknowledged."""
+    from llmss_amd.serving.consumer import processing_key
+
+    drv, tok, m = driver
+    srv = MiniRedisServer().start()
+    b = RedisBroker(srv.host, srv.port)
+    n = 6
+    for i in range(n):
+        b.lpush(PQUEUE, json.dumps({"prompt": f"burst {i}", "max_new_tokens": 3, "is_greedy": True,
+                                    "temperature": 1.0, "top_p": 0.95, "top_k": 50, "request_id": f"b{i}"}))
+    before = drv.engine.stats["prefill_steps"]
+    consumer = Consumer(drv, tok, RedisBroker(srv.host, srv.port), poll_timeout=0.2, consumer_id="cb").start()
+    try:
+        for i in range(n):
+            msg = b.brpop(reply_key(f"b{i}"), 60)
+            assert msg is not None and json.loads(msg)["continuation"] == _offline(m, tok, f"burst {i}", 3)
+        assert drv.engine.stats["prefill_steps"] - before == 1
+        for _ in range(100):
+            if b.llen(processing_key("cb")) == 0:
+                break
+            time.sleep(0.05)
+        assert b.llen(processing_key("cb")) == 0 and consumer.served == n
+    finally:
+        consumer.stop()
+        srv.stop()
+
+
 def test_admission_window_batches_a_burst(driver):
     """A burst of concurrent submissions to an idle driver is admitted in one prefill step."""
     drv, tok, m = driver
