@@ -3,6 +3,7 @@ TP driver + consumer, gRPC (direct and via the broker), request/response correla
 concurrent clients (reference quirk Q11), and reference-format interoperability."""
 import concurrent.futures as cf
 import json
+import os
 import threading
 import time
 
@@ -416,3 +417,20 @@ def test_aio_server_stop_completes_on_its_own_loop(driver):
         with pytest.raises(grpc.RpcError):
             stub.Generate(GenerateRequest(prompt="x", max_new_tokens=1), timeout=5)
         ch.close()
+
+
+@pytest.mark.parametrize("mode", [["--mode", "pubsub"], ["--mode", "pubsub", "--frontend-inproc"], ["--mode", "grpc"]])
+def test_serving_bench_runs_on_cpu(mode):
+    """bench/serving_bench.py end to end on a tiny model: client process, (for pub/sub) the front-end + broker
+    process, consumer and engine; one JSON line whose requests were all answered."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench", "serving_bench.py"), "--model", "tiny-llama",
+                        "--clients", "3", "--requests", "2", "--prompt-len", "12", "--gen-len", "4"] + mode,
+                       capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["requests"] == 6 and d["value"] > 0
+    assert d["frontend"] == (None if "grpc" in mode else ("in-process" if "--frontend-inproc" in mode else "own process"))
