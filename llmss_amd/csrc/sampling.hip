@@ -163,6 +163,7 @@ __global__ __launch_bounds__(1024) void sample_kernel(const T* __restrict__ logi
 // ---------------------------------------------------------------------------------------------
 constexpr int SV3_BINS = 2048;
 constexpr int SV3_MAXC = 2048;
+constexpr int SV3_SORT_MIN = 128;  // boundary bins with more candidates are sorted (sv3_sort), fewer ranked all-pairs
 
 struct Sv3Smem {
   unsigned cnt[SV3_BINS];
@@ -210,6 +211,33 @@ __device__ void sv3_find(const T* arr, unsigned long long target, int limit, Sv3
   if (e0 < target && e0 + a0 >= target) { sm.bin = 2 * t; sm.excl = e0; }
   else if (e1 < target && e1 + a1 >= target) { sm.bin = 2 * t + 1; sm.excl = e1; }
   __syncthreads();
+}
+
+// Sort the boundary bin's n candidates (sm.cv / sm.ci) into rank order - value descending, index ascending, the
+// strict order the selection uses - with a bitonic network over the next power of two (<= SV3_MAXC, padding
+// -inf / INT_MAX sorts last). O(n log^2 n) work in log^2 barrier steps: the rank selections below then read
+// position r - 1 (top-k) and an integer prefix scan (top-p) instead of comparing every candidate with every
+// other one, which took 100-170 us per call on a flat top-p row (n ~ 1-2 K; bench/sampler_bench.py).
+__device__ __attribute__((noinline)) void sv3_sort(Sv3Smem& sm, int n) {
+  int P = 1;
+  while (P < n) P <<= 1;
+  for (int i = n + (int)threadIdx.x; i < P; i += blockDim.x) { sm.cv[i] = -INFINITY; sm.ci[i] = 0x7fffffff; }
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = threadIdx.x; t < (P >> 1); t += blockDim.x) {
+        const int i = 2 * t - (t & (j - 1)), l = i + j;
+        const float vi = sm.cv[i], vl = sm.cv[l];
+        const int ii = sm.ci[i], il = sm.ci[l];
+        const bool l_first = vl > vi || (vl == vi && il < ii);
+        if (l_first == ((i & k) == 0)) {
+          sm.cv[i] = vl; sm.cv[l] = vi;
+          sm.ci[i] = il; sm.ci[l] = ii;
+        }
+      }
+      __syncthreads();
+    }
+  }
 }
 
 // LROW: the packed row lives in LDS instead of VGPRs. At CPT = 8 (vocab 32K-57K, e.g. GPT-2's
@@ -298,7 +326,10 @@ FOR_ELEMS(i) {
       if (n > SV3_MAXC) {  // pathological tie mass: keep the whole bin
         thr = mx - (float)(bk + 1) / 32.f;
         thr = nextafterf(thr, INFINITY);
-      } else {
+      } else if (n > SV3_SORT_MIN) {
+        sv3_sort(sm, n);
+        thr = sm.cv[r - 1];  // the k-th largest (1 <= r <= n: bk holds it)
+      } else {  // a few candidates: all-pairs ranks in one pass beat the sort's barrier steps
         for (int c = tid; c < n; c += 1024) {
           const float v = sm.cv[c];
           const int vi = sm.ci[c];
@@ -348,7 +379,17 @@ FOR_ELEMS(i) {
       float tp = -INFINITY;
       if (n > SV3_MAXC) {
         tp = nextafterf(mx - (float)(bp + 1) / 32.f, INFINITY);
-      } else {
+      } else if (n > SV3_SORT_MIN) {
+        // rank order, then the first candidate whose inclusive mass prefix (above + masses ranked before it +
+        // its own) reaches the target; integer sums, so every rank finds the same one. The histogram is no
+        // longer needed: its mass array holds the sorted candidates' masses.
+        sv3_sort(sm, n);
+        for (int c = tid; c < n; c += 1024) sm.mass[c] = sv3_mass(sm.cv[c], mx);
+        __syncthreads();
+        sv3_find(sm.mass, target - above, n, sm);
+        const int c = sm.bin;
+        tp = sm.excl + sm.mass[c] >= target - above ? sm.cv[c] : -INFINITY;
+      } else {  // a few candidates: the same selection with all-pairs sums
         if (tid == 0) sm.thr = -INFINITY;
         __syncthreads();
         for (int c = tid; c < n; c += 1024) {
@@ -418,12 +459,10 @@ void launch_sample(const void* logits, int64_t ld, bool fp32_logits, int B, int 
   sample_v3_kernel<CPT_, LROW_><<<B, 1024, 0, st>>>((const bf16_t*)logits, ld, V, (const float*)temperature,      \
                                                     (const int*)top_k, (const float*)top_p, (const int64_t*)seeds, \
                                                     (int64_t*)out, (int64_t*)out2)
-    static const bool lrow_small = [] {  // LLMSS_SAMPLER_LROW=1: LDS-resident rows at CPT 2 / 4 too
-      const char* e = getenv("LLMSS_SAMPLER_LROW");
-      return e && e[0] == '1';
-    }();
-    if (chunks <= 2048) { if (lrow_small) SV3(2, true); else SV3(2, false); }
-    else if (chunks <= 4096) { if (lrow_small) SV3(4, true); else SV3(4, false); }
+    // register-resident rows up to CPT 4 (LDS rows measured 2-10 % slower there, profiles/r5_sampler); CPT 8
+    // would spill, so its row lives in LDS
+    if (chunks <= 2048) SV3(2, false);
+    else if (chunks <= 4096) SV3(4, false);
     else SV3(8, true);
 #undef SV3
     HIP_CHECK_LAUNCH();

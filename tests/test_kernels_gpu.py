@@ -520,6 +520,28 @@ def test_sample_kept_set_exact(V, k, p, temp):
             assert seen[b] == sets[b]
 
 
+@pytest.mark.parametrize("V", [32000, 50304, 1000])
+@pytest.mark.parametrize("k,p,scale", [(0, 0.95, 0.3), (0, 0.5, 0.5), (2000, 0.9, 0.3), (40, 0.95, 0.05)])
+def test_sample_flat_rows(V, k, p, scale):
+    """Near-flat logits put hundreds of tokens into the boundary bin of the top-p / top-k selection (the
+    sorted-candidate path of sample_v3_kernel): every draw in the exact kept set, identical on a repeat. Scales are
+    chosen so the boundary bin holds at most SV3_MAXC = 2048 tokens; beyond that the kernel keeps the whole bin by
+    design (a superset of the exact set)."""
+    torch.manual_seed(V + k)
+    B = 4
+    logits = rnd(B, V, scale=scale)
+    sets = _kept_sets(logits, 1.0, k, p)
+    tt = torch.ones(B, device=dev)
+    tk = torch.full((B,), k, dtype=torch.int32, device=dev)
+    tp = torch.full((B,), p, device=dev)
+    for s in range(16):
+        seeds = torch.arange(B, dtype=torch.int64, device=dev) * 7919 + s * 104729
+        o = H.sample(logits, tt, tk, tp, seeds).tolist()
+        assert o == H.sample(logits, tt, tk, tp, seeds).tolist()
+        for b in range(B):
+            assert o[b] in sets[b], (b, o[b], len(sets[b]))
+
+
 @pytest.mark.parametrize("tile,stages", [(1, 2), (1, 3), (2, 2), (2, 4), (3, 3), (3, 4)])
 @pytest.mark.parametrize("per_cu", [1, 2, 3])
 @pytest.mark.parametrize("M,N,K", [(512, 1536, 4096), (300, 2752, 1376), (64, 4096, 11008), (130, 544, 208)])
