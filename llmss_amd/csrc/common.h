@@ -303,6 +303,74 @@ __device__ __forceinline__ void qkv_store_chunk(const QkvEpi& e, const float* ct
   }
 }
 
+// Stores rows [r0, r0 + rows) of a tile's fp32 epilogue image (EpiImg<BN> layout at `ct`, row 0 = tile row r0)
+// cooperatively over NTHR threads: fp32 split-K slab rows (part), the QKV RoPE / KV-write epilogue (qe.D), SwiGLU
+// pairs (glu) or bf16 rows with bias / activation. Shared by tile_store_lds and the decode GEMM (gemm_dec.hip),
+// which builds the image from K-split waves.
+template <int BN, int NTHR, int R>
+__device__ __forceinline__ void img_store_rows(const float* ct, int rows, int r0, int m0, int n0, int M, int N,
+                                               float* __restrict__ part, bf16_t* __restrict__ Y, int64_t ldy,
+                                               const bf16_t* __restrict__ bias, int act, int glu, const QkvEpi& qe) {
+  using Img = EpiImg<BN>;
+  if (qe.D) {  // QKV projection: RoPE + paged KV write (N % 8 == 0, ldy % 8 == 0: host-checked)
+    qkv_store_chunk<BN, NTHR, R>(qe, ct, rows, r0, m0, n0, M, N, Y, ldy, bias);
+  } else if (part) {  // fp32 slab rows: 4 floats (16 B) per thread-step
+    constexpr int VPR = BN / 4;
+    for (int v = threadIdx.x; v < rows * VPR; v += NTHR) {
+      const int r = v / VPR, c = (v - r * VPR) * 4;
+      const int m = m0 + r0 + r, n = n0 + c;
+      if (m >= M || n >= N) continue;
+      const f32x4 val = Img::ld4(ct, r, c);
+      float* dst = part + (int64_t)m * N + n;
+      if (n + 3 < N && (N & 3) == 0) *reinterpret_cast<f32x4*>(dst) = val;
+      else
+        for (int j = 0; j < 4 && n + j < N; ++j) dst[j] = val[j];
+    }
+  } else if (glu) {  // out col 16p + j = silu(gate col 32p + j) * up col 32p + 16 + j, 8 per thread-step
+    constexpr int VPR = BN / 16;
+    for (int v = threadIdx.x; v < rows * VPR; v += NTHR) {
+      const int r = v / VPR, oc = (v - r * VPR) * 8;
+      const int p = oc >> 4, j = oc & 15;
+      const int cg = 32 * p + j, m = m0 + r0 + r, ng = n0 + cg;
+      if (m >= M || ng >= N) continue;  // N % 32 == 0: the whole gate|up pair exists
+      u16x8 o;
+      float gx[8], ux[8];
+      Img::ld8(ct, r, cg, gx);
+      Img::ld8(ct, r, cg + 16, ux);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float gv = gx[e], uv = ux[e];
+        if (bias) { gv += bf2f(bias[ng + e]); uv += bf2f(bias[ng + 16 + e]); }
+        o[e] = f2bf(silu(gv) * uv);
+      }
+      bf16_t* dst = Y + (int64_t)m * ldy + n0 / 2 + oc;
+      if (ng + 16 + 7 < N && (ldy & 7) == 0) *reinterpret_cast<u16x8*>(dst) = o;
+      else
+        for (int e = 0; e < 8 && ng + 16 + e < N; ++e) dst[e] = o[e];
+    }
+  } else {  // bf16 rows: 8 values (16 B) per thread-step
+    constexpr int VPR = BN / 8;
+    for (int v = threadIdx.x; v < rows * VPR; v += NTHR) {
+      const int r = v / VPR, c = (v - r * VPR) * 8;
+      const int m = m0 + r0 + r, n = n0 + c;
+      if (m >= M || n >= N) continue;
+      u16x8 o;
+      float xv[8];
+      Img::ld8(ct, r, c, xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = xv[e];
+        if (bias && n + e < N) x += bf2f(bias[n + e]);
+        o[e] = f2bf(apply_act(x, act));
+      }
+      bf16_t* dst = Y + (int64_t)m * ldy + n;
+      if (n + 7 < N && (ldy & 7) == 0) *reinterpret_cast<u16x8*>(dst) = o;
+      else
+        for (int e = 0; e < 8 && n + e < N; ++e) dst[e] = o[e];
+    }
+  }
+}
+
 // Cooperative GEMM epilogue through LDS. A wave's accumulators (MT x NT mfma_f32_16x16x32 tiles in
 // the C layout: lane (li = lane & 15, g = lane >> 4) holds rows 4g..4g+3 of column li) are written
 // row-major into a padded fp32 image in LDS, then every thread stores 16 B row-contiguous pieces:
@@ -339,63 +407,7 @@ __device__ __forceinline__ void tile_store_lds(const f32x4 (&acc)[MT][NT], char*
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const int rows = BM - r0 < R ? BM - r0 : R;  // the last chunk may be shorter
-    if (qe.D) {  // QKV projection: RoPE + paged KV write (N % 8 == 0, ldy % 8 == 0: host-checked)
-      qkv_store_chunk<BN, NTHR, R>(qe, ct, rows, r0, m0, n0, M, N, Y, ldy, bias);
-    } else if (part) {  // fp32 slab rows: 4 floats (16 B) per thread-step
-      constexpr int VPR = BN / 4;
-      for (int v = threadIdx.x; v < rows * VPR; v += NTHR) {
-        const int r = v / VPR, c = (v - r * VPR) * 4;
-        const int m = m0 + r0 + r, n = n0 + c;
-        if (m >= M || n >= N) continue;
-        const f32x4 val = Img::ld4(ct, r, c);
-        float* dst = part + (int64_t)m * N + n;
-        if (n + 3 < N && (N & 3) == 0) *reinterpret_cast<f32x4*>(dst) = val;
-        else
-          for (int j = 0; j < 4 && n + j < N; ++j) dst[j] = val[j];
-      }
-    } else if (glu) {  // out col 16p + j = silu(gate col 32p + j) * up col 32p + 16 + j, 8 per thread-step
-      constexpr int VPR = BN / 16;
-      for (int v = threadIdx.x; v < rows * VPR; v += NTHR) {
-        const int r = v / VPR, oc = (v - r * VPR) * 8;
-        const int p = oc >> 4, j = oc & 15;
-        const int cg = 32 * p + j, m = m0 + r0 + r, ng = n0 + cg;
-        if (m >= M || ng >= N) continue;  // N % 32 == 0: the whole gate|up pair exists
-        u16x8 o;
-        float gx[8], ux[8];
-        Img::ld8(ct, r, cg, gx);
-        Img::ld8(ct, r, cg + 16, ux);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float gv = gx[e], uv = ux[e];
-          if (bias) { gv += bf2f(bias[ng + e]); uv += bf2f(bias[ng + 16 + e]); }
-          o[e] = f2bf(silu(gv) * uv);
-        }
-        bf16_t* dst = Y + (int64_t)m * ldy + n0 / 2 + oc;
-        if (ng + 16 + 7 < N && (ldy & 7) == 0) *reinterpret_cast<u16x8*>(dst) = o;
-        else
-          for (int e = 0; e < 8 && ng + 16 + e < N; ++e) dst[e] = o[e];
-      }
-    } else {  // bf16 rows: 8 values (16 B) per thread-step
-      constexpr int VPR = BN / 8;
-      for (int v = threadIdx.x; v < rows * VPR; v += NTHR) {
-        const int r = v / VPR, c = (v - r * VPR) * 8;
-        const int m = m0 + r0 + r, n = n0 + c;
-        if (m >= M || n >= N) continue;
-        u16x8 o;
-        float xv[8];
-        Img::ld8(ct, r, c, xv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float x = xv[e];
-          if (bias && n + e < N) x += bf2f(bias[n + e]);
-          o[e] = f2bf(apply_act(x, act));
-        }
-        bf16_t* dst = Y + (int64_t)m * ldy + n;
-        if (n + 7 < N && (ldy & 7) == 0) *reinterpret_cast<u16x8*>(dst) = o;
-        else
-          for (int e = 0; e < 8 && n + e < N; ++e) dst[e] = o[e];
-      }
-    }
+    img_store_rows<BN, NTHR, R>(ct, rows, r0, m0, n0, M, N, part, Y, ldy, bias, act, glu, qe);
     if (r0 + R < BM) {  // the next chunk overwrites the image
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();

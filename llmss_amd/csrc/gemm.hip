@@ -1356,6 +1356,18 @@ __global__ __launch_bounds__(256) void gemm_f8f8_kernel(const unsigned char* __r
   }
 }
 
+// decode GEMM (csrc/gemm_dec.hip): hint tile bit 1024 (nt_hint bit 18), tile bits = the BN code, depth bits = ring
+// depth code (2 / 3 / 4 / 4 stages per wave), split_hint = K split over the grid (fp32 slabs for the consumer)
+void launch_gemm_dec(int code, int depth, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
+                     const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
+                     int split, hipStream_t st, const QkvEpi* qe);
+bool gemm_dec_bn(int code, int* bn);
+static constexpr int kDecHint = 1024;
+static int dec_split(int M, int N, int K, int split_hint, int64_t ws_bytes) {
+  int s = std::max(1, std::min(split_hint, (K + 63) / 64));
+  if ((int64_t)s * M * N * 4 > ws_bytes) s = 1;
+  return s;
+}
 bool gemm_mid_dims(int tsel, int* bm, int* bn, int* threads);
 void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
@@ -1791,11 +1803,31 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   const int tsel_raw = tsel;
   int s = split_hint;
   const bool f8 = wscale != nullptr;  // fp8-e4m3 weights (W8A16): half the weight bytes of a decode step
+  if (tsel & kDecHint) {  // K split over the waves (gemm_dec.hip), M <= 64, bf16 weights
+    if (f8) throw std::runtime_error("gemm_dec: bf16 weights only");
+    s = dec_split(M, N, K, split_hint, ws_bytes);
+    if (qe && s > 1) throw std::runtime_error("gemm_dec: the QKV epilogue needs an unsplit plan");
+    static constexpr int kDecDepth[4] = {2, 3, 4, 4};
+    float* part = s > 1 ? (float*)workspace : nullptr;
+    launch_gemm_dec(tsel & 15, kDecDepth[(tsel >> 4) & 3], X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, part, M, N, K,
+                    s > 1 ? 0 : act, s > 1 ? 0 : g, s, st, qe);
+    if (s > 1 && partial_out && !g && act == 0) return s;
+    if (s > 1) {
+      const int nout = g ? N / 2 : N;
+      dim3 rgrid(std::min((nout + 255) / 256, 64), M);
+      splitk_reduce_kernel<<<rgrid, 256, 0, st>>>(part, s, M, N, B, Y, ldy, act, g);
+      HIP_CHECK_LAUNCH();
+    }
+    return 0;
+  }
   if (f8 && (tsel & 15) >= 5) tsel = (tsel & ~15) | 1;  // 8-wave and mid tiles are bf16-only
   gemm_tiled_plan(M, N, K, &tsel, &s, g != 0);
   static constexpr int kDepth[4] = {2, 3, 4, 6};
   int ns = kDepth[(tsel >> 4) & 3];  // LDS ring depth (hint bits 4-5); bit 6: default-policy weights
   tsel &= 15;
+  // the ping-pong kernel's zero-page K tail works on 8-element chunks and its LDS-DMA rows need 16-B aligned
+  // strides: anything else runs on the 128x128 tile (tuned hints and C++ callers included, not just linear())
+  if (tsel == 4 && (K % 8 || ldx % 8 || ldw % 8)) tsel = 1;
   if ((tsel == 1 || tsel == 5) && ns > 3) ns = 3;  // 128x128 / 256x128 x 4 stages exceed the 160 KiB LDS
   if ((tsel == 2 || tsel == 6) && ns > 4) ns = 4;
   if (f8 && tsel == 4) tsel = 1;
@@ -1911,6 +1943,11 @@ int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int n
     if (split_hint > 0) s = split_hint;
   } else {
     int tsel = tiled_hint;
+    if (tsel & kDecHint) {
+      if (w_fp8) return 0;  // rejected at launch
+      s = dec_split(M, N, K, split_hint, ws_bytes);
+      return s > 1 ? s : 0;
+    }
     if ((tsel & 128) && !w_fp8 && (tsel & 15) < 5) return 0;  // stream-K combines in-kernel
     if (w_fp8 && ((tsel & 15) == 4 || (tsel & 15) >= 5)) tsel = (tsel & ~15) | 1;
     if ((tsel & 256) && (tsel & 15) != 4) {  // split-K combined in-launch
@@ -1944,6 +1981,14 @@ int launch_gemm_qkv(const void* x, int64_t ldx, const void* w, int64_t ldw, cons
   if (qe.do_rope && (qe.rot % 8 || qe.rot > qe.D || (qe.style == 0 && qe.rot % 16))) return -1;
   if (nt_hint == 0 && split_hint == 0) gemm_tuned_get(M, N, K, false, 3, &nt_hint, &split_hint);
   if (nt_hint & 0xff) return -1;  // streaming kernels have no LDS-staged epilogue
+  if ((nt_hint >> 8) & kDecHint) {  // decode GEMM: unsplit plans only (the epilogue needs finished sums)
+    int bn;
+    if (M > 64 || dec_split(M, N, K, split_hint, ws_bytes) > 1 || !gemm_dec_bn((nt_hint >> 8) & 15, &bn)) return -1;
+    if (qe.do_rope && qe.style == 0 && bn % qe.D) return -1;
+    launch_tiled((const bf16_t*)x, ldx, w, ldw, (const bf16_t*)bias, (bf16_t*)y, ldy, M, N, K, 0, 0, nt_hint >> 8, 1,
+                 workspace, ws_bytes, false, st, nullptr, &qe);
+    return 0;
+  }
   int tsel = nt_hint >> 8, s = split_hint;
   gemm_tiled_plan(M, N, K, &tsel, &s, false);
   if ((tsel & 15) == 4 || (tsel & 128)) return -1;
@@ -1970,7 +2015,9 @@ int launch_gemm_qkv_args(const void* x, int64_t ldx, const void* w, int64_t ldw,
 
 void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk) {
   if (gemm_tuned_get(M, N, K, false, w_fp8 ? 1 : 0, nt, splitk)) {
-    if ((*nt >> 8) & (128 | 256)) {
+    if ((*nt >> 8) & kDecHint) {
+      *splitk = dec_split(M, N, K, *splitk, INT64_MAX);
+    } else if ((*nt >> 8) & (128 | 256)) {
       *splitk = 1;  // stream-K / split-K combine finish their tiles in-kernel: no partial slabs for the consumer
     } else if (*nt >> 8) {  // tiled hint: the split the kernel will really use
       int tsel = *nt >> 8;

@@ -87,6 +87,12 @@ def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, 
     # (64 x 256 tiles of a 12288-column QKV: 48 tiles x 5 = 240 workgroups)
     nk = -(-K // 64)
     out += [((t | d) << 8, s) for t, d in mids for s in (1, 2, 3, 4, 5, 6, 8, 11, 12) if s == 1 or nk // s >= 2]
+    # K split over the waves of a workgroup, wave-private rings (hint bit 1024, csrc/gemm_dec.hip): M <= 64, column
+    # widths 16-64, grids of 64-1024 workgroups (profiles/r6_dec: GPT-2-XL's up projection 9.9 vs 11.2 us)
+    if M <= 64:
+        for code, bn in ((1, 16), (2, 32), (3, 48), (4, 64)):
+            tiles = -(-N // bn)
+            out += [((code | 32 | 1024) << 8, s) for s in (1, 2, 3, 4, 5, 8, 10) if s <= nk and 64 <= tiles * s <= 1024]
     # interleaved ring (hint bit 512, csrc/gemm_mid.hip ILV): >= 3 stages
     if M >= ILV_MIN_M and K % 64 == 0:
         out += [((t | d | 512) << 8, s) for t, d in mids if d >= 16 for s in (1, 2, 3, 4, 5, 6, 8)
@@ -212,6 +218,9 @@ def qkv_epi_candidates(M: int, N: int, K: int, D: int, neox_rope: bool) -> List[
         tiles += [(9, 128, (0,))]
     nk = -(-K // 64)
     out = []
+    if M <= 64:  # the K-split-wave decode kernel (csrc/gemm_dec.hip): unsplit plans only
+        out += [((code | 32 | 1024) << 8, 1) for code, bn in ((1, 16), (2, 32), (3, 48), (4, 64))
+                if not (neox_rope and bn % D)]
     for t, bn, depths in tiles:
         if neox_rope and bn % D:
             continue

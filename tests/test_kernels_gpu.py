@@ -350,6 +350,93 @@ def test_gemm_mid_k_tail_reads_nothing_past_the_operands(tile):
         close(y, R.linear(x.float(), w.float(), None), 2e-2)
 
 
+DEC_BN = {1: 16, 2: 32, 3: 48, 4: 64, 5: 96}  # csrc/gemm_dec.hip tile codes (hint bit 1024 of the tile bits)
+
+
+@pytest.mark.parametrize("code", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("depth", [0, 16, 32])
+@pytest.mark.parametrize("split", [1, 3, 8])
+@pytest.mark.parametrize("M,N,K", [(64, 4800, 1600), (1, 1600, 6400), (17, 2752, 4096), (33, 4096, 1376),
+                                   (64, 200, 64 * 5 + 16), (5, 96, 16), (48, 1600, 1600)])
+def test_gemm_dec(code, depth, split, M, N, K):
+    """The K-split-wave decode GEMM (csrc/gemm_dec.hip) against the fp32 oracle: every column width and ring depth,
+    M = 1..64 (16 / 32 / 64-row variants), ragged N, partial last k-steps (K % 64 = 16, 32) including a
+    single-k-step K, grid splits whose slices leave some waves without k-steps, NaN-filled outputs; bias + GELU,
+    SwiGLU and the fp32 split-K slabs a consumer sums (partial_ok)."""
+    torch.manual_seed(0)
+    x, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
+    b = rnd(N, scale=0.1)
+    hint = (code | depth | 1024) << 8
+    y = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=x.device)
+    close(H.linear(x, w, b, act="gelu_tanh", nt_hint=hint, split_hint=split, out=y),
+          R.linear(x.float(), w.float(), b.float(), act="gelu_tanh"), 2e-2)
+    if N % 32 == 0 and (DEC_BN[code] % 32 == 0 or min(split, -(-K // 64)) > 1):  # SwiGLU in-kernel or in the reduce
+        y = torch.full((M, N // 2), float("nan"), dtype=torch.bfloat16, device=x.device)
+        close(H.linear(x, w, None, glu=True, nt_hint=hint, split_hint=split, out=y),
+              R.linear(x.float(), w.float(), None, glu=True), 2e-2)
+    H._GEMM_WS.get(64 << 20, x.device).fill_(float("nan"))
+    p = H.linear(x, w, b, nt_hint=hint, split_hint=split, partial_ok=True)
+    ref = R.linear(x.float(), w.float(), b.float())
+    if isinstance(p, H.PartialSum):
+        assert split > 1 and p.S == min(split, -(-K // 64))
+        got = p.buf[:p.S * M * N].view(p.S, M, N).sum(0) + b.float()
+        close(got, ref, 2e-2)
+    else:
+        assert split == 1 or -(-K // 64) == 1
+        close(p, ref, 2e-2)
+
+
+@pytest.mark.parametrize("code", [2, 4])
+def test_gemm_dec_k_tail_reads_nothing_past_the_operands(code):
+    """As test_gemm_mid_k_tail_...: operands at the front of NaN-filled buffers, a partial last k-step."""
+    torch.manual_seed(0)
+    M, N, K = 64, 384, 64 * 3 + 16
+    xb = torch.full((M * K + 4096,), float("nan"), dtype=torch.bfloat16, device=dev)
+    wb = torch.full((N * K + 4096,), float("nan"), dtype=torch.bfloat16, device=dev)
+    x, w = xb[: M * K].view(M, K), wb[: N * K].view(N, K)
+    x.copy_(rnd(M, K))
+    w.copy_(rnd(N, K, scale=K ** -0.5))
+    for split in (1, 2):
+        y = H.linear(x, w, None, nt_hint=(code | 16 | 1024) << 8, split_hint=split)
+        close(y, R.linear(x.float(), w.float(), None), 2e-2)
+
+
+@pytest.mark.parametrize("code", [1, 2, 4, 5])
+@pytest.mark.parametrize("style,D,rot,nh,nkv", [("none", 64, 0, 25, 25), ("gptj", 256, 64, 4, 4), ("neox", 64, 64, 8, 1)])
+def test_gemm_dec_qkv_epilogue(code, style, D, rot, nh, nkv):
+    """The decode GEMM with the QKV RoPE / paged-KV-write epilogue (GPT-2-XL's unrotated heads, GPT-J's interleaved
+    partial rotation) == GEMM + rope_cache; neox RoPE on a tile narrower than a head and split plans are refused."""
+    torch.manual_seed(0)
+    T, K, bs, nb = 64, 512, 16, 40
+    N = (nh + 2 * nkv) * D
+    x, w = rnd(T, K), rnd(N, K, scale=K ** -0.5)
+    b = rnd(N, scale=0.1)
+    do_rope = style != "none"
+    st = "gptj" if style == "gptj" else "neox"
+    pos = torch.randint(0, 120, (T,), device=dev)
+    cos, sin = R.rope_tables(128, rot if do_rope else 64, 10000.0, dev)
+    slots = torch.randperm(nb * bs, device=dev)[:T]
+    slots[5] = -1
+    kc1 = torch.full((nb, nkv, bs, D), float("nan"), dtype=torch.bfloat16, device=dev)
+    vc1 = torch.full_like(kc1, float("nan"))
+    hint = (code | 16 | 1024) << 8
+    assert H.linear_qkv(x, w, b, pos, cos, sin, kc1, vc1, slots, nh, nkv, D, rot, st, do_rope, nt_hint=hint,
+                        split_hint=2) is None
+    y = H.linear_qkv(x, w, b, pos, cos, sin, kc1, vc1, slots, nh, nkv, D, rot, st, do_rope, nt_hint=hint,
+                     split_hint=1)
+    if do_rope and st == "neox" and DEC_BN[code] % D:
+        assert y is None
+        return
+    assert y is not None
+    q2 = H.linear(x, w, b)
+    kc2, vc2 = torch.full_like(kc1, float("nan")), torch.full_like(vc1, float("nan"))
+    R.rope_cache(q2, pos, cos, sin, kc2, vc2, slots, nh, nkv, D, rot, st, do_rope=do_rope)
+    close(y, q2, 1e-2)
+    for a, r in ((kc1, kc2), (vc1, vc2)):
+        assert torch.equal(a.isnan(), r.isnan())
+        close(a.nan_to_num(0), r.nan_to_num(0), 1e-2)
+
+
 @pytest.mark.parametrize("M", [1, 8, 64, 100])
 def test_gemm_fp8(M):
     torch.manual_seed(0)
