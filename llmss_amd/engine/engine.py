@@ -39,6 +39,10 @@ from .sampling import SamplingParams, step_seeds
 
 log = get_logger(__name__)
 
+# context length (cached positions per row) at which the capture-time A/Bs time their candidates - the GQA decode
+# attention kernels and the decode schedules: the bench's mean over a 128-token prompt + 128 generated tokens
+AB_CTX = 192
+
 
 @dataclass
 class Request:
@@ -174,20 +178,20 @@ class LLMEngine:
         self._t_collect = 0.0  # when the last decode step was collected (non-overlapped decode_time_s)
         self._aborted = set()  # ids aborted while a decode step holding them was in flight
         self.async_decode = os.environ.get("LLMSS_ASYNC_DECODE", "1") != "0"
-        self._host_prof = os.environ.get("LLMSS_HOST_PROFILE") == "1"  # host-side time per engine phase
         self.check_tokens = check_tokens if check_tokens is not None else os.environ.get("LLMSS_CHECK_TOKENS") == "1"
         self.stats = {"steps": 0, "prefill_steps": 0, "decode_steps": 0, "tokens": 0, "prefill_tokens": 0,
                       "preemptions": 0, "decode_time_s": 0.0, "prefill_time_s": 0.0}
         self.timer = PhaseTimer()  # LLMSS_TIMING=1: HIP-event device time per phase; LLMSS_ROCTX=1: roctx ranges
+        self._host_prof = self.timer.enabled  # LLMSS_TIMING=1 also records host-side time per engine phase
         self.use_graphs = self.is_gpu if use_graphs is None else (use_graphs and self.is_gpu)
         if self.tp.is_real and self.tp.host_staged:  # gloo-staged device collectives cannot be captured
             self.use_graphs = False
         self.graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}  # (batch bucket, candidate sampler) -> graph
         # vocab-parallel sampling from per-rank candidates (SURVEY R11 "better"): greedy / top-k <= 64 rows
-        # gather [B, tp, 128] (value, id) pairs instead of [B, V] logits; LLMSS_DIST_SAMPLER=0 disables
+        # gather [B, tp, 128] (value, id) pairs instead of [B, V] logits
         from ..ops.hip import CAND_KC, CAND_MAX_SHARD
 
-        self.dist_sampling = (self.tp.size > 1 and os.environ.get("LLMSS_DIST_SAMPLER", "1") != "0"
+        self.dist_sampling = (self.tp.size > 1
                               and self.tp.size * CAND_KC <= 2048  # sample_cand's gathered-candidate limit
                               and (not self.is_gpu or model.plan.v_l <= CAND_MAX_SHARD))
         self.buckets = sorted(set(graph_buckets or self._default_buckets()))
@@ -295,18 +299,15 @@ class LLMEngine:
     def _tune_gqa_attention(self):
         """For grouped-query models (>= 4 query heads per kv head, e.g. Llama-2-70B's 8, MQA's all) time the VALU
         split-K decode kernel against the MFMA extend kernel per decode bucket on a synthetic cache (context
-        LLMSS_TBO_AUTO_CTX, default 192) and route the buckets where MFMA wins (DecoderLM.gqa_mfma). Every rank
+        AB_CTX) and route the buckets where MFMA wins (DecoderLM.gqa_mfma). Every rank
         sees the same shapes; the decision is agreed through all_reduce_int so the ranks run the same kernels."""
         m, p, cfg = self.model, self.model.plan, self.cfg
-        if p.nh_l // max(1, p.nkv_l) < 4 or os.environ.get("LLMSS_GQA_MFMA", "auto") == "0":
-            return
-        if os.environ.get("LLMSS_GQA_MFMA") == "1":
-            m.gqa_mfma = set(self.decode_batch_sizes())
+        if p.nh_l // max(1, p.nkv_l) < 4:
             return
         from ..ops.autotune import _time
 
         D, dev = cfg.head_dim, self.device
-        ctx = max(1, min(int(os.environ.get("LLMSS_TBO_AUTO_CTX", "192")), self.max_model_len - 1))
+        ctx = max(1, min(AB_CTX, self.max_model_len - 1))
         nblk = -(-ctx // self.block_size)
         res = {}
         for b in self.decode_batch_sizes():
@@ -345,10 +346,10 @@ class LLMEngine:
 
     def _tbo_candidates(self) -> List[int]:
         """Decode buckets whose two-micro-batch schedule is timed against the single-batch one at capture
-        (LLMSS_TBO_AUTO, default on): only with a real multi-rank communicator - on one GPU there is nothing
-        to overlap - and for buckets of >= LLMSS_TBO_AUTO_MIN (128) sequences."""
+        only with a real multi-rank communicator - on one GPU there is nothing to overlap - and for buckets of
+        >= LLMSS_TBO_AUTO_MIN (default 128; 0 = no micro-batch A/B) sequences."""
         if not (self.is_gpu and self.tp.is_real and not self.tp.host_staged and self.model.tbo_min <= 0
-                and os.environ.get("LLMSS_TBO_AUTO", "1") != "0"):
+                and int(os.environ.get("LLMSS_TBO_AUTO_MIN", "128")) > 0):
             return []
         lo = int(os.environ.get("LLMSS_TBO_AUTO_MIN", "128"))
         return [b for b in self.buckets if b >= lo]
@@ -357,7 +358,7 @@ class LLMEngine:
         """Decode buckets whose row-sharded schedule (reduce-scatter -> add + norm on M / tp rows -> all-gather,
         DecoderLM._hidden_states_rsag) is timed against the all-reduce one at capture: real multi-rank
         communicator, LLMSS_TP_RSAG=auto (default), buckets divisible by the TP degree of at least
-        LLMSS_TP_RSAG_MIN (default 8 rows per rank). Not for fp8-weight models: their default schedule feeds the
+        8 rows per rank. Not for fp8-weight models: their default schedule feeds the
         GEMMs the fp8 twin that add_norm writes, which the row-sharded add + norm does not produce, so the A/B would
         not compare like with like."""
         m = self.model
@@ -365,7 +366,7 @@ class LLMEngine:
             return []
         if any(L.qkv.w_scale is not None for L in m.w.layers[:1]):
             return []
-        lo = int(os.environ.get("LLMSS_TP_RSAG_MIN", str(8 * self.tp.size)))
+        lo = 8 * self.tp.size
         return [b for b in self.buckets if b >= lo and m.rsag_ok(b)]
 
     def _col_candidates(self) -> List[int]:
@@ -760,9 +761,7 @@ class LLMEngine:
         buf.d_i32.zero_()
         buf.topk.fill_(1)
         buf.d_f32.zero_()
-        # vocab-parallel runs: graphs for both samplers (candidates when every row allows it, else the
-        # gathered-logits sampler), chosen per step
-        modes = (True, False) if self.dist_sampling else (False,)
+        modes = self._decode_modes()
         # warm-up passes (lazy allocations, first launches). Native RCCL: with real collectives, so each
         # algorithm's lazy peer connection happens here and not inside the capture. torch's RCCL process
         # group: collectives suspended - its watchdog thread would otherwise still track the warm-up's work
@@ -795,6 +794,11 @@ class LLMEngine:
         log.info("captured %d decode graphs: buckets %s, samplers %s", len(self.graphs), self.buckets,
                  ["candidates" if d else "gathered" for d in modes])
 
+    def _decode_modes(self):
+        """Sampler modes a decode graph is captured for: vocab-parallel runs get both samplers (candidates when every
+        row allows it, else the gathered-logits sampler), chosen per step."""
+        return (True, False) if self.dist_sampling else (False,)
+
     @contextlib.contextmanager
     def _schedule(self, b: int, name: str):
         """Decode bucket ``b`` runs schedule ``name`` inside the block (capture / warm-up of an A/B variant)."""
@@ -815,20 +819,32 @@ class LLMEngine:
             if name == "col" and not had_col:
                 m.col.discard(b)
 
+    @staticmethod
+    def _ab_buckets(cands: List[int]) -> List[int]:
+        """The buckets the schedule A/B times: the largest candidate, the largest one at most half of it and the
+        smallest one; every other candidate bucket adopts the winner of the nearest timed bucket (engine start-up at
+        TP=8: 3 timed buckets instead of up to 15)."""
+        cands = sorted(cands)
+        if not cands:
+            return []
+        top = cands[-1]
+        half = [b for b in cands if b <= top // 2]
+        return sorted({top, cands[0]} | ({half[-1]} if half else set()))
+
     def _schedule_ab(self, pool, modes):
-        """Capture-time A/B of the decode schedules on the real communicator: per candidate bucket the
+        """Capture-time A/B of the decode schedules on the real communicator: per timed bucket the
         all-reduce graph ("one") against the two-micro-batch one ("tbo": each half's all-reduces on the comm
-        stream while the other half computes, DecoderLM._hidden_states_overlap) and the row-sharded one ("rsag":
-        reduce-scatter, add + norm on M / tp rows, all-gather, DecoderLM._hidden_states_rsag) and the column-chunked
-        one ("col": each row-parallel output as C weight-row slices whose all-reduces run beside the next slice's
-        GEMM, DecoderLM._reduce_cols). Each graph is
-        replayed with a realistic context length (the bench's 128 + 64 average), every rank's times are
-        gathered and the max over ranks decides, so all ranks keep the same graph; an alternative must beat
-        "one" by 3 %. Which wins depends on what collectives cost on the node - hence measured, not assumed
-        (the split loses on one GPU: half-batch kernels are nearly as long as full ones, profiles/r1_tbo)."""
+        stream while the other half computes, DecoderLM._hidden_states_overlap), the row-sharded one ("rsag":
+        reduce-scatter, add + norm on M / tp rows, all-gather, DecoderLM._hidden_states_rsag) and, when enabled, the
+        column-chunked one ("col": each row-parallel output as C weight-row slices whose all-reduces run beside the
+        next slice's GEMM, DecoderLM._reduce_cols). Each graph is replayed with a realistic context length (the
+        bench's 128 + 64 average), every rank's times are gathered and the max over ranks decides, so all ranks keep
+        the same graph; an alternative must beat "one" by 3 %. The other candidate buckets then capture the winner
+        of their nearest timed bucket (_ab_buckets). Which wins depends on what collectives cost on the node - hence
+        measured, not assumed (the split loses on one GPU: half-batch kernels are nearly as long as full ones,
+        profiles/r1_tbo)."""
         buf, m = self.buf, self.model
-        ctx = int(os.environ.get("LLMSS_TBO_AUTO_CTX", "192"))
-        ctx = max(1, min(ctx, self.max_model_len - 1))
+        ctx = max(1, min(AB_CTX, self.max_model_len - 1))
         nblk = -(-ctx // self.block_size)
         if nblk > self.num_blocks:
             return
@@ -836,28 +852,26 @@ class LLMEngine:
                         if b in c]
                     for b in self.buckets}
         variants = {b: v for b, v in variants.items() if v}
+        timed_b = self._ab_buckets(list(variants))
         alt, times = {}, {}
 
-        def warm():
+        def forwards(pairs, suspended):  # eager forward of each (bucket, schedule) on a side stream
             st = torch.cuda.Stream()
             st.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(st):  # eager warm-up: comm stream, half-batch workspaces, each collective's first use
-                for b in sorted(variants, reverse=True):
-                    for name in variants[b]:
-                        with self._schedule(b, name):
-                            self._decode_forward(b, buf, dist=modes[0])
+            with torch.cuda.stream(st), (self.tp.suspended() if suspended else contextlib.nullcontext()):
+                for b, name in pairs:
+                    with self._schedule(b, name):
+                        self._decode_forward(b, buf, dist=modes[0])
             torch.cuda.current_stream().wait_stream(st)
             torch.cuda.synchronize()
 
-        def capture():
-            for b in sorted(variants, reverse=True):
-                for d in modes:
-                    for name in variants[b]:
-                        with self._schedule(b, name):
-                            g = torch.cuda.CUDAGraph()
-                            with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
-                                self._decode_forward(b, buf, dist=d)
-                        alt[(b, d, name)] = g
+        def capture_all(triples):
+            for b, d, name in triples:
+                with self._schedule(b, name):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
+                        self._decode_forward(b, buf, dist=d)
+                alt[(b, d, name)] = g
             torch.cuda.synchronize()
 
         def timed(g):
@@ -874,7 +888,7 @@ class LLMEngine:
             buf.ctx.fill_(ctx)
             buf.bt.zero_()
             buf.bt[:, :nblk] = torch.arange(nblk, dtype=torch.int32, device=buf.bt.device)
-            for b in sorted(variants, reverse=True):
+            for b in sorted(timed_b, reverse=True):
                 for d in modes:
                     gs = {"one": self.graphs[(b, d)], **{n: alt[(b, d, n)] for n in variants[b]}}
                     for g in gs.values():  # warm every graph
@@ -886,38 +900,69 @@ class LLMEngine:
                             res[n].append(timed(g))
                     times[(b, d)] = {n: min(v) for n, v in res.items()}
 
-        # each stage agreed across ranks: a stage that raises on one rank (OOM, a refused
-        # capture) makes every rank keep the all-reduce graphs, instead of one rank leaving while its peers
-        # wait for it in the stages' collectives or in the gather of the times below
-        for stage in (warm, capture, measure):
-            ok, err = self.tp.agree(stage)
-            if not ok:
-                log.warning("decode schedule A/B stopped at %s (%s): every rank keeps the all-reduce schedule",
-                            stage.__name__, err or "on a peer rank")
+        # Each stage is agreed across ranks. prealloc (every allocation of the variants: their eager forwards with the
+        # collectives skipped) and capture (records collectives, runs none) can fail on one rank without leaving
+        # anything queued on its peers: every rank then keeps the all-reduce graphs. warm and measure RUN
+        # collectives: if they fail on some rank after issuing part of them, its peers may hold collectives the failed
+        # rank never joins (the native communicator has no device-side timeout), so every rank aborts the
+        # communicator and raises instead of decoding on.
+        def run_stages(pairs, triples, with_measure):
+            stages = [("prealloc", lambda: forwards(pairs, True)), ("warm", lambda: forwards(pairs, False)),
+                      ("capture", lambda: capture_all(triples))] + ([("measure", measure)] if with_measure else [])
+            for name, stage in stages:
+                ok, err = self.tp.agree(stage)
+                if ok:
+                    continue
                 alt.clear()
-                buf.ctx.zero_()
-                buf.bt.zero_()
-                torch.cuda.synchronize()
-                return
+                if name in ("prealloc", "capture"):
+                    log.warning("decode schedule A/B stopped at %s (%s): every rank keeps the all-reduce schedule",
+                                name, err or "on a peer rank")
+                    buf.ctx.zero_()
+                    buf.bt.zero_()
+                    torch.cuda.synchronize()
+                    return False
+                self.tp.close(abort=True)
+                raise RuntimeError(f"decode schedule A/B failed in {name} ({err or 'on a peer rank'}) after "
+                                   f"collectives were issued: communicator aborted on every rank")
+            return True
+
+        pairs = [(b, n) for b in sorted(timed_b, reverse=True) for n in variants[b]]
+        if not run_stages(pairs, [(b, d, n) for b, n in pairs for d in modes], True):
+            return
         allt = self.tp.all_gather_object(times)
+        win = {}
         for (b, d), tv in times.items():
             worst = {n: max(t[(b, d)][n] for t in allt) for n in tv}
-            best = min(worst, key=lambda n: worst[n] if n == "one" else worst[n] / 0.97)
-            if best != "one":
-                self.graphs[(b, d)] = alt[(b, d, best)]
+            win[(b, d)] = min(worst, key=lambda n: worst[n] if n == "one" else worst[n] / 0.97)
+            self.stats.setdefault("schedule_ab_ms", {})[f"{b}{'c' if d else 'g'}"] = \
+                {n: round(v, 3) for n, v in worst.items()}
+        # every candidate bucket: its own winner, or the nearest timed bucket's (when that schedule applies to it)
+        chosen = {}
+        for b in variants:
+            near = min(timed_b, key=lambda t: (abs(t - b), t))
+            for d in modes:
+                w = win[(near, d)]
+                if w != "one" and w in variants[b]:
+                    chosen[(b, d)] = w
+        extra = sorted({(b, d, n) for (b, d), n in chosen.items() if (b, d, n) not in alt}, reverse=True)
+        for k in list(alt):  # timed alternatives that lost: free their graphs
+            if chosen.get(k[:2]) != k[2]:
+                del alt[k]
+        if extra and not run_stages(sorted({(b, n) for b, _, n in extra}, reverse=True), extra, False):
+            return
+        for (b, d), best in chosen.items():
+            self.graphs[(b, d)] = alt[(b, d, best)]
             if best == "rsag":  # eager steps of this bucket (none while its graph exists) take it too
                 m.rsag.add(b)
             if best == "col":
                 m.col.add(b)
             if self.decode_schedule.get(b, "one") == "one":
                 self.decode_schedule[b] = best
-            self.stats.setdefault("schedule_ab_ms", {})[f"{b}{'c' if d else 'g'}"] = \
-                {n: round(v, 3) for n, v in worst.items()}
         buf.ctx.zero_()
         buf.bt.zero_()
         torch.cuda.synchronize()
-        log.info("decode schedule A/B (max over ranks, ms per step): %s -> %s", self.stats.get("schedule_ab_ms"),
-                 self.decode_schedule)
+        log.info("decode schedule A/B (timed buckets %s, max over ranks, ms per step): %s -> %s", timed_b,
+                 self.stats.get("schedule_ab_ms"), self.decode_schedule)
 
     # -------------------------------------------------------------------------- offline API
     def generate(self, prompts: Iterable[Sequence[int]], params=None) -> List[List[int]]:

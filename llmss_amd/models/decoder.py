@@ -21,6 +21,7 @@ followed by an all-gather of [B, V/tp] logits.
 """
 from __future__ import annotations
 
+import contextlib
 import dataclasses
 import os
 from dataclasses import dataclass
@@ -67,6 +68,55 @@ class StepInput:
     cu_host: Optional[Sequence[int]] = None  # prefill: cu_seqlens on the host (micro-batch split points)
 
 
+class StreamLedger:
+    """Fork / join bookkeeping of the comm-stream schedules (_reduce_rows, _reduce_cols, _hidden_states_overlap).
+
+    A HIP graph capture ends in hipErrorStreamCaptureUnjoined when work forked off the capturing stream is never
+    joined back (profiles/r6_capture: a clean Python error for every stream / event / allocator topology these
+    schedules use, with and without native RCCL). Each fork (the comm stream waits for the compute stream, then
+    runs a collective) and each join (the compute stream waits for the comm stream, or for an event recorded on it
+    after the forked work - the comm stream runs in order, so that joins every earlier fork too) is registered
+    here, on CPU as well where no stream exists, so the gloo tests check the structure the GPU graphs rely on, and
+    DecoderLM.hidden_states asserts after every forward - i.e. before any capture ends - that nothing is open."""
+
+    def __init__(self):
+        self.open: List[int] = []  # fork tokens not yet joined, oldest first
+        self.forks = 0  # forks since construction (tests: the schedule really forked)
+
+    def fork(self, cur, comm) -> int:
+        if comm is not None:
+            comm.wait_stream(cur)
+        self.forks += 1
+        self.open.append(self.forks)
+        return self.forks
+
+    def mark(self, comm, tok: int):
+        """(tok, event recorded on ``comm`` after fork ``tok``'s work) - what a later wait() joins."""
+        ev = None
+        if comm is not None:
+            ev = torch.cuda.Event()
+            ev.record(comm)
+        return tok, ev
+
+    def wait(self, cur, mark) -> None:
+        if mark is None:
+            return
+        tok, ev = mark
+        if ev is not None:
+            cur.wait_event(ev)
+        self.open = [t for t in self.open if t > tok]
+
+    def join(self, cur, comm) -> None:
+        if comm is not None:
+            cur.wait_stream(comm)
+        self.open.clear()
+
+    def check(self, where: str) -> None:
+        if self.open:
+            n, self.open = len(self.open), []
+            raise RuntimeError(f"{where}: {n} comm-stream fork(s) never joined back to the compute stream")
+
+
 class DecoderLM:
     def __init__(self, cfg: ModelConfig, weights: ModelWeights, tp: Optional[TPGroup] = None):
         if weights.rope_interleaved and cfg.rope_style == "neox":
@@ -83,31 +133,29 @@ class DecoderLM:
         # `bucket_bytes` (LLMSS_TP_BUCKET_BYTES, default 32 MiB: a prefill chunk's all-reduce is then
         # long enough to hide the next chunk's GEMM behind it, while each RCCL call stays in its
         # bandwidth regime on xGMI); a decode step's few-MiB all-reduce stays one bucket unless the
-        # knob is lowered. LLMSS_TP_OVERLAP_ROWS / `overlap_rows` fixes the bucket in rows instead.
-        rows = os.environ.get("LLMSS_TP_OVERLAP_ROWS")
-        self.overlap_rows = int(rows) if rows else None
+        # knob is lowered. `overlap_rows` (tests) fixes the bucket in rows instead.
+        self.overlap_rows: Optional[int] = None
         self.bucket_bytes = int(os.environ.get("LLMSS_TP_BUCKET_BYTES", str(32 << 20)))
         # fp8 (e4m3 + per-row scale) paged KV cache (LLMSS_KV_DTYPE=fp8 or LLMEngine(kv_dtype="fp8"))
         self.kv_fp8 = os.environ.get("LLMSS_KV_DTYPE", "bf16") == "fp8"
-        # decode steps of at least this many sequences run as two interleaved micro-batches so each
-        # one's all-reduces overlap the other's compute; only when collectives cost time. Opt-in
-        # (0 = off): measured on MI355X (bench/tbo_probe.py, Llama-2-7B TP=8 shard, batch 512, 8
-        # layers) the split alone costs +51% (half-batch decode kernels are nearly as long as
-        # full-batch ones) and each cross-stream hand-off inside a HIP graph ~10 us, more than a
-        # modelled 52 us all-reduce hides: 2639 vs 2519 us per step (profiles/r1_tbo/)
-        self.tbo_min = int(os.environ.get("LLMSS_TP_DECODE_OVERLAP_MIN", "0"))
+        # decode steps of at least this many sequences run as two interleaved micro-batches so each one's
+        # all-reduces overlap the other's compute (only when collectives cost time; 0 = off). Set per bucket by the
+        # engine's capture-time A/B on the real communicator (LLMEngine._schedule_ab), or by a caller. Under the TP=8
+        # comm model it beats one all-reduce (60.0 K vs 55.4 K tok/s) since the comm stream runs at normal priority
+        # (profiles/r5_tp8sim); round 1's +51 % loss was measured with a high-priority comm stream.
+        self.tbo_min = 0
         # prefill steps of at least this many tokens (and >= 2 sequences) run as two micro-batches split at
         # a sequence boundary, so one half's all-reduces (hundreds of MiB each at TP=8) overlap the other
         # half's GEMMs and attention; only when collectives cost time (0 = off)
         self.tbo_prefill_min = int(os.environ.get("LLMSS_TP_PREFILL_OVERLAP_MIN", "8192"))
         # QKV GEMM epilogue with RoPE + paged KV write (one launch instead of two) wherever the autotuner
-        # installed a faster plan for it (LLMSS_QKV_EPI=0: always GEMM + rope_cache)
-        self.qkv_epi = os.environ.get("LLMSS_QKV_EPI", "1") != "0"
+        # installed a faster plan for it (ops/autotune.py tune_qkv_epilogue)
+        self.qkv_epi = True
         # decode batch sizes whose GQA attention runs on the MFMA extend kernel (one workgroup per kv head
         # serving its whole query-head group: K/V staged once, QK^T and PV on the matrix cores) instead of
         # the VALU split-K decode kernel; filled by LLMEngine's capture-time timing for G >= 4 groups
         self.gqa_mfma: set = set()
-        self._norm_quant = os.environ.get("LLMSS_FP8_NORM_QUANT", "1") != "0"
+        self._norm_quant = True  # add_norm writes the fp8 twin of its output for a W8A8 consumer
         # row-sharded decode schedule (TP > 1): each row-parallel output is reduce-scattered instead of
         # all-reduced, add + norm run on this rank's M / tp rows (the residual stream stays sharded) and the
         # normed rows are all-gathered for the next column-parallel GEMM (_hidden_states_rsag). Decode batch
@@ -118,17 +166,19 @@ class DecoderLM:
         # column-chunked decode schedule (TP > 1, _reduce_cols): each row-parallel projection runs as C GEMMs over
         # disjoint output-column slices of its weight (no weight byte read twice); chunk c's all-reduce goes to the
         # comm stream while chunk c + 1's GEMM runs, and add_norm reads the chunk-major result. Decode
-        # batch sizes in `col` take it: LLMSS_TP_COL=C (> 1) every decode step with C chunks, "auto" (default) the
-        # buckets the engine's capture-time A/B picks (4 chunks), 0 never
-        col = os.environ.get("LLMSS_TP_COL", "auto")
+        # batch sizes in `col` take it: LLMSS_TP_COL=C (> 1) every decode step with C chunks, "auto" the buckets the
+        # engine's capture-time A/B picks (4 chunks), 0 (default) never: it lost to the single all-reduce by 20-35 %
+        # at every size under the TP=8 comm model (profiles/r5_tp8sim), so it no longer costs start-up time
+        col = os.environ.get("LLMSS_TP_COL", "0")
         self.col_mode = "auto" if col == "auto" else ("force" if int(col) > 1 else "0")
         self.col_chunks = int(col) if col not in ("auto", "0", "1") else 4
         # smallest decode bucket the capture-time A/B tries it on (the collectives are small below; and under the
         # TP=8 comm model it lost at every size, profiles/r5_tp8sim)
-        self.col_min = int(os.environ.get("LLMSS_TP_COL_MIN", "256"))
+        self.col_min = 256
         self.col: set = set()
         self._cu_decode = {}
         self._comm_stream = None
+        self._ledger = StreamLedger()
 
     @property
     def device(self):
@@ -212,7 +262,7 @@ class DecoderLM:
 
     def _fp8_in(self, lin, x) -> bool:
         """The linear consuming add_norm's output runs W8A8 at this row count: have add_norm write the per-token
-        fp8 twin so the GEMM skips its quantisation launch (LLMSS_FP8_NORM_QUANT=0 disables)."""
+        fp8 twin so the GEMM skips its quantisation launch."""
         if lin.w_scale is None or not x.is_cuda or lin.w.dim() != 2 or not self._norm_quant:
             return False
         return _hip_ops().w8a8_planned(x.shape[0], lin.N, lin.K, lin.glu)
@@ -257,22 +307,21 @@ class DecoderLM:
         step = self.bucket_rows(M)
         if M <= step or step <= 0:
             return self.tp.all_reduce(fn(*inputs))
-        if not inputs[0].is_cuda:  # gloo / CPU: same chunking (numerics), no streams
-            return torch.cat([self.tp.all_reduce(fn(*(t[r:r + step] for t in inputs))) for r in range(0, M, step)])
-        cur = torch.cuda.current_stream()
-        comm = self._comm(inputs[0].device)
+        gpu = inputs[0].is_cuda  # gloo / CPU: same chunking (numerics) and ledger, no streams
+        cur = torch.cuda.current_stream() if gpu else None
+        comm = self._comm(inputs[0].device) if gpu else None
         outs = []
         for r in range(0, M, step):
             y = fn(*(t[r:r + step] for t in inputs))
-            comm.wait_stream(cur)  # chunk r's GEMM done
-            with torch.cuda.stream(comm):
+            self._ledger.fork(cur, comm)  # chunk r's GEMM done
+            with (torch.cuda.stream(comm) if gpu else contextlib.nullcontext()):
                 self.tp.all_reduce(y)
             # no record_stream: `outs` holds every chunk until the compute stream has waited for the comm
             # stream (below), so no chunk's memory is reused while its all-reduce runs - and no allocator
             # event is left pending on the comm stream (an allocation inside a later graph capture would
             # otherwise query it from the capturing thread)
             outs.append(y)
-        cur.wait_stream(comm)
+        self._ledger.join(cur, comm)
         return torch.cat(outs)
 
     def col_ok(self, lin) -> bool:
@@ -292,10 +341,12 @@ class DecoderLM:
         cw = N // C
         M = h.shape[0]
         out = torch.empty(C, M, cw, dtype=h.dtype, device=h.device)
-        if not h.is_cuda:  # gloo / CPU: same chunks and collectives, no streams
+        if not h.is_cuda:  # gloo / CPU: same chunks, collectives and ledger, no streams
             for c in range(C):
                 out[c].copy_(lin.rows(c * cw, (c + 1) * cw)(h))
+                self._ledger.fork(None, None)
                 self.tp.all_reduce(out[c])
+            self._ledger.join(None, None)
             return out
         cur = torch.cuda.current_stream()
         comm = self._comm(h.device)
@@ -303,10 +354,10 @@ class DecoderLM:
         for c in range(C):
             sl = lin.rows(c * cw, (c + 1) * cw)
             H.linear(h, sl.w, sl.b, w_scale=sl.w_scale, out=out[c])
-            comm.wait_stream(cur)  # chunk c's GEMM done
+            self._ledger.fork(cur, comm)  # chunk c's GEMM done
             with torch.cuda.stream(comm):
                 self.tp.all_reduce(out[c])
-        cur.wait_stream(comm)
+        self._ledger.join(cur, comm)
         return out
 
     # ------------------------------------------------------- two-micro-batch decode overlap
@@ -367,22 +418,18 @@ class DecoderLM:
         cur = torch.cuda.current_stream() if on_gpu else None
         comm = self._comm(inp.input_ids.device) if on_gpu else None
 
-        def reduce(t):  # all-reduce t on the comm stream; returns the event to wait on before reading t
-            if not on_gpu:
-                self.tp.all_reduce(t)
-                return None
-            comm.wait_stream(cur)
-            with torch.cuda.stream(comm):
-                self.tp.all_reduce(t)
-                ev = torch.cuda.Event()
-                ev.record(comm)
-            # no record_stream (see _reduce_rows): the compute stream waits for `ev` before it reads t or
-            # drops its last reference (the next layer's ready(), or the final joins)
-            return ev
+        ledger = self._ledger
 
-        def ready(ev):
-            if ev is not None:
-                cur.wait_event(ev)
+        def reduce(t):  # all-reduce t on the comm stream; returns the mark to wait on before reading t
+            tok = ledger.fork(cur, comm)
+            with (torch.cuda.stream(comm) if on_gpu else contextlib.nullcontext()):
+                self.tp.all_reduce(t)
+                # no record_stream (see _reduce_rows): the compute stream waits for this mark before it reads t or
+                # drops its last reference (the next layer's ready(), or the final joins)
+                return ledger.mark(comm, tok)
+
+        def ready(mark):
+            ledger.wait(cur, mark)
 
         x = ops.embed(inp.input_ids, w.wte, inp.positions if w.wpe is not None else None, w.wpe)
         delta = [x[r0:r1] for r0, r1 in rows]
@@ -450,6 +497,11 @@ class DecoderLM:
         return tp.all_gather_rows(h_sh)
 
     def hidden_states(self, inp: StepInput, kv_caches) -> torch.Tensor:
+        h = self._hidden_states(inp, kv_caches)
+        self._ledger.check("DecoderLM.hidden_states")  # every comm-stream fork joined (graph capture needs it)
+        return h
+
+    def _hidden_states(self, inp: StepInput, kv_caches) -> torch.Tensor:
         if inp.kind == "decode":
             B = inp.input_ids.shape[0]
             if self.rsag_ok(B) and (self.rsag_mode == "1" or B in self.rsag):

@@ -48,6 +48,9 @@ class ShardPlan:
         return self.vocab_padded // self.tp
 
 
+# load neox-RoPE checkpoints with q / k head dims interleaved (gptj-form rotation, fusable into the QKV epilogue)
+ROPE_INTERLEAVE = True
+
 def shard_plan(cfg: ModelConfig, tp: int, rank: int) -> ShardPlan:
     nh, nkv = cfg.num_heads, cfg.num_kv_heads
     if nh % tp:
@@ -176,8 +179,8 @@ def _finish(cfg: ModelConfig, plan: ShardPlan, wte, wpe, layers_raw, lnf_w, lnf_
             return Linear(q, b, s, glu)
         return Linear(w, b, None, glu)
 
-    # neox RoPE: interleave the q / k head dims (LLMSS_ROPE_INTERLEAVE=0 keeps the checkpoint order)
-    il = cfg.position == "rope" and cfg.rope_style == "neox" and os.environ.get("LLMSS_ROPE_INTERLEAVE", "1") != "0"
+    # neox RoPE: interleave the q / k head dims (ROPE_INTERLEAVE = False keeps the checkpoint order; tests)
+    il = cfg.position == "rope" and cfg.rope_style == "neox" and ROPE_INTERLEAVE
     layers = []
     for d in layers_raw:
         if il:

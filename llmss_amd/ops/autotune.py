@@ -28,6 +28,7 @@ log = get_logger(__name__)
 
 _SLAB_READ_BPS = 4.0e12  # consumer-side fp32 partial reads (add_norm / rope), bytes/s
 ILV_MIN_M = 128  # smallest M whose plans include the interleaved ring (profiles/r4_gemm/sweep512_ilv.log)
+FINALISTS = 6  # candidates re-timed at full length after the short first round
 
 
 @dataclass(frozen=True)
@@ -162,25 +163,32 @@ def tune_shape(M: int, shape: GemmShape, device, weight_budget: int = 600 << 20,
             return r
         return f
 
-    def cost(nt, s):
+    def cost(nt, s, n=iters):
         f = run(nt, s)
         r = f(0)
         slabs = r.S if isinstance(r, H.PartialSum) else 0
         for i in range(2):
             f(i)
         torch.cuda.synchronize(device)
-        t = _time(f, iters)
+        t = _time(f, n)
         return t + (slabs * M * N * 4 / _SLAB_READ_BPS * 1e6 if slabs else 0.0)
 
     default = cost(0, 0)
     best = (0, 0, default)
     if cands is None:
         cands = candidates(M, N, K, shape.glu, shape.fp8)
+    # two rounds (engine start-up time): every candidate on a short graph (4 calls), then the
+    # FINALISTS fastest of them again at the full `iters` - a short graph ranks plans that differ by > ~3 % the
+    # same way, and the final choice is made on the long timings only
+    quick = []
     for nt, s in cands:
         try:
-            t = cost(nt, s)
+            quick.append((cost(nt, s, 4), nt, s))
         except (ValueError, RuntimeError):  # config rejected by host-side validation
             continue
+    quick.sort()
+    for _, nt, s in quick[:FINALISTS]:
+        t = cost(nt, s)
         if t < best[2] * 0.98:  # prefer the static plan unless a candidate is clearly faster
             best = (nt, s, t)
     del ws
@@ -313,6 +321,20 @@ def _reinstall_qkv(lib, model, results):
             lib.gemm_tuned_set(M, L.qkv.N, L.qkv.K, False, 3, plan[0], plan[1])
 
 
+def representatives(ms: Sequence[int]) -> Dict[int, int]:
+    """Row count whose tuned plan each decode size uses: every size up to 64 is tuned itself (the K-split-wave
+    kernel's 16 / 32 / 64-row variants and the streaming kernels change plans there); above 64 every other size,
+    counted down from the largest, and the sizes in between take the plan of the next larger tuned size (a plan is
+    valid at any M; the 96-512-row buckets of a TP=8 engine differ by <= 25 % in M). Halves the tuning time of a
+    TP=8 engine's large buckets (VERDICT r5 weak #8)."""
+    ms = sorted(set(int(m) for m in ms))
+    out = {m: m for m in ms if m <= 64}
+    big = [m for m in ms if m > 64][::-1]
+    for i, m in enumerate(big):
+        out[m] = m if i % 2 == 0 else big[i - 1]
+    return out
+
+
 def tune_model(model, ms: Sequence[int], native=None) -> Dict[Tuple[str, int], Tuple[int, int, float, float]]:
     """Tune every (shape, M) pair and install the winners in the native plan table."""
     from .. import _native
@@ -322,26 +344,27 @@ def tune_model(model, ms: Sequence[int], native=None) -> Dict[Tuple[str, int], T
     t0 = time.perf_counter()
     res = {}
     done = _DONE
+    rep = representatives(ms)
     for name, shp in model_shapes(model).items():
         for M in sorted(set(int(m) for m in ms)):
             if name.endswith("_col") and getattr(model, "col_mode", "0") != "force" and M < model.col_min:
                 continue  # column chunks run only in the buckets the capture-time A/B tries them on
-            key = (M, shp, str(dev))
+            key = (rep[M], shp, str(dev))
             if key not in done:
-                done[key] = tune_shape(M, shp, dev)
+                done[key] = tune_shape(rep[M], shp, dev)
             nt, s, t, t0_us = done[key]
             if nt:
                 lib.gemm_tuned_set(M, shp.N, shp.K, shp.glu, int(shp.fp8), nt, s)
             res[(name, M)] = done[key]
-    if os.environ.get("LLMSS_QKV_EPI", "1") != "0":
-        key = ("qkv_epi", tuple(sorted(set(int(m) for m in ms))), model_shapes(model)["qkv"], str(dev),
-               model.cfg.head_dim, model.cfg.rotary_dim, model.cfg.rope_style, model.cfg.position)
-        if key not in _QKV_DONE:
-            _QKV_DONE[key] = tune_qkv_epilogue(model, ms, lib)
-        else:  # re-install this process's earlier winners
-            _reinstall_qkv(lib, model, _QKV_DONE[key])
-        for M, (u, f) in _QKV_DONE[key].items():
-            res[("qkv_epi", M)] = (0, 0, min(u, f), u)
+    # the fused QKV epilogue is a candidate wherever it applies (tune_qkv_epilogue decides per bucket)
+    key = ("qkv_epi", tuple(sorted(set(int(m) for m in ms))), model_shapes(model)["qkv"], str(dev),
+           model.cfg.head_dim, model.cfg.rotary_dim, model.cfg.rope_style, model.cfg.position)
+    if key not in _QKV_DONE:
+        _QKV_DONE[key] = tune_qkv_epilogue(model, ms, lib)
+    else:  # re-install this process's earlier winners
+        _reinstall_qkv(lib, model, _QKV_DONE[key])
+    for M, (u, f) in _QKV_DONE[key].items():
+        res[("qkv_epi", M)] = (0, 0, min(u, f), u)
     torch.cuda.synchronize(dev)
     gain = sum(v[3] - v[2] for v in res.values())
     log.info("autotuned %d GEMM shapes in %.1fs (sum of per-call gains %.1f us)", len(res),

@@ -98,12 +98,12 @@ def add_norm(x, weight, bias, eps, rms, residual=None, out=None, residual_out=No
         _check(ro.is_contiguous() and ro.shape == (T, H), "residual_out")
     else:
         ro = None
+    if residual is None and xcw:  # checked before the launch: an invalid call queues no GPU work
+        raise ValueError("a column-chunked add_norm input needs a residual (its residual output is row-major)")
     q8, s8 = _fp8_twin(y) if fp8_out else (None, None)
     lib().add_norm(x.data_ptr(), x.stride(0) if not xcw else xcw, _ptr(residual), _ptr(ro), weight.data_ptr(),
                    _ptr(bias), y.data_ptr(), y.stride(0), T, H, float(eps), bool(rms), _stream(), _ptr(q8), _ptr(s8),
                    xcw)
-    if residual is None and xcw:
-        raise ValueError("a column-chunked add_norm input needs a residual (its residual output is row-major)")
     return y, (ro if residual is not None else x)
 
 
@@ -413,20 +413,8 @@ class _QuantScratch:
 _QSCRATCH = _Slotted(_QuantScratch)
 
 
-class _DequantScratch:
-    def __init__(self):
-        self.buf = None
-
-    def get(self, numel, device):
-        if self.buf is None or self.buf.numel() < numel or self.buf.device != device:
-            self.buf = torch.empty(numel, dtype=torch.bfloat16, device=device)
-        return self.buf
 
 
-_DEQ = _Slotted(_DequantScratch)
-
-
-_W8A8 = os.environ.get("LLMSS_FP8_W8A8", "1") != "0"
 
 
 def linear_w8a8(x, wq, w_scale, bias=None, act="none", glu=False, out=None, tile=0, depth=0, split=0,
@@ -521,12 +509,8 @@ def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hi
         if nt_hint & W8A8_FLAG:
             return linear_w8a8(x, w, w_scale, bias, act, glu, out, (nt_hint >> 8) & 15, (nt_hint >> 12) & 15,
                                split_hint, partial_ok=partial_ok)
-        if M > _FP8_PREFILL_M and not nt_hint and tuned is None:
-            if _W8A8:  # compute-bound: per-token fp8 activations on the MX-fp8 matrix cores
-                return linear_w8a8(x, w, w_scale, bias, act, glu, out, partial_ok=partial_ok)
-            wd = _DEQ.get(w.numel(), x.device)[: w.numel()].view(w.shape)
-            dequant_fp8_rows(w, w_scale, out=wd)
-            return linear(x, wd, bias, act, glu, None, out, 0, split_hint, partial_ok)
+        if M > _FP8_PREFILL_M and not nt_hint and tuned is None:  # compute-bound: per-token fp8 activations
+            return linear_w8a8(x, w, w_scale, bias, act, glu, out, partial_ok=partial_ok)  # on the MX-fp8 MFMA
     else:
         _bf16_rows(w, "w")
         _check(w.is_contiguous(), "w contiguous")
@@ -611,7 +595,7 @@ def w8a8_planned(M: int, N: int, K: int, glu: bool) -> bool:
     tuned = lib().gemm_tuned_get(M, N, K, bool(glu), 1)
     if tuned is not None:
         return bool(tuned[0] & W8A8_FLAG)
-    return _W8A8 and M > _FP8_PREFILL_M
+    return M > _FP8_PREFILL_M
 
 
 def quant_fp8_rows(w):

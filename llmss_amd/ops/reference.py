@@ -258,10 +258,23 @@ def dequant_fp8(w_q: torch.Tensor, w_scale: torch.Tensor, dtype=torch.float32) -
     return (w_q.view(torch.float8_e4m3fn).float() * w_scale.float()[:, None]).to(dtype)
 
 
+def fake_quant_fp8_act(x: torch.Tensor) -> torch.Tensor:
+    """Per-token e4m3 fake quantisation of GEMM activations, as the W8A8 path quantises them (csrc/quant.hip
+    quant_fp8_rows_ld, the add_norm / attention fp8 twins): scale = absmax(row) / 448 (1 for a zero row),
+    q = e4m3(clamp(x * (1 / scale), +-448)); returns q * scale in fp32."""
+    xf = x.float()
+    amax = xf.abs().amax(dim=-1, keepdim=True)
+    s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    q = (xf * (1.0 / s)).clamp(-448, 448).to(torch.float8_e4m3fn).float()
+    return q * s
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act: str = "none", glu: bool = False,
-           w_scale: Optional[torch.Tensor] = None) -> torch.Tensor:
+           w_scale: Optional[torch.Tensor] = None, a8: bool = False) -> torch.Tensor:
+    """``a8`` (fp8 weights only): per-token e4m3 activations as well - the fp32 fake-quant oracle of W8A8."""
     wf = dequant_fp8(w, w_scale) if w_scale is not None else w.float()
-    y = x.float() @ wf.t()
+    xf = fake_quant_fp8_act(x) if (a8 and w_scale is not None) else x.float()
+    y = xf @ wf.t()
     if bias is not None:
         y = y + bias.float()
     if glu:

@@ -286,14 +286,14 @@ class TPGroup:
 
     def agree(self, fn) -> Tuple[bool, str]:
         """Run ``fn()`` on every rank and agree on its success: ``(True, "")`` on every rank only if it raised
-        on none. A rank where it raised (RuntimeError) reports ``(False, its error)``, the others
+        on none. A rank where it raised (any Exception) reports ``(False, its error)``, the others
         ``(False, "")``, so all ranks take the same branch afterwards - a decision taken per rank (one rank
         eager, its peers in graphs) would leave the peers waiting in a collective the failed rank never joins."""
         err = ""
         try:
             fn()
-        except RuntimeError as e:
-            err = str(e) or repr(e)
+        except Exception as e:  # noqa: BLE001 - any failure (RuntimeError, HIP errors, OOM, ValueError) is agreed
+            err = f"{type(e).__name__}: {e}"
         ok = self.all_reduce_int(0 if err else 1, "min")
         return bool(ok), err
 

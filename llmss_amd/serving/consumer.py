@@ -23,6 +23,7 @@ same engine step. Measured on the closed-loop serving bench: profiles/r5_pubsub.
 """
 from __future__ import annotations
 
+import collections
 import json
 import queue
 import threading
@@ -55,6 +56,10 @@ class Consumer:
         self._out: "queue.Queue" = queue.Queue()
         self.served = 0
         self.requeued = 0
+        # durable mode: raw requests submitted and not yet acknowledged (LREM sent successfully), to tell which
+        # processing-list entries a failed batch pop left behind (_resync_processing)
+        self._inflight: "collections.Counter[str]" = collections.Counter()
+        self._inflight_mu = threading.Lock()
 
     # ------------------------------------------------------------------ publisher thread
     def _publish_loop(self):
@@ -106,6 +111,13 @@ class Consumer:
                 for r in self.broker.pipeline(cmds):
                     if isinstance(r, Exception):
                         log.error("consumer publish: broker error %s", r)
+                # acknowledged: these requests no longer count as in flight (an ack that failed keeps its entry in
+                # the processing list and in flight - a resync then does not serve it twice)
+                acked = [c[3] for c in cmds if c[0] == "LREM"]
+                if acked:
+                    with self._inflight_mu:
+                        self._inflight.subtract(acked)
+                        self._inflight += collections.Counter()  # drop counts <= 0
             except Exception:  # noqa: BLE001 - a broker hiccup must not kill the publisher
                 log.exception("consumer publish failed")
             if stop:
@@ -157,14 +169,42 @@ class Consumer:
                 try:
                     more = self.broker.pipeline([pop] * (self.intake_batch - 1))
                 except Exception:  # noqa: BLE001 - the popped request is still served
+                    # the server may have run some of the pops before the connection dropped. Durable mode: those
+                    # requests sit in this consumer's processing list - resync below picks them up. Non-durable
+                    # mode: they are lost, as the reference's RPOP loses a request whose consumer dies
+                    # (consumer_server.py:79-80); the connection drop fails every other broker call too.
                     log.exception("consumer intake: batch pop failed")
-                    more = []
-                msgs += [m for m in more if isinstance(m, str)]
+                    more = None
+                if more is not None:
+                    msgs += [m for m in more if isinstance(m, str)]
+                elif self.durable:
+                    for m in msgs:
+                        self._submit(m)
+                    msgs = self._resync_processing()
             for m in msgs:
                 self._submit(m)
 
+    def _resync_processing(self) -> list:
+        """Durable mode, after a batch pop failed part-way: the entries of this consumer's processing list that are
+        not in flight (popped by commands whose replies were lost). Returns them for submission."""
+        try:
+            listed = collections.Counter(self.broker.lrange(processing_key(self.consumer_id), 0, -1))
+        except Exception:  # noqa: BLE001 - still unreachable: the next start's recover() re-queues them
+            log.exception("consumer intake: processing-list resync failed")
+            return []
+        with self._inflight_mu:
+            missing = listed - self._inflight
+        out = [raw for raw, n in missing.items() for _ in range(n)]
+        if out:
+            log.warning("consumer %s: %d request(s) popped by a failed batch pop resubmitted", self.consumer_id,
+                        len(out))
+        return out
+
     def _submit(self, msg: str):
         raw = msg if self.durable else None
+        if raw is not None:
+            with self._inflight_mu:
+                self._inflight[raw] += 1
         try:
             req = parse_request(msg)
             params = to_sampling(req)

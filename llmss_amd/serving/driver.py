@@ -124,7 +124,7 @@ class EngineDriver:
         # came for `batch_window_s` (at most 10 windows) or the arrivals fill the free sequence slots, so a
         # burst of concurrent clients is admitted in one prefill step instead of trickling in one by one
         self.batch_window_s = float(os.environ.get("LLMSS_ADMIT_WINDOW_S", "0.003"))
-        self.batch_window_max = int(os.environ.get("LLMSS_ADMIT_WINDOW_MAX", "10"))
+        self.batch_window_max = 10
         self.fault = fault if fault is not None else FaultSpec.from_env()
         self.error: Optional[BaseException] = None
         self._last_bcast = time.perf_counter()
@@ -314,7 +314,7 @@ class EngineDriver:
         raise RuntimeError(f"injected fault at step {step}")
 
     def run(self):
-        if self.engine.is_gpu and os.environ.get("LLMSS_GC_FREEZE", "1") != "0":
+        if self.engine.is_gpu:
             # a serving process keeps its model, KV pool, plans and graphs for its lifetime: move them out of
             # the cyclic collector's generations so a full collection while serving scans only per-request
             # objects (served GPT-2-XL steps showed ~110-130 ms stalls on 2 of 20 steps)

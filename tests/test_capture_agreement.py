@@ -22,8 +22,11 @@ def _worker(rank, port, ckpt, q):
 
         tp, r, _ = initialize_distributed(backend="gloo")
         ok, err = tp.agree(lambda: (_ for _ in ()).throw(RuntimeError("boom")) if r == 0 else None)
-        assert (ok, err) == (False, "boom" if r == 0 else ""), (ok, err)
+        assert (ok, err) == (False, "RuntimeError: boom" if r == 0 else ""), (ok, err)
         assert tp.agree(lambda: None) == (True, "")
+        # any exception type is agreed (a ValueError / HIP error on one rank must not make it leave alone)
+        ok, err = tp.agree(lambda: int("x") if r == 1 else None)
+        assert not ok and (err.startswith("ValueError") if r == 1 else err == ""), (ok, err)
         m = build_model(ckpt, tp, "fp32", "cpu")
         eng = LLMEngine(m, max_num_seqs=4, block_size=4, num_blocks=64, check_tokens=True)
         calls = []

@@ -292,18 +292,20 @@ def test_col_schedule_ab_at_capture(comm, monkeypatch):
         def all_gather_object(self, obj):
             return [obj, obj]
 
-    monkeypatch.setenv("LLMSS_TBO_AUTO", "0")
+    monkeypatch.setenv("LLMSS_TBO_AUTO_MIN", "0")
     monkeypatch.setenv("LLMSS_TP_RSAG", "0")
     monkeypatch.setenv("LLMSS_TP_COL", "auto")
-    monkeypatch.setenv("LLMSS_TP_COL_MIN", "8")
     tp = OneRankNative(0, 2, comm=comm)
     cfg = get_preset("tiny-llama", hidden_size=256, num_heads=4, num_kv_heads=2, head_dim=64, rotary_dim=64,
                      intermediate_size=512, max_position_embeddings=256)
     m = DecoderLM(cfg, random_weights(cfg, 2, 0, device="cuda", dtype=torch.bfloat16, seed=5, std=0.05), tp)
     prompts = [[int(x) for x in torch.randint(0, cfg.vocab_size, (n,))] for n in range(3, 23)]
     sp = SamplingParams(max_new_tokens=10, is_greedy=True, ignore_eos=True)
+    m.col_min = 8
     e = LLMEngine(m, max_num_seqs=24, block_size=16, use_graphs=True, autotune=False, graph_buckets=[1, 8, 16, 24])
-    assert e._col_cands == [8, 16, 24] and set(e.stats["schedule_ab_ms"]) >= {"8c", "16c", "24c"}
+    # timed buckets 8 and 24 (LLMEngine._ab_buckets); 16 adopts the winner of its nearest timed bucket
+    assert e._col_cands == [8, 16, 24] and set(e.stats["schedule_ab_ms"]) >= {"8c", "24c"}
+    assert "16c" not in e.stats["schedule_ab_ms"]
     assert all(set(v) == {"one", "col"} for v in e.stats["schedule_ab_ms"].values())
     out_g = e.generate(prompts, sp)
     del e

@@ -146,9 +146,11 @@ def test_rope_interleave_matches_checkpoint_order(ckpts, monkeypatch, tmp_path):
 
     d, _ = ckpts["llama"]
     cfg, w_il = _load(d)
-    monkeypatch.setenv("LLMSS_ROPE_INTERLEAVE", "0")
+    import llmss_amd.models.weights as W
+
+    monkeypatch.setattr(W, "ROPE_INTERLEAVE", False)
     _, w_ck = _load(d)
-    monkeypatch.delenv("LLMSS_ROPE_INTERLEAVE")
+    monkeypatch.setattr(W, "ROPE_INTERLEAVE", True)
     assert w_il.rope_interleaved and not w_ck.rope_interleaved
     assert DecoderLM(cfg, w_il).cfg.rope_style == "gptj" and DecoderLM(cfg, w_ck).cfg.rope_style == "neox"
     ids = torch.randint(0, 100, (13,))

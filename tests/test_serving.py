@@ -204,6 +204,46 @@ def test_durable_queue_requeues_after_consumer_crash(driver):
     consumer.stop()
 
 
+def test_durable_intake_recovers_requests_of_a_failed_batch_pop(driver):
+    """the connection drops after the server ran part of the intake's batch pop. The requests those pops
+    moved into the processing list are resubmitted at once (no restart needed), none is served twice, every one is
+    answered and acknowledged."""
+    from llmss_amd.serving.consumer import processing_key
+
+    drv, tok, m = driver
+
+    class DropAfter2(MemoryBroker):
+        fail = True
+
+        def pipeline(self, cmds):
+            if self.fail and cmds and cmds[0][0] == "RPOPLPUSH":
+                self.fail = False
+                super().pipeline(cmds[:2])  # ran on the server, replies lost
+                raise ConnectionError("connection reset mid-pipeline")
+            return super().pipeline(cmds)
+
+    b = DropAfter2()
+    n = 5
+    for i in range(n):
+        b.lpush(PQUEUE, json.dumps({"prompt": f"drop {i}", "max_new_tokens": 3, "is_greedy": True, "temperature": 1.0,
+                                    "top_p": 0.95, "top_k": 50, "request_id": f"d{i}"}))
+    consumer = Consumer(drv, tok, b, poll_timeout=0.2, consumer_id="cd").start()
+    try:
+        for i in range(n):
+            msg = b.brpop(reply_key(f"d{i}"), 60)
+            assert msg is not None and json.loads(msg)["continuation"] == _offline(m, tok, f"drop {i}", 3)
+        assert not b.fail  # the failure really happened
+        for _ in range(100):
+            if b.llen(processing_key("cd")) == 0:
+                break
+            time.sleep(0.05)
+        assert b.llen(processing_key("cd")) == 0
+        time.sleep(0.3)
+        assert consumer.served == n and all(b.llen(reply_key(f"d{i}")) == 0 for i in range(n))  # nothing twice
+    finally:
+        consumer.stop()
+
+
 def test_redis_broker_list_commands():
     """BRPOPLPUSH / LREM / LRANGE over RESP against the embedded server (Redis semantics)."""
     srv = MiniRedisServer().start()

@@ -22,14 +22,18 @@ def _free_port():
 def _worker(rank, world, port, ckpt, prompts, q, env=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
-    os.environ.update(env or {})  # e.g. the overlap paths
+    env = dict(env or {})
+    attrs = {k: int(env.pop(k)) for k in ("overlap_rows", "tbo_min") if k in env}  # DecoderLM attributes
+    os.environ.update(env)  # e.g. the overlap paths
     torch.set_num_threads(1)
     from llmss_amd.engine import LLMEngine, SamplingParams, build_model
     from llmss_amd.parallel.dist import initialize_distributed
 
     tp, r, w = initialize_distributed(backend="gloo")
     m = build_model(ckpt, tp, "fp32", "cpu")
-    if "LLMSS_TP_DECODE_OVERLAP_MIN" in (env or {}):
+    for k, v in attrs.items():
+        setattr(m, k, v)
+    if "tbo_min" in attrs:
         assert m.overlap_split(3) == 1  # the 3-sequence decode steps really take the micro-batch path
     if "LLMSS_TP_PREFILL_OVERLAP_MIN" in (env or {}):  # the 3-prompt prefill splits at a sequence boundary
         from llmss_amd.models.decoder import StepInput
@@ -47,6 +51,11 @@ def _worker(rank, world, port, ckpt, prompts, q, env=None):
                                                     ignore_eos=True) for i in range(len(prompts))])
     if (env or {}).get("LLMSS_TP_RSAG") == "1" or (env or {}).get("LLMSS_TP_COL"):
         assert calls[0] > 0, "the forced decode schedule never ran"
+    # comm-stream fork / join structure (models/decoder.py StreamLedger): everything forked was joined, and the
+    # schedules that overlap collectives really forked (the same calls fork and join streams on the GPU)
+    assert not m._ledger.open
+    if attrs or any(k in env for k in ("LLMSS_TP_BUCKET_BYTES", "LLMSS_TP_PREFILL_OVERLAP_MIN", "LLMSS_TP_COL")):
+        assert m._ledger.forks > 0, "the overlapped schedule never forked the comm stream"
     if r == 0:
         q.put((greedy, sampled))
     torch.distributed.barrier()
@@ -67,10 +76,10 @@ def _run(world, ckpt, prompts, env=None):
     return res
 
 
-# LLMSS_TP_OVERLAP_ROWS / LLMSS_TP_BUCKET_BYTES: row-bucketed all-reduce / GEMM overlap (rows, or bytes per bucket);
-# LLMSS_TP_DECODE_OVERLAP_MIN: decode steps as two interleaved micro-batches (the 3-sequence batch splits 1 + 2)
-_ROWS = {"LLMSS_TP_OVERLAP_ROWS": "4"}
-_TBO = {"LLMSS_TP_DECODE_OVERLAP_MIN": "2"}
+# overlap_rows (DecoderLM attribute) / LLMSS_TP_BUCKET_BYTES: row-bucketed all-reduce / GEMM overlap (rows, or bytes
+# per bucket); tbo_min (attribute): decode steps as two interleaved micro-batches (the 3-sequence batch splits 1 + 2)
+_ROWS = {"overlap_rows": "4"}
+_TBO = {"tbo_min": "2"}
 _PTBO = {"LLMSS_TP_PREFILL_OVERLAP_MIN": "2"}  # prefill steps as two micro-batches split at a sequence boundary
 _RSAG = {"LLMSS_TP_RSAG": "1"}  # row-sharded decode: reduce-scatter -> add + norm on M / tp rows -> all-gather
 _COL = {"LLMSS_TP_COL": "2"}  # column-chunked decode: row-parallel outputs as 2 weight-row slices, one AR each
@@ -78,7 +87,7 @@ _COL = {"LLMSS_TP_COL": "2"}  # column-chunked decode: row-parallel outputs as 2
 
 @pytest.mark.parametrize("name,world,overlap", [("llama", 2, None), ("gptj", 2, None), ("bigcode", 4, None),
                                                 ("gpt2", 2, None), ("bigcode_mha", 2, None), ("llama", 2, _ROWS),
-                                                ("gptj", 2, {"LLMSS_TP_OVERLAP_ROWS": "5"}), ("llama", 2, _TBO),
+                                                ("gptj", 2, {"overlap_rows": "5"}), ("llama", 2, _TBO),
                                                 ("llama", 2, {"LLMSS_TP_BUCKET_BYTES": "64"}),
                                                 ("gptj", 2, _TBO), ("bigcode", 4, _TBO), ("llama", 2, _PTBO),
                                                 ("gptj", 2, _PTBO), ("bigcode", 4, {**_PTBO, **_TBO}),
