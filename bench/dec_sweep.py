@@ -70,6 +70,8 @@ def main():
                         continue
                     if partial or s == 1:
                         cands.append(((code | d | 1024) << 8, s, partial and s > 1))
+                    if 1 < s <= 4:  # split-K combined in the launch: finished output
+                        cands.append(((code | d | 1024 | 256) << 8, s, False))
         for t, bn in ({} if args.only_dec else MID_BN).items():
             for d in (32, 48):
                 for s in sorted({1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 13, 16, 20, 25}):

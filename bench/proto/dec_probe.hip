@@ -27,7 +27,7 @@ static void launch(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* part, int
                    hipStream_t st) {
   dim3 grid((N + BN - 1) / BN, split);
   gemm_dec_kernel<MT, BN, NS, MODE><<<grid, 256, 0, st>>>(X, K, W, K, nullptr, Y, N, split > 1 ? part : nullptr, M, N,
-                                                          K, 0, 0, QkvEpi{});
+                                                          K, 0, 0, QkvEpi{}, nullptr);
 }
 
 using Fn = void (*)(const bf16_t*, const bf16_t*, bf16_t*, float*, int, int, int, int, hipStream_t);

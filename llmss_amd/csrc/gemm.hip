@@ -1360,8 +1360,14 @@ __global__ __launch_bounds__(256) void gemm_f8f8_kernel(const unsigned char* __r
 // depth code (2 / 3 / 4 / 4 stages per wave), split_hint = K split over the grid (fp32 slabs for the consumer)
 void launch_gemm_dec(int code, int depth, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
-                     int split, hipStream_t st, const QkvEpi* qe);
+                     int split, hipStream_t st, const QkvEpi* qe, int* cnt);
 bool gemm_dec_bn(int code, int* bn);
+// the decode GEMM's in-launch combine (hint bit 256 with a split) fits the workspace: [tile][split][64 * bn] fp32
+static bool dec_combine_fits(int N, int tsel, int s, int64_t ws_bytes) {
+  int bn;
+  if (!(tsel & 256) || s <= 1 || !gemm_dec_bn(tsel & 15, &bn)) return false;
+  return (int64_t)((N + bn - 1) / bn) * s * 64 * bn * 4 <= ws_bytes;
+}
 static constexpr int kDecHint = 1024;
 static int dec_split(int M, int N, int K, int split_hint, int64_t ws_bytes) {
   int s = std::max(1, std::min(split_hint, (K + 63) / 64));
@@ -1806,11 +1812,19 @@ int launch_tiled(const bf16_t* X, int64_t ldx, const void* W, int64_t ldw, const
   if (tsel & kDecHint) {  // K split over the waves (gemm_dec.hip), M <= 64, bf16 weights
     if (f8) throw std::runtime_error("gemm_dec: bf16 weights only");
     s = dec_split(M, N, K, split_hint, ws_bytes);
-    if (qe && s > 1) throw std::runtime_error("gemm_dec: the QKV epilogue needs an unsplit plan");
+    if (s > 1 && Y && dec_combine_fits(N, tsel, s, ws_bytes)) {  // split-K combined in the launch: finished Y
+      int bn;
+      gemm_dec_bn(tsel & 15, &bn);
+      static constexpr int kDecDepthC[4] = {2, 3, 4, 4};
+      launch_gemm_dec(tsel & 15, kDecDepthC[(tsel >> 4) & 3], X, ldx, (const bf16_t*)W, ldw, B, Y, ldy,
+                      (float*)workspace, M, N, K, act, g, s, st, qe, sk_counters((N + bn - 1) / bn));
+      return 0;
+    }
+    if (qe && s > 1) throw std::runtime_error("gemm_dec: the QKV epilogue needs an unsplit or in-launch-combined plan");
     static constexpr int kDecDepth[4] = {2, 3, 4, 4};
     float* part = s > 1 ? (float*)workspace : nullptr;
     launch_gemm_dec(tsel & 15, kDecDepth[(tsel >> 4) & 3], X, ldx, (const bf16_t*)W, ldw, B, Y, ldy, part, M, N, K,
-                    s > 1 ? 0 : act, s > 1 ? 0 : g, s, st, qe);
+                    s > 1 ? 0 : act, s > 1 ? 0 : g, s, st, qe, nullptr);
     if (s > 1 && partial_out && !g && act == 0) return s;
     if (s > 1) {
       const int nout = g ? N / 2 : N;
@@ -1946,6 +1960,7 @@ int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int n
     if (tsel & kDecHint) {
       if (w_fp8) return 0;  // rejected at launch
       s = dec_split(M, N, K, split_hint, ws_bytes);
+      if (dec_combine_fits(N, tsel, s, ws_bytes)) return 0;  // combined in the launch
       return s > 1 ? s : 0;
     }
     if ((tsel & 128) && !w_fp8 && (tsel & 15) < 5) return 0;  // stream-K combines in-kernel
@@ -1981,11 +1996,14 @@ int launch_gemm_qkv(const void* x, int64_t ldx, const void* w, int64_t ldw, cons
   if (qe.do_rope && (qe.rot % 8 || qe.rot > qe.D || (qe.style == 0 && qe.rot % 16))) return -1;
   if (nt_hint == 0 && split_hint == 0) gemm_tuned_get(M, N, K, false, 3, &nt_hint, &split_hint);
   if (nt_hint & 0xff) return -1;  // streaming kernels have no LDS-staged epilogue
-  if ((nt_hint >> 8) & kDecHint) {  // decode GEMM: unsplit plans only (the epilogue needs finished sums)
+  if ((nt_hint >> 8) & kDecHint) {  // decode GEMM: unsplit, or split and combined in the launch (finished sums)
     int bn;
-    if (M > 64 || dec_split(M, N, K, split_hint, ws_bytes) > 1 || !gemm_dec_bn((nt_hint >> 8) & 15, &bn)) return -1;
+    if (M > 64 || !gemm_dec_bn((nt_hint >> 8) & 15, &bn)) return -1;
     if (qe.do_rope && qe.style == 0 && bn % qe.D) return -1;
-    launch_tiled((const bf16_t*)x, ldx, w, ldw, (const bf16_t*)bias, (bf16_t*)y, ldy, M, N, K, 0, 0, nt_hint >> 8, 1,
+    const int s = dec_split(M, N, K, split_hint, ws_bytes);
+    const int tsel = (nt_hint >> 8) | (s > 1 ? 256 : 0);
+    if (s > 1 && !dec_combine_fits(N, tsel, s, ws_bytes)) return -1;
+    launch_tiled((const bf16_t*)x, ldx, w, ldw, (const bf16_t*)bias, (bf16_t*)y, ldy, M, N, K, 0, 0, tsel, s,
                  workspace, ws_bytes, false, st, nullptr, &qe);
     return 0;
   }
@@ -2016,7 +2034,7 @@ int launch_gemm_qkv_args(const void* x, int64_t ldx, const void* w, int64_t ldw,
 void gemm_plan(int M, int N, int K, bool w_fp8, int* nt, int* splitk) {
   if (gemm_tuned_get(M, N, K, false, w_fp8 ? 1 : 0, nt, splitk)) {
     if ((*nt >> 8) & kDecHint) {
-      *splitk = dec_split(M, N, K, *splitk, INT64_MAX);
+      *splitk = ((*nt >> 8) & 256) ? 1 : dec_split(M, N, K, *splitk, INT64_MAX);
     } else if ((*nt >> 8) & (128 | 256)) {
       *splitk = 1;  // stream-K / split-K combine finish their tiles in-kernel: no partial slabs for the consumer
     } else if (*nt >> 8) {  // tiled hint: the split the kernel will really use

@@ -49,6 +49,47 @@ __device__ __forceinline__ void dec_wait(int younger_stages) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// In-launch split-K combine on the epilogue image (hint bit 256 with a grid split): every K slice of a column tile
+// writes its fp32 image, row-major [AR][BN], write-through (sc1) into its slab of the tile's workspace region
+// [tile][S][AR * BN]; every wave drains its stores, then one lane takes a ticket on the tile's counter (relaxed,
+// agent scope: MI355X_MICROARCH "Valid forms" row 1, as common.h splitk_combine). The slice that draws S - 1 reads
+// all S slabs back with sc1 loads and sums them in slice order 0..S-1 - the same sums whatever the arrival order -
+// into its image, resets the counter, and returns true: it runs the epilogue. The others return false.
+template <int BN, int AR>
+__device__ __forceinline__ bool dec_combine(float* ct, float* ws, int* cnt, int tile, int S, int z, int* lds_word) {
+  using Img = EpiImg<BN>;
+  constexpr int V4 = AR * BN / 4;  // 16-B pieces of one slab
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(ws) + (int64_t)tile * S * AR * BN * 4,
+                                                    (short)0, (int)((uint32_t)S * (uint32_t)(AR * BN * 4)), 0x00020000);
+  const uint32_t slab_b = (uint32_t)(AR * BN * 4);
+  for (int v = threadIdx.x; v < V4; v += blockDim.x) {
+    const int r = v / (BN / 4), c = (v - r * (BN / 4)) * 4;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, Img::ld4(ct, r, c)), rs, (uint32_t)(v * 16),
+                                           (uint32_t)z * slab_b, 16);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains before the ticket
+  __syncthreads();
+  if (threadIdx.x == 0) *lds_word = __hip_atomic_fetch_add(cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (*lds_word != S - 1) return false;
+  if (threadIdx.x == 0) __hip_atomic_store(cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+  for (int v = threadIdx.x; v < V4; v += blockDim.x) {
+    const int r = v / (BN / 4), c = (v - r * (BN / 4)) * 4;
+    f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < S; ++s) {
+      const f32x4 p = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(v * 16),
+                                                                                      (uint32_t)s * slab_b, 16));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sum[i] += p[i];
+    }
+    *reinterpret_cast<f32x4*>(ct + Img::at(r, c)) = sum;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  return true;
+}
+
 }  // namespace
 
 // MODE (bench/proto/dec_probe.hip only; the library instantiates 0): 1 = weight (B) loads only, 2 = activation (A)
@@ -58,7 +99,7 @@ __global__ __launch_bounds__(256) void gemm_dec_kernel(const bf16_t* __restrict_
                                                        const bf16_t* __restrict__ B, int64_t ldb,
                                                        const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
                                                        int64_t ldy, float* __restrict__ part, int M, int N, int K,
-                                                       int act, int glu, QkvEpi qe) {
+                                                       int act, int glu, QkvEpi qe, int* __restrict__ cnt) {
   using C = DecCfg<MT, BN, NSW>;
   static_assert(BN % 16 == 0 && C::BL >= 1, "BN: multiple of 16");
   static_assert(3 * C::LOADS <= 63, "vmcnt immediate");
@@ -214,6 +255,10 @@ __global__ __launch_bounds__(256) void gemm_dec_kernel(const bf16_t* __restrict_
     if (M < 0) part[threadIdx.x] = ct[threadIdx.x];  // keep the sums live without storing them
     return;
   }
+  if (cnt) {  // split-K combined in this launch: the tile's last arriving K slice sums every slice and stores
+    if (!dec_combine<BN, AR>(ct, part, cnt, n0 / BN, gridDim.y, zk, reinterpret_cast<int*>(smem))) return;
+    part = nullptr;
+  }
   img_store_rows<BN, 64 * NW, AR>(ct, AR, 0, 0, n0, M, N, part ? part + (int64_t)zk * M * N : nullptr, Y, ldy, bias,
                                   act, glu, qe);
 }
@@ -222,11 +267,11 @@ __global__ __launch_bounds__(256) void gemm_dec_kernel(const bf16_t* __restrict_
 template <int MT, int BN, int NS>
 static void dec_launch(dim3 grid, hipStream_t st, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
                        const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
-                       const QkvEpi& qv) {
+                       const QkvEpi& qv, int* cnt) {
   if constexpr (NS > 2 && !DecCfg<MT, BN, NS>::FITS) {
-    dec_launch<MT, BN, NS - 1>(grid, st, X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, qv);
+    dec_launch<MT, BN, NS - 1>(grid, st, X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, qv, cnt);
   } else {
-    gemm_dec_kernel<MT, BN, NS><<<grid, 256, 0, st>>>(X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, qv);
+    gemm_dec_kernel<MT, BN, NS><<<grid, 256, 0, st>>>(X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, qv, cnt);
   }
 }
 
@@ -246,9 +291,11 @@ static int dec_depth(int mt, int bn, int want) {
   return ns;
 }
 
+// cnt != nullptr: split-K combined in the launch (dec_combine; `part` = the workspace holding [tile][split][64 * bn]
+// fp32 slabs, sized by the caller), finished output in Y with act / glu / the QKV epilogue
 void launch_gemm_dec(int code, int depth, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
-                     int split, hipStream_t st, const QkvEpi* qe) {
+                     int split, hipStream_t st, const QkvEpi* qe, int* cnt) {
   int bn;
   if (!gemm_dec_bn(code, &bn)) throw std::runtime_error("gemm_dec: bad tile code");
   if (M < 1 || M > 64) throw std::runtime_error("gemm_dec: M must be 1..64");
@@ -261,9 +308,9 @@ void launch_gemm_dec(int code, int depth, const bf16_t* X, int64_t ldx, const bf
   dim3 grid((N + bn - 1) / bn, split);
 #define DECN(MT_, BN_)                                                                                           \
   do {                                                                                                           \
-    if (ns >= 4) dec_launch<MT_, BN_, 4>(grid, st, X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, qv);   \
-    else if (ns == 3) dec_launch<MT_, BN_, 3>(grid, st, X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, qv); \
-    else dec_launch<MT_, BN_, 2>(grid, st, X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, qv);          \
+    if (ns >= 4) dec_launch<MT_, BN_, 4>(grid, st, X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, qv, cnt);   \
+    else if (ns == 3) dec_launch<MT_, BN_, 3>(grid, st, X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, qv, cnt); \
+    else dec_launch<MT_, BN_, 2>(grid, st, X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, qv, cnt);          \
   } while (0)
 #define DECB(MT_)                                                                                                \
   do {                                                                                                           \

@@ -94,6 +94,8 @@ def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, 
         for code, bn in ((1, 16), (2, 32), (3, 48), (4, 64)):
             tiles = -(-N // bn)
             out += [((code | 32 | 1024) << 8, s) for s in (1, 2, 3, 4, 5, 8, 10) if s <= nk and 64 <= tiles * s <= 1024]
+            # (its in-launch split-K combine, hint bit 256, is selectable but not a candidate: 15.2 us at best for
+            # GPT-2-XL's up projection against 10.6 unsplit, profiles/r6_dec)
     # interleaved ring (hint bit 512, csrc/gemm_mid.hip ILV): >= 3 stages
     if M >= ILV_MIN_M and K % 64 == 0:
         out += [((t | d | 512) << 8, s) for t, d in mids if d >= 16 for s in (1, 2, 3, 4, 5, 6, 8)
@@ -226,7 +228,7 @@ def qkv_epi_candidates(M: int, N: int, K: int, D: int, neox_rope: bool) -> List[
         tiles += [(9, 128, (0,))]
     nk = -(-K // 64)
     out = []
-    if M <= 64:  # the K-split-wave decode kernel (csrc/gemm_dec.hip): unsplit plans only
+    if M <= 64:  # the K-split-wave decode kernel (csrc/gemm_dec.hip), unsplit (its in-launch combine measured slower)
         out += [((code | 32 | 1024) << 8, 1) for code, bn in ((1, 16), (2, 32), (3, 48), (4, 64))
                 if not (neox_rope and bn % D)]
     for t, bn, depths in tiles:

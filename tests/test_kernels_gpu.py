@@ -386,6 +386,36 @@ def test_gemm_dec(code, depth, split, M, N, K):
         close(p, ref, 2e-2)
 
 
+@pytest.mark.parametrize("code", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("split", [2, 3, 5])
+@pytest.mark.parametrize("M,N,K", [(64, 6400, 1600), (7, 4800, 1600), (33, 2752, 4096), (64, 200, 64 * 5 + 16)])
+def test_gemm_dec_combine_in_launch(code, split, M, N, K):
+    """The decode GEMM's split-K combined in the launch (hint bit 256): the tile's last K slice sums every slice's
+    write-through slab in slice order and runs the epilogue. Bit-identical to the same plan's slabs summed by the
+    separate reduce launch (activation-free), across repeated calls (self-resetting tile counters), with NaN-filled
+    outputs and a NaN-poisoned workspace; GELU and SwiGLU against the fp32 oracle."""
+    torch.manual_seed(0)
+    x, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
+    b = rnd(N, scale=0.1)
+    hint, comb = (code | 16 | 1024) << 8, (code | 16 | 1024 | 256) << 8
+    H._GEMM_WS.get(64 << 20, x.device).fill_(float("nan"))
+    ref = H.linear(x, w, b, nt_hint=hint, split_hint=split)  # slabs + splitk_reduce
+    for _ in range(3):
+        y = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=dev)
+        got = H.linear(x, w, b, nt_hint=comb, split_hint=split, out=y)
+        assert torch.equal(got, ref), (got.float() - ref.float()).abs().max().item()
+    close(got, R.linear(x.float(), w.float(), b.float()), 2e-2)
+    y = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=dev)
+    close(H.linear(x, w, b, act="gelu_tanh", nt_hint=comb, split_hint=split, out=y),
+          R.linear(x.float(), w.float(), b.float(), act="gelu_tanh"), 2e-2)
+    if N % 32 == 0 and DEC_BN[code] % 32 == 0:
+        y = torch.full((M, N // 2), float("nan"), dtype=torch.bfloat16, device=dev)
+        close(H.linear(x, w, None, glu=True, nt_hint=comb, split_hint=split, out=y),
+              R.linear(x.float(), w.float(), None, glu=True), 2e-2)
+    p = H.linear(x, w, None, nt_hint=comb, split_hint=split, partial_ok=True)  # finished, not slabs
+    assert not isinstance(p, H.PartialSum)
+
+
 @pytest.mark.parametrize("code", [2, 4])
 def test_gemm_dec_k_tail_reads_nothing_past_the_operands(code):
     """As test_gemm_mid_k_tail_...: operands at the front of NaN-filled buffers, a partial last k-step."""
@@ -402,10 +432,12 @@ def test_gemm_dec_k_tail_reads_nothing_past_the_operands(code):
 
 
 @pytest.mark.parametrize("code", [1, 2, 4, 5])
+@pytest.mark.parametrize("split", [1, 2, 3])
 @pytest.mark.parametrize("style,D,rot,nh,nkv", [("none", 64, 0, 25, 25), ("gptj", 256, 64, 4, 4), ("neox", 64, 64, 8, 1)])
-def test_gemm_dec_qkv_epilogue(code, style, D, rot, nh, nkv):
+def test_gemm_dec_qkv_epilogue(code, split, style, D, rot, nh, nkv):
     """The decode GEMM with the QKV RoPE / paged-KV-write epilogue (GPT-2-XL's unrotated heads, GPT-J's interleaved
-    partial rotation) == GEMM + rope_cache; neox RoPE on a tile narrower than a head and split plans are refused."""
+    partial rotation) == GEMM + rope_cache, unsplit or split and combined in the launch; neox RoPE on a tile narrower
+    than a head is refused."""
     torch.manual_seed(0)
     T, K, bs, nb = 64, 512, 16, 40
     N = (nh + 2 * nkv) * D
@@ -420,10 +452,8 @@ def test_gemm_dec_qkv_epilogue(code, style, D, rot, nh, nkv):
     kc1 = torch.full((nb, nkv, bs, D), float("nan"), dtype=torch.bfloat16, device=dev)
     vc1 = torch.full_like(kc1, float("nan"))
     hint = (code | 16 | 1024) << 8
-    assert H.linear_qkv(x, w, b, pos, cos, sin, kc1, vc1, slots, nh, nkv, D, rot, st, do_rope, nt_hint=hint,
-                        split_hint=2) is None
     y = H.linear_qkv(x, w, b, pos, cos, sin, kc1, vc1, slots, nh, nkv, D, rot, st, do_rope, nt_hint=hint,
-                     split_hint=1)
+                     split_hint=split)
     if do_rope and st == "neox" and DEC_BN[code] % D:
         assert y is None
         return
