@@ -125,11 +125,26 @@ class EngineDriver:
         # burst of concurrent clients is admitted in one prefill step instead of trickling in one by one
         self.batch_window_s = float(os.environ.get("LLMSS_ADMIT_WINDOW_S", "0.003"))
         self.batch_window_max = 10
+        # closed-loop clients send their next request as soon as a reply lands, but through the pub/sub path
+        # (front-end -> broker -> consumer, two extra processes) a cohort's re-submissions reach the inbox spread
+        # over more than one quiet period and used to split into cohorts that never re-align (profiles/r5_pubsub).
+        # Two bounded corrections, both inside the batch_window_max * batch_window_s cap:
+        # * `_expect` counts the replies of the last `resubmit_horizon_s` not yet matched by an arrival; while a
+        #   window holds fewer arrivals than that, it tolerates a 4x longer gap between them.
+        # * near-drain hold: arrivals while every running sequence is within `merge_steps` tokens of its length
+        #   limit wait (at most the cap) for the engine to drain, so they prefill with the re-submissions of the
+        #   sequences about to finish instead of one step ahead of them.
+        self.resubmit_horizon_s = 0.25
+        self.merge_steps = 2
+        self._expect = 0
+        self._expect_t = 0.0
+        self._held: list = []  # inbox items held back by the near-drain rule, oldest first
+        self._held_t = 0.0
         self.fault = fault if fault is not None else FaultSpec.from_env()
         self.error: Optional[BaseException] = None
         self._last_bcast = time.perf_counter()
         self.stats = {"ctrl_bcasts": 0, "ctrl_payloads": 0, "admit_windows": 0, "admit_window_s": 0.0,
-                      "admit_window_reqs": 0}
+                      "admit_window_reqs": 0, "admit_held": 0}
         self._rid_stride = 1
         # global rank of this replica's leader (broadcast src is a global rank in torch.distributed)
         self._src = dist.get_global_rank(self.cg, 0) if self.tp.is_real else 0
@@ -262,12 +277,32 @@ class EngineDriver:
         dist.broadcast(buf, src=self._src, group=self.cg)
         return msg if self.leader else pickle.loads(buf.numpy().tobytes())
 
+    def _next_item(self, timeout: Optional[float]):
+        """The oldest held-back item, else the inbox's (waiting up to `timeout`; None = do not wait)."""
+        if self._held:
+            return self._held.pop(0)
+        return self.inbox.get_nowait() if timeout is None else self.inbox.get(timeout=timeout)
+
+    def _near_drain(self) -> bool:
+        """Nothing waits and every running sequence is within merge_steps tokens of its length limit."""
+        sch = self.engine.sched
+        if sch.num_waiting() or not sch.num_running():
+            return False
+        lim = self.merge_steps
+        return all(r.finished or len(r.output_ids) + lim >= r.params.max_new_tokens
+                   for r in self.engine.requests.values())
+
     def _collect(self, block: bool):
-        """Leader: drain the inbox (blocking when idle). Returns a control message."""
-        new, aborts, stop = [], [], False
+        """Leader: drain the held-back items and the inbox (blocking when idle). Returns a control message."""
+        new, raw, aborts, stop = [], [], [], False
+        held = bool(self._held)
+        now = time.perf_counter()
+        expect = self._expect if now - self._expect_t < self.resubmit_horizon_s else 0
+        t_start = self._held_t if held else now
         try:
-            item = self.inbox.get(timeout=self.idle_wait_s) if block else self.inbox.get_nowait()
-            t_start = time.perf_counter()
+            item = self._next_item(self.idle_wait_s if block and not held else None)
+            if not held:
+                t_start = time.perf_counter()
             t_end = t_start + self.batch_window_max * self.batch_window_s
             # a burst that fills every free sequence slot closes the window at once: a later arrival could not
             # join this prefill step anyway
@@ -277,19 +312,29 @@ class EngineDriver:
                 kind, v = item
                 if kind == "new":
                     new.append((v.rid, v.prompt_ids, v.params.__dict__.copy()))
+                    raw.append(item)
                 elif kind == "abort":
                     aborts.append(v)
                 elif kind == "stop":
                     stop = True
                 try:
-                    item = self.inbox.get_nowait()
+                    item = self._next_item(None)
                 except queue.Empty:
                     if not (block and self.batch_window_s > 0 and new and not stop) or time.perf_counter() > t_end \
                             or len(new) >= cap:
                         raise
-                    item = self.inbox.get(timeout=self.batch_window_s)
+                    item = self.inbox.get(timeout=self.batch_window_s * (4 if len(new) < expect else 1))
         except queue.Empty:
             pass
+        if new and not block and not stop and time.perf_counter() < t_end and self._near_drain():
+            # hold the arrivals back until the engine drains (or the cap): they join the next idle window
+            gone = set(aborts)
+            self._held = [it for it in raw if it[1].rid not in gone]
+            self._held_t = t_start
+            self.stats["admit_held"] += 0 if held else 1
+            new = []
+        elif new:
+            self._expect = max(0, expect - len(new))
         if block and new:
             self.stats["admit_windows"] += 1
             self.stats["admit_window_s"] += time.perf_counter() - t_start
@@ -405,6 +450,10 @@ class EngineDriver:
         h.finish_reason = reason
         if req is not None:
             h.metrics = req.metrics()
+        if reason not in ("error", "abort", "deadline"):  # a closed-loop client's next request is on its way
+            now = time.perf_counter()
+            self._expect = (self._expect if now - self._expect_t < self.resubmit_horizon_s else 0) + 1
+            self._expect_t = now
         if h.stream:
             h.tokens.put(None)
         if h.sink is not None:

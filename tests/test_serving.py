@@ -408,6 +408,75 @@ def test_admission_window_closes_when_slots_are_full(model_dir):
         drv.stop()
 
 
+def _own_driver(model_dir, **kw):
+    m = build_model(model_dir, None, "fp32", "cpu")
+    tok = load_tokenizer(model_dir, m.cfg.vocab_size)
+    eng = LLMEngine(m, max_num_seqs=8, block_size=4, num_blocks=256, eos_token_id=None, **kw)
+    return EngineDriver(eng), tok
+
+
+@pytest.mark.parametrize("expecting", [True, False])
+def test_admission_window_waits_longer_for_expected_resubmissions(model_dir, expecting):
+    """Closed-loop clients behind the pub/sub hops re-submit spread over more than one quiet period: after 4 replies,
+    4 arrivals in two groups 2.5 windows apart are still ONE prefill step (the window tolerates a 4x gap while fewer
+    arrivals than recent replies came). Without the expectation (horizon 0) the same arrivals take two steps."""
+    drv, tok = _own_driver(model_dir)
+    drv.batch_window_s = 0.04
+    drv.resubmit_horizon_s = 30.0 if expecting else 0.0
+    drv.start()
+    eng = drv.engine
+    try:
+        sp = SamplingParams(max_new_tokens=3, is_greedy=True)
+        hs = [drv.submit(encode(tok, f"first {i}"), sp) for i in range(4)]
+        assert all(h.wait(60) for h in hs)
+        time.sleep(0.2)  # the engine is idle again
+        before = eng.stats["prefill_steps"]
+        hs = [drv.submit(encode(tok, f"again {i}"), sp) for i in range(2)]
+        time.sleep(0.1)
+        hs += [drv.submit(encode(tok, f"again {i}"), sp) for i in range(2, 4)]
+        assert all(h.wait(60) for h in hs)
+        assert eng.stats["prefill_steps"] - before == (1 if expecting else 2), drv.stats
+    finally:
+        drv.stop()
+
+
+def test_admission_holds_arrivals_while_the_engine_is_about_to_drain(model_dir):
+    """Arrivals while every running sequence is within merge_steps tokens of its limit are held back and admitted
+    with the next idle window (with the re-submissions of the finishing sequences) - unless the cap runs out. Far
+    from the limit they are admitted at once. Driven by hand: no driver thread."""
+    drv, tok = _own_driver(model_dir)
+    eng = drv.engine
+    drv.merge_steps = 3
+    drv.batch_window_s, drv.batch_window_max = 0.01, 100000  # the hold cap cannot run out in this test
+    eng.add_request(encode(tok, "running"), SamplingParams(max_new_tokens=3, is_greedy=True))
+    eng.step()  # prefill: the sequence runs, 3 tokens or fewer left
+    h = drv.submit(encode(tok, "arrives"), SamplingParams(max_new_tokens=3, is_greedy=True))
+    msg = drv._collect(block=False)
+    assert msg["new"] == [] and [it[1].rid for it in drv._held] == [h.rid] and drv.stats["admit_held"] == 1
+    msg = drv._collect(block=False)  # still near the drain: still held, counted once
+    assert msg["new"] == [] and len(drv._held) == 1 and drv.stats["admit_held"] == 1
+    while eng.has_unfinished():
+        eng.step()
+    eng.pop_finished()
+    msg = drv._collect(block=True)
+    assert [r[0] for r in msg["new"]] == [h.rid] and not drv._held
+    # far from the limit: admitted at once
+    eng.add_request(encode(tok, "long"), SamplingParams(max_new_tokens=50, is_greedy=True))
+    eng.step()
+    h2 = drv.submit(encode(tok, "arrives 2"), SamplingParams(max_new_tokens=3, is_greedy=True))
+    assert [r[0] for r in drv._collect(block=False)["new"]] == [h2.rid]
+    # the cap: a hold never outlives batch_window_max windows from the first held arrival
+    drv2, _ = _own_driver(model_dir)
+    drv2.merge_steps, drv2.batch_window_s = 3, 0.001
+    drv2.engine.add_request(encode(tok, "running"), SamplingParams(max_new_tokens=3, is_greedy=True))
+    drv2.engine.step()
+    h3 = drv2.submit(encode(tok, "arrives 3"), SamplingParams(max_new_tokens=3, is_greedy=True))
+    drv2._held_t = time.perf_counter()
+    drv2._held = [drv2.inbox.get_nowait()]
+    time.sleep(0.05)
+    assert [r[0] for r in drv2._collect(block=False)["new"]] == [h3.rid] and not drv2._held
+
+
 def test_aio_server_stop_after_its_loop_ended(driver):
     """stop().wait() returns when the server's loop already ended (it used to schedule the stop onto the dead
     loop and wait forever)."""
