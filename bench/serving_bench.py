@@ -215,7 +215,9 @@ def main():
     res = json.loads(out.strip().splitlines()[-1])
     res.update(mode=a.mode, model=a.model, fp8=a.fp8, data="synthetic prompts, random-init weights",
                frontend=None if a.mode == "grpc" else ("in-process" if fe is None else "own process"),
-               prefill_chunk=eng.prefill_chunk, engine_stats=eng.stats)
+               prefill_chunk=eng.prefill_chunk, engine_stats=eng.stats,
+               driver_stats={k: v for k, v in drv.stats.items() if k.startswith("admit")},
+               admissions=list(drv.admit_log)[-48:])
     print(json.dumps(res), flush=True)
     # orderly shutdown: front-ends first, then the engine thread, then device state. A teardown that takes
     # over a minute dumps every thread's stack (a run once went silent here after printing its result)

@@ -1382,12 +1382,14 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
                      bool ilv = false);
 
 // tile: 1 = 128x128, 2 = 64x128, 3 = 64x64; ring depth 2-4; split-K over grid.y; 8-13: the gemm_mid tiles
-// (buffer-descriptor staging, csrc/gemm_mid.hip, fp8 MFMA variant; K % 128 == 0)
+// (buffer-descriptor staging, csrc/gemm_mid.hip, fp8 MFMA variant; K % 128 == 0; ilv: its software-pipelined
+// k-loop, >= 3 stages)
 // partial_out: a split plan without activation / GLU leaves its fp32 slabs [split, M, N] (scales applied, no
 // bias) in `workspace` for the consumer (rope_cache / add_norm sum them) and returns the split; else 0.
 int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq, int64_t ldw, const void* wsc,
                      const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, int tile,
-                     int depth, int split, void* workspace, int64_t ws_bytes, hipStream_t st, bool partial_out) {
+                     int depth, int split, void* workspace, int64_t ws_bytes, hipStream_t st, bool partial_out,
+                     bool ilv) {
   if (M == 0 || N == 0) return 0;
   if (K % 16) throw std::runtime_error("gemm_f8f8: K must be a multiple of 16");
   if (glu && (N % 32)) throw std::runtime_error("gemm_f8f8: glu needs N % 32 == 0");
@@ -1411,7 +1413,7 @@ int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq
   if (tile == 0) {  // auto: 128x128 when it fills the chip, else 64x128 / 64x64, split to >= ~256 WGs
     tile = ((M + 127) / 128) * ((N + 127) / 128) >= 240 ? 1 : (((M + 63) / 64) * ((N + 127) / 128) >= 240 ? 2 : 3);
     return launch_gemm_f8f8(xq, ldx, xs, wq, ldw, wsc, bias, y, ldy, M, N, K, act, glu, tile, depth, split, workspace,
-                            ws_bytes, st, partial_out);
+                            ws_bytes, st, partial_out, ilv);
   }
   if (split <= 0) {
     split = 1;
@@ -1434,7 +1436,7 @@ int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq
   gemm_f8f8_kernel<BM_, BN_, NS_><<<grid, 256, 0, st>>>(A, ldx, XS, Bw, ldw, WSc, Bi, Y, ldy, part, M, N, K, act_k, glu_k)
   if (mid) {
     launch_gemm_mid(tile, depth, M <= bm, (const bf16_t*)xq, ldx, (const bf16_t*)wq, ldw, Bi, Y, ldy, part, M, N, K,
-                    act_k, glu_k, split, st, nullptr, nullptr, XS, WSc);
+                    act_k, glu_k, split, st, nullptr, nullptr, XS, WSc, ilv);
   } else if (tile == 1) {
     if (depth >= 3) LF(128, 128, 3); else LF(128, 128, 2);
   } else if (tile == 2) {

@@ -179,16 +179,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
     else if (NS >= 3 && younger >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
-  if constexpr (ILV) {
-    static_assert(NS >= 3 && !F8 && MODE == 0, "interleaved ring: bf16 row-major weights, >= 3 stages");
-    static_assert((NS - 3) * LOADS <= 63, "vmcnt immediate");
-    constexpr int RPG = (MT + NT + MT - 1) / MT;  // fragment reads per group of NT MFMAs
-    constexpr int LPG = (LOADS + MT - 1) / MT;    // ring loads per group
-    // s_waitcnt vmcnt((NS - 3) * LOADS) lgkmcnt(0) through the builtin (the wait-count pass sees it): stage t+1
-    // landed with stages up to t+NS-2 in flight, and this wave's fragment reads are done
-    constexpr int VN = (NS - 3) * LOADS;
-    constexpr int WAIT_MID = (VN & 15) | (7 << 4) | ((VN >> 4) << 14);
-    // load l (< LOADS) of a ring stage: A rows first, then B rows
+  // load l (< LOADS) of a ring stage: A rows first, then B rows (the interleaved rings issue a stage piecewise)
 #define MID_LOAD1(L_, T_, SA_)                                                                                   \
   do {                                                                                                           \
     const int so_ = (T_) * 128;                                                                                  \
@@ -200,6 +191,87 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
                                                16, (uint32_t)vb[(L_) < AL ? 0 : (L_) - AL], (uint32_t)so_, 0,    \
                                                WNT ? 2 : 0);                                                     \
   } while (0)
+  if constexpr (ILV && F8) {
+    // fp8 software pipeline: a k-step is ONE 16x16x128 MFMA per (mt, nt), so it cannot be halved as in the bf16
+    // ring below. Instead k-step t+1's fragments are read into the other register set between k-step t's MFMAs,
+    // and ring stage t+NS-1 is issued among them. One barrier per k-step, at its start, once this wave's copy of
+    // stage t+1 landed: every wave is then past its reads of stage t-1 (done in step t-2), whose slot takes stage
+    // t+NS-1. The ring keeps NS-2 stages in flight ahead of the reads (NS-1 in the plain loop).
+    static_assert(NS >= 3 && MODE == 0, "fp8 interleaved ring: >= 3 stages");
+    static_assert((NS - 3) * LOADS <= 63, "vmcnt immediate");
+    constexpr int NR = 2 * (MT + NT);        // ds_read_b128 per k-step: lo / hi chunk of every A and B tile
+    constexpr int RPG = (NR + MT - 1) / MT;  // fragment reads per group of NT MFMAs
+    constexpr int LPG = (LOADS + MT - 1) / MT;
+    typedef int __attribute__((ext_vector_type(8))) i32x8_t;
+    u32x4 fr[2][NR];  // [register set][read]: A tile q -> 2q (lo), 2q + 1 (hi); B tile q -> 2 (MT + q) (+1)
+#define F8_RD(SET_, R_, SN_)                                                                                     \
+  fr[SET_][R_] = *reinterpret_cast<const u32x4*>(                                                                \
+      (SN_) + ((R_) / 2 < MT ? arow * 128 + ((R_) / 2) * 2048 : A_BYTES + brow * 128 + ((R_) / 2 - MT) * 2048) + \
+      (((R_) & 1) ? y1 : y0))
+#define F8_OP(SET_, Q_)                                                                                          \
+  __builtin_bit_cast(i32x8_t, __builtin_shufflevector(fr[SET_][2 * (Q_)], fr[SET_][2 * (Q_) + 1], 0, 1, 2, 3, 4, 5, 6, 7))
+    // k-step t on register set P_: MFMAs interleaved with (ISSUE_) stage t+NS-1's loads and (NEXT_) stage t+1's
+    // fragment reads into set P_ ^ 1
+#define F8_STEP(P_, ISSUE_, NEXT_)                                                                               \
+  do {                                                                                                           \
+    const int nx_ = cur == NS - 1 ? 0 : cur + 1;                                                                 \
+    const char* sn_ = smem + nx_ * STAGE;                                                                        \
+    char* sl_ = smem + (cur == 0 ? NS - 1 : cur - 1) * STAGE;                                                    \
+    if (NEXT_) {                                                                                                 \
+      ring_wait(min(t1 - 2 - t, NS - 3)); /* this wave's copy of stage t+1 landed ... */                         \
+      __builtin_amdgcn_s_barrier();       /* ... every wave's; every wave is past step t-1 */                    \
+      asm volatile("" ::: "memory");                                                                             \
+    }                                                                                                            \
+    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) {                                                          \
+      if (ISSUE_) {                                                                                              \
+        _Pragma("unroll") for (int l = mt * LPG; l < (mt + 1) * LPG && l < LOADS; ++l) MID_LOAD1(l, t + NS - 1, sl_); \
+      }                                                                                                          \
+      if (NEXT_) {                                                                                               \
+        _Pragma("unroll") for (int r = mt * RPG; r < (mt + 1) * RPG && r < NR; ++r) F8_RD((P_) ^ 1, r, sn_);     \
+      }                                                                                                          \
+      const i32x8_t a_ = F8_OP(P_, mt);                                                                          \
+      _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) acc[mt][nt] =                                            \
+          __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a_, F8_OP(P_, MT + nt), acc[mt][nt], 0, 0, 0, 127, 0, 127); \
+      __builtin_amdgcn_sched_barrier(0);                                                                         \
+    }                                                                                                            \
+    __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): the next step's fragments are in registers */             \
+    cur = nx_;                                                                                                   \
+    ++t;                                                                                                         \
+  } while (0)
+    int cur = 0, t = t0;
+    ring_wait(min(t1 - 1 - t0, NS - 2));  // stage t0 landed ...
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // ... for every wave
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int r = 0; r < NR; ++r) F8_RD(0, r, smem);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    int par = 0;  // register set holding the current step's fragments
+    // steady state, unrolled over the two register sets: every step issues a stage and reads the next one
+    while (true) {
+      if (t + NS - 1 >= t1) break;
+      F8_STEP(0, true, true);
+      if (t + NS - 1 >= t1) { par = 1; break; }
+      F8_STEP(1, true, true);
+    }
+    // the last (<= NS - 1) k-steps: nothing left to stage
+    while (t < t1) {
+      if (par == 0) F8_STEP(0, false, t + 1 < t1);
+      else F8_STEP(1, false, t + 1 < t1);
+      par ^= 1;
+    }
+#undef F8_STEP
+#undef F8_OP
+#undef F8_RD
+  } else if constexpr (ILV) {
+    static_assert(NS >= 3 && MODE == 0, "interleaved ring: bf16 row-major weights, >= 3 stages");
+    static_assert((NS - 3) * LOADS <= 63, "vmcnt immediate");
+    constexpr int RPG = (MT + NT + MT - 1) / MT;  // fragment reads per group of NT MFMAs
+    constexpr int LPG = (LOADS + MT - 1) / MT;    // ring loads per group
+    // s_waitcnt vmcnt((NS - 3) * LOADS) lgkmcnt(0) through the builtin (the wait-count pass sees it): stage t+1
+    // landed with stages up to t+NS-2 in flight, and this wave's fragment reads are done
+    constexpr int VN = (NS - 3) * LOADS;
+    constexpr int WAIT_MID = (VN & 15) | (7 << 4) | ((VN >> 4) << 14);
     s16x8 a0[MT], b0[NT], a1[MT], b1[NT];
     ring_wait(min(t1 - 1 - t0, NS - 2));  // stage t0 landed ...
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -403,7 +475,9 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
   if ((uint64_t)bm * ldx * 2 >= (1ull << 31) || (uint64_t)bn * ldw * 2 >= (1ull << 31))
     throw std::runtime_error("gemm_mid: row stride too large for 32-bit buffer offsets");
   const int ns = mid_depth(bm, bn, depth);
-  ilv = ilv && !f8 && ns >= 3 && K % 64 == 0;  // the interleaved ring's preconditions
+  // the interleaved rings' preconditions; the fp8 one holds two fragment sets, which 8-wave tiles (256 VGPRs per
+  // lane at two waves per SIMD) spill to scratch: 5-8x slower (profiles/r6_f8)
+  ilv = ilv && ns >= 3 && K % 64 == 0 && (!f8 || wm * wn <= 4);
   const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   dim3 grid(tiles, split);
 #define MID1(BM_, BN_, WM_, WN_, NS_, WNT_)                                                                        \
@@ -413,13 +487,18 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
 #define MID1F8(BM_, BN_, WM_, WN_, NS_, WNT_)                                                                      \
   gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, WNT_, true><<<grid, 64 * WM_ * WN_, 0, st>>>(                    \
       X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, cnt, qv, xs, wsc)
+#define MID1F8I(BM_, BN_, WM_, WN_, NS_, WNT_)                                                                     \
+  gemm_mid_kernel<BM_, BN_, WM_, WN_, (NS_ < 3 ? 3 : NS_), WNT_, true, 0, true><<<grid, 64 * WM_ * WN_, 0, st>>>( \
+      X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, cnt, qv, xs, wsc)
 #define MID1I(BM_, BN_, WM_, WN_, NS_, WNT_)                                                                       \
   gemm_mid_kernel<BM_, BN_, WM_, WN_, (NS_ < 3 ? 3 : NS_), WNT_, false, 0, true>                              \
       <<<grid, 64 * WM_ * WN_, 0, st>>>(X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, cnt, qv, nullptr,     \
                                         nullptr)
 #define MID(BM_, BN_, WM_, WN_, NS_)                                                                             \
   do {                                                                                                         \
-    if (f8) {                                                                                                  \
+    if (f8 && ilv && NS_ >= 3) {                                                                               \
+      if (wnt) MID1F8I(BM_, BN_, WM_, WN_, NS_, true); else MID1F8I(BM_, BN_, WM_, WN_, NS_, false);          \
+    } else if (f8) {                                                                                           \
       if (wnt) MID1F8(BM_, BN_, WM_, WN_, NS_, true); else MID1F8(BM_, BN_, WM_, WN_, NS_, false);            \
     } else if (ilv && NS_ >= 3) {                                                                              \
       if (wnt) MID1I(BM_, BN_, WM_, WN_, NS_, true); else MID1I(BM_, BN_, WM_, WN_, NS_, false);              \
@@ -454,6 +533,7 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
 #undef MID
 #undef MID1
 #undef MID1F8
+#undef MID1F8I
 #undef MID1I
   HIP_CHECK_LAUNCH();
 }

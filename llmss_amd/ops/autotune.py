@@ -60,6 +60,11 @@ def candidates(M: int, N: int, K: int, glu: bool, fp8: bool) -> List[Tuple[int, 
                 mt = [11, 10, 13, 15, 7] + ([8, 12] if M > 64 else []) + ([9] if M >= 256 else [])
                 out += [(W8A8_FLAG | (t << 8) | (d << 12), s) for t in mt for d in (3, 4)
                         for s in (1, 2, 3, 4, 5, 6, 8)]
+                if M >= ILV_MIN_M:  # their software-pipelined k-loop (W8A8_ILV), 3-5 stages, 4-wave tiles
+                    from .hip import W8A8_ILV
+
+                    out += [(W8A8_FLAG | W8A8_ILV | (t << 8) | (d << 12), s) for t in mt if t not in (9, 12)
+                            for d in (3, 4, 5) for s in (1, 2, 4) if (K // 128) // s >= 3]
             if M >= 256 and K % 128 == 0:
                 out.append((W8A8_FLAG | (4 << 8), 1))
         return out

@@ -383,11 +383,11 @@ class PartialSum:
 
 _FP8_PREFILL_M = 128  # untuned fp8 calls above this M run W8A8 (compute-bound); below, W8A16 weight streaming
 
-
-
 # nt_hint flag of a W8A8 plan (the tuned table's fp8 entries or an explicit hint): tile = (nt >> 8) & 15
-# (1 128x128, 2 64x128, 3 64x64, 4 256x256), ring depth = (nt >> 12) & 15, split-K = the plan's split
+# (1 128x128, 2 64x128, 3 64x64, 4 256x256, 7-15 the gemm_mid tiles), ring depth = (nt >> 12) & 15, split-K = the
+# plan's split; W8A8_ILV: the gemm_mid tiles' software-pipelined k-loop (the bf16 plans' interleave bit 512 << 8)
 W8A8_FLAG = 1 << 20
+W8A8_ILV = 512 << 8
 
 
 class _QuantScratch:
@@ -413,12 +413,8 @@ class _QuantScratch:
 _QSCRATCH = _Slotted(_QuantScratch)
 
 
-
-
-
-
 def linear_w8a8(x, wq, w_scale, bias=None, act="none", glu=False, out=None, tile=0, depth=0, split=0,
-                partial_ok=False):
+                partial_ok=False, ilv=False):
     """Y = (fp8(x) . wq^T) * x_scale[m] * w_scale[n] on the MX-fp8 MFMA (2x the bf16 matrix rate). The
     activations are quantised per token into a reusable scratch (graph-capturable). ``partial_ok``: a split
     plan may return its fp32 slabs as a :class:`PartialSum` for the consumer (rope_cache / add_norm)."""
@@ -447,7 +443,7 @@ def linear_w8a8(x, wq, w_scale, bias=None, act="none", glu=False, out=None, tile
         _bf16_rows(y, "out", nout)
     S = lib().gemm_f8f8(xq.data_ptr(), K, xs.data_ptr(), wq.data_ptr(), K, w_scale.data_ptr(), _ptr(bias), _ptr(y),
                         y.stride(0) if y is not None else nout, M, N, K, _ACT[act], bool(glu), int(tile), int(depth),
-                        int(split), ws.data_ptr(), ws.numel() * 4, _stream(), y is None)
+                        int(split), ws.data_ptr(), ws.numel() * 4, _stream(), y is None, bool(ilv))
     if y is None:
         if S <= 1:
             raise RuntimeError("internal: partial W8A8 GEMM did not produce partial slabs")
@@ -508,7 +504,7 @@ def linear(x, w, bias=None, act="none", glu=False, w_scale=None, out=None, nt_hi
             nt_hint, split_hint = tuned
         if nt_hint & W8A8_FLAG:
             return linear_w8a8(x, w, w_scale, bias, act, glu, out, (nt_hint >> 8) & 15, (nt_hint >> 12) & 15,
-                               split_hint, partial_ok=partial_ok)
+                               split_hint, partial_ok=partial_ok, ilv=bool(nt_hint & W8A8_ILV))
         if M > _FP8_PREFILL_M and not nt_hint and tuned is None:  # compute-bound: per-token fp8 activations
             return linear_w8a8(x, w, w_scale, bias, act, glu, out, partial_ok=partial_ok)  # on the MX-fp8 MFMA
     else:

@@ -28,6 +28,7 @@ ranks on several hosts fall back to it automatically.
 """
 from __future__ import annotations
 
+import collections
 import gc
 import os
 import queue
@@ -140,6 +141,8 @@ class EngineDriver:
         self._expect_t = 0.0
         self._held: list = []  # inbox items held back by the near-drain rule, oldest first
         self._held_t = 0.0
+        # the last admissions: (requests, engine was idle, window seconds, expected re-submissions) - diagnostics
+        self.admit_log: "collections.deque" = collections.deque(maxlen=128)
         self.fault = fault if fault is not None else FaultSpec.from_env()
         self.error: Optional[BaseException] = None
         self._last_bcast = time.perf_counter()
@@ -335,6 +338,7 @@ class EngineDriver:
             new = []
         elif new:
             self._expect = max(0, expect - len(new))
+            self.admit_log.append((len(new), block, round(time.perf_counter() - t_start, 4), expect))
         if block and new:
             self.stats["admit_windows"] += 1
             self.stats["admit_window_s"] += time.perf_counter() - t_start

@@ -829,3 +829,25 @@ def test_gemm_w8a8_mid_tiles(tile, depth, split, M, N, K):
         close(r, R.linear(xd, q, None, w_scale=s), 2e-2)
     else:
         close(p, R.linear(xd, q, None, w_scale=s), 2e-2)
+
+
+@pytest.mark.parametrize("tile,depth", [(8, 3), (8, 4), (8, 5), (11, 4), (9, 3), (12, 3), (13, 5), (15, 3)])
+@pytest.mark.parametrize("split", [1, 3])
+@pytest.mark.parametrize("M,N,K", [(512, 2752, 4096), (300, 544, 3072), (129, 1024, 640)])
+def test_gemm_w8a8_mid_tiles_software_pipelined(tile, depth, split, M, N, K):
+    """The fp8 gemm_mid k-loop with k-step t+1's fragment reads and the ring issue between k-step t's MFMAs
+    (W8A8_ILV): bit-identical to the plain loop (same MFMA order per accumulator) and to fp32 math on the same fp8
+    operands, through short K ranges per split (1-2 steps: the pipeline's prologue and tail alone) too."""
+    torch.manual_seed(0)
+    x, w, b = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
+    q, s = H.quant_fp8_rows(w)
+    xq, xs = H.quant_fp8_rows(x)
+    xd = R.dequant_fp8(xq, xs)
+    for glu in ([False] if tile in ODD_NT_TILES else [False, True]):
+        kw = dict(act="none" if glu else "gelu_tanh", glu=glu, tile=tile, depth=depth, split=split)
+        y = H.linear_w8a8(x, q, s, None if glu else b, ilv=True, **kw)
+        assert torch.equal(y, H.linear_w8a8(x, q, s, None if glu else b, **kw))
+        close(y, R.linear(xd, q, None if glu else b.float(), act=kw["act"], glu=glu, w_scale=s), 2e-2)
+    # through the nt_hint encoding a tuned plan carries
+    hint = H.W8A8_FLAG | H.W8A8_ILV | (tile << 8) | (depth << 12)
+    close(H.linear(x, q, b, w_scale=s, nt_hint=hint, split_hint=split), R.linear(xd, q, b.float(), w_scale=s), 2e-2)

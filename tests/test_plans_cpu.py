@@ -61,6 +61,16 @@ def test_interleaved_ring_candidates_only_where_the_kernel_takes_them():
     assert not ilv(A.candidates(512, 4096, 1376, False, False))  # partial last k-step
 
 
+def test_w8a8_software_pipelined_candidates_are_4_wave_gemm_mid_tiles():
+    """W8A8_ILV (the fp8 gemm_mid k-loop with the next step's reads between the MFMAs) is a candidate for M >= 128
+    on the 4-wave gemm_mid tiles only: the 8-wave ones spill its second fragment set (profiles/r6_f8)."""
+    from llmss_amd.ops.hip import W8A8_FLAG, W8A8_ILV
+
+    c = [(n, s) for n, s in A.candidates(512, 7168, 8192, True, True) if n & W8A8_FLAG and n & W8A8_ILV]
+    tiles = {(n >> 8) & 15 for n, _ in c}
+    assert 8 in tiles and 11 in tiles and not tiles & {9, 12} and tiles <= {7, 8, 10, 11, 13, 15}
+    assert all(3 <= (n >> 12) & 15 <= 5 for n, _ in c)
+    assert not [n for n, _ in A.candidates(64, 7168, 8192, True, True) if n & W8A8_FLAG and n & W8A8_ILV]
 
 
 @pytest.mark.parametrize("col", ["4", "0"])
