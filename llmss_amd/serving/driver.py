@@ -131,11 +131,14 @@ class EngineDriver:
         # over more than one quiet period and used to split into cohorts that never re-align (profiles/r5_pubsub).
         # Two bounded corrections, both inside the batch_window_max * batch_window_s cap:
         # * `_expect` counts the replies of the last `resubmit_horizon_s` not yet matched by an arrival; while a
-        #   window holds fewer arrivals than that, it tolerates a 4x longer gap between them.
+        #   window holds fewer arrivals than that, it tolerates a 4x longer gap between them and stays open up to
+        #   `resubmit_windows` windows instead of batch_window_max (GPT-2-XL over pub/sub: 64 re-submissions
+        #   arrive over 40-50 ms, profiles/r6_pubsub)
         # * near-drain hold: arrivals while every running sequence is within `merge_steps` tokens of its length
-        #   limit wait (at most the cap) for the engine to drain, so they prefill with the re-submissions of the
-        #   sequences about to finish instead of one step ahead of them.
+        #   limit wait (at most batch_window_max windows) for the engine to drain, so they prefill with the
+        #   re-submissions of the sequences about to finish instead of one step ahead of them.
         self.resubmit_horizon_s = 0.25
+        self.resubmit_windows = 25
         self.merge_steps = 2
         self._expect = 0
         self._expect_t = 0.0
@@ -323,10 +326,12 @@ class EngineDriver:
                 try:
                     item = self._next_item(None)
                 except queue.Empty:
-                    if not (block and self.batch_window_s > 0 and new and not stop) or time.perf_counter() > t_end \
+                    short = len(new) < expect  # replies whose re-submission has not arrived yet
+                    lim = t_start + self.resubmit_windows * self.batch_window_s if short else t_end
+                    if not (block and self.batch_window_s > 0 and new and not stop) or time.perf_counter() > lim \
                             or len(new) >= cap:
                         raise
-                    item = self.inbox.get(timeout=self.batch_window_s * (4 if len(new) < expect else 1))
+                    item = self.inbox.get(timeout=self.batch_window_s * (4 if short else 1))
         except queue.Empty:
             pass
         if new and not block and not stop and time.perf_counter() < t_end and self._near_drain():

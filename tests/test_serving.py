@@ -417,25 +417,29 @@ def _own_driver(model_dir, **kw):
 
 @pytest.mark.parametrize("expecting", [True, False])
 def test_admission_window_waits_longer_for_expected_resubmissions(model_dir, expecting):
-    """Closed-loop clients behind the pub/sub hops re-submit spread over more than one quiet period: after 4 replies,
-    4 arrivals in two groups 2.5 windows apart are still ONE prefill step (the window tolerates a 4x gap while fewer
-    arrivals than recent replies came). Without the expectation (horizon 0) the same arrivals take two steps."""
+    """Closed-loop clients behind the pub/sub hops re-submit spread over more than one quiet period: after 6 replies,
+    6 arrivals in groups 2.5 windows apart, 12.5 windows in all (past batch_window_max), are still ONE prefill step:
+    while fewer arrivals than recent replies came, the window tolerates a 4x gap and stays open up to
+    resubmit_windows. Without the expectation (horizon 0) the same arrivals take several steps."""
     drv, tok = _own_driver(model_dir)
-    drv.batch_window_s = 0.04
+    drv.batch_window_s = 0.02
     drv.resubmit_horizon_s = 30.0 if expecting else 0.0
     drv.start()
     eng = drv.engine
     try:
         sp = SamplingParams(max_new_tokens=3, is_greedy=True)
-        hs = [drv.submit(encode(tok, f"first {i}"), sp) for i in range(4)]
+        hs = [drv.submit(encode(tok, f"first {i}"), sp) for i in range(6)]
         assert all(h.wait(60) for h in hs)
         time.sleep(0.2)  # the engine is idle again
         before = eng.stats["prefill_steps"]
-        hs = [drv.submit(encode(tok, f"again {i}"), sp) for i in range(2)]
-        time.sleep(0.1)
-        hs += [drv.submit(encode(tok, f"again {i}"), sp) for i in range(2, 4)]
+        hs = []
+        for i in range(6):
+            if i:
+                time.sleep(0.05)
+            hs.append(drv.submit(encode(tok, f"again {i}"), sp))
         assert all(h.wait(60) for h in hs)
-        assert eng.stats["prefill_steps"] - before == (1 if expecting else 2), drv.stats
+        steps = eng.stats["prefill_steps"] - before
+        assert steps == 1 if expecting else steps >= 2, (steps, list(drv.admit_log))
     finally:
         drv.stop()
 
