@@ -3,7 +3,7 @@ one MI355X served over gRPC"; "pubsub producer/consumer under concurrent gRPC cl
 
   --mode grpc    clients -> gRPC Generate service on the engine driver (direct)
   --mode pubsub  clients -> gRPC front-end -> RESP broker (mini Redis) -> consumer -> engine
-                 (front-end and broker in their own process, as a producer server and Redis would be;
+                 (front-end and broker in a process each, as a producer server and Redis would be;
                  --frontend-inproc puts them in the engine process, sharing its interpreter lock)
 
 Random-init weights of the named architecture, random printable prompts (byte tokenizer: one
@@ -148,18 +148,29 @@ def main():
                     help="pubsub: run the broker and the gRPC front-end inside the engine process")
     ap.add_argument("--client-port", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--frontend", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--broker", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args()
 
-    if a.frontend:  # pub/sub front-end role: broker + gRPC BrokerServicer, no GPU; runs until stdin closes
-        from llmss_amd.serving.broker import MiniRedisServer, RedisBroker
-        from llmss_amd.serving.grpc_api import BrokerServicer, serve
+    if a.broker:  # pub/sub broker role (the Redis server): runs until stdin closes
+        from llmss_amd.serving.broker import MiniRedisServer
 
         mini = MiniRedisServer().start()
-        srv = serve(BrokerServicer(RedisBroker(mini.host, mini.port)), port=0, host="127.0.0.1")
-        print(f"{mini.port} {srv.bound_port}", flush=True)
+        print(mini.port, flush=True)
+        sys.stdin.read()
+        mini.stop()
+        return
+    if a.frontend:  # pub/sub front-end role: gRPC front-end on a broker in its own process; runs until stdin closes
+        from llmss_amd.serving.grpc_api import AioBrokerServicer, serve
+
+        br = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--broker"], stdin=subprocess.PIPE,
+                              stdout=subprocess.PIPE, text=True)
+        port = int(br.stdout.readline())
+        srv = serve(AioBrokerServicer("127.0.0.1", port), port=0, host="127.0.0.1")
+        print(f"{port} {srv.bound_port}", flush=True)
         sys.stdin.read()
         srv.stop(0).wait(30)
-        mini.stop()
+        br.stdin.close()
+        br.wait(30)
         return
 
     if a.client_port:
@@ -185,7 +196,7 @@ def main():
     from llmss_amd.serving.broker import MiniRedisServer, RedisBroker
     from llmss_amd.serving.consumer import Consumer
     from llmss_amd.serving.driver import EngineDriver
-    from llmss_amd.serving.grpc_api import BrokerServicer, EngineServicer, serve
+    from llmss_amd.serving.grpc_api import AioBrokerServicer, EngineServicer, serve
     from llmss_amd.utils.tokenizer import load_tokenizer
 
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
@@ -206,7 +217,7 @@ def main():
     else:
         mini = MiniRedisServer().start()
         consumer = Consumer(drv, tok, RedisBroker(mini.host, mini.port), poll_timeout=0.05).start()
-        srv = serve(BrokerServicer(RedisBroker(mini.host, mini.port)), port=0, host="127.0.0.1")
+        srv = serve(AioBrokerServicer(mini.host, mini.port), port=0, host="127.0.0.1")
         servers.append(srv)
         port = srv.bound_port
     out, _ = child.communicate(f"{port}\n", timeout=1800)

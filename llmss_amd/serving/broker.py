@@ -4,7 +4,7 @@
 * :class:`RedisBroker` - a minimal RESP2 client over a TCP socket (the ``redis`` package is not
   required); speaks to a real ``redis-server`` or to :class:`MiniRedisServer`.
 * :class:`MemoryBroker` - thread-safe in-process lists (tests, single-process serving).
-* :class:`MiniRedisServer` - a small threaded RESP server implementing the list commands the
+* :class:`MiniRedisServer` - a small single-threaded (asyncio) RESP server implementing the list commands the
   pub/sub path needs (LPUSH/RPUSH/LPOP/RPOP/LLEN/BRPOP/BLPOP/RPOPLPUSH/BRPOPLPUSH/LREM/LRANGE/DEL/PING), so the
   PoC runs where no ``redis-server`` is installed.
 
@@ -17,10 +17,9 @@ Blocking pops (``brpop``) replace the reference's busy ``while True: if llen: rp
 from __future__ import annotations
 
 import socket
-import socketserver
 import threading
 import time
-from collections import defaultdict, deque
+from collections import deque
 from typing import Dict, List, Optional, Tuple
 
 PQUEUE = "pqueue"
@@ -88,92 +87,113 @@ class Broker:
 
 # ------------------------------------------------------------------------------- in-memory
 class MemoryBroker(Broker):
+    """Thread-safe in-process lists. A blocking pop waits on its key's own condition, so a push wakes only the
+    waiters of that key: with one shared condition every push woke every blocked pop (the pub/sub front-end's 64
+    reply waiters: 64 x 64 wake-ups per batch of replies, each taking the interpreter lock - 60-75 ms for a
+    GPT-2-XL cohort's re-submissions to get through, profiles/r6_pubsub). A list that empties is deleted, as in
+    Redis, so one-shot reply keys leave nothing behind."""
+
     def __init__(self):
-        self._lists: Dict[str, deque] = defaultdict(deque)
-        self._cv = threading.Condition()
+        self._lists: Dict[str, deque] = {}
+        self._lock = threading.Lock()
+        self._waiters: Dict[str, list] = {}  # key -> [Condition on self._lock, number of waiting threads]
+
+    def _push(self, key, value, left):  # lock held
+        q = self._lists.get(key)
+        if q is None:
+            q = self._lists[key] = deque()
+        if left:
+            q.appendleft(value)
+        else:
+            q.append(value)
+        w = self._waiters.get(key)
+        if w is not None:
+            w[0].notify()  # one element satisfies one pop
+        return len(q)
+
+    def _pop(self, key, right=True):  # lock held
+        q = self._lists.get(key)
+        if not q:
+            return None
+        v = q.pop() if right else q.popleft()
+        if not q:
+            del self._lists[key]
+        return v
+
+    def _wait(self, key, rem):  # lock held; False once the deadline has passed
+        if rem is not None and rem <= 0:
+            return False
+        w = self._waiters.get(key)
+        if w is None:
+            w = self._waiters[key] = [threading.Condition(self._lock), 0]
+        w[1] += 1
+        try:
+            w[0].wait(rem)
+        finally:
+            w[1] -= 1
+            if w[1] == 0:
+                del self._waiters[key]
+        return True
+
+    def _blocking(self, key, timeout, take):
+        deadline = None if not timeout else time.monotonic() + timeout
+        with self._lock:
+            while True:
+                v = take()
+                if v is not None:
+                    w = self._waiters.get(key)
+                    if w is not None and self._lists.get(key):
+                        w[0].notify()  # more elements left than this pop took: pass the wake-up on
+                    return v
+                if not self._wait(key, None if deadline is None else deadline - time.monotonic()):
+                    return None
 
     def lpush(self, key, value):
-        with self._cv:
-            self._lists[key].appendleft(value)
-            self._cv.notify_all()
-            return len(self._lists[key])
+        with self._lock:
+            return self._push(key, value, True)
 
     def rpush(self, key, value):
-        with self._cv:
-            self._lists[key].append(value)
-            self._cv.notify_all()
-            return len(self._lists[key])
+        with self._lock:
+            return self._push(key, value, False)
 
     def rpop(self, key):
-        with self._cv:
-            q = self._lists.get(key)
-            return q.pop() if q else None
+        with self._lock:
+            return self._pop(key)
 
     def lpop(self, key):
-        with self._cv:
-            q = self._lists.get(key)
-            return q.popleft() if q else None
+        with self._lock:
+            return self._pop(key, right=False)
 
     def llen(self, key):
-        with self._cv:
+        with self._lock:
             return len(self._lists.get(key, ()))
 
     def brpop(self, key, timeout=0):
-        deadline = None if not timeout else time.monotonic() + timeout
-        with self._cv:
-            while True:
-                q = self._lists.get(key)
-                if q:
-                    return q.pop()
-                rem = None if deadline is None else deadline - time.monotonic()
-                if rem is not None and rem <= 0:
-                    return None
-                self._cv.wait(rem)
+        return self._blocking(key, timeout, lambda: self._pop(key))
 
     def blpop(self, key, timeout=0):
-        deadline = None if not timeout else time.monotonic() + timeout
-        with self._cv:
-            while True:
-                q = self._lists.get(key)
-                if q:
-                    return q.popleft()
-                rem = None if deadline is None else deadline - time.monotonic()
-                if rem is not None and rem <= 0:
-                    return None
-                self._cv.wait(rem)
+        return self._blocking(key, timeout, lambda: self._pop(key, right=False))
 
     def delete(self, key):
-        with self._cv:
+        with self._lock:
             return 1 if self._lists.pop(key, None) is not None else 0
 
+    def _move(self, src, dst):  # lock held
+        v = self._pop(src)
+        if v is not None:
+            self._push(dst, v, True)
+        return v
+
     def brpoplpush(self, src, dst, timeout=0):
-        deadline = None if not timeout else time.monotonic() + timeout
-        with self._cv:
-            while True:
-                q = self._lists.get(src)
-                if q:
-                    v = q.pop()
-                    self._lists[dst].appendleft(v)
-                    self._cv.notify_all()
-                    return v
-                rem = None if deadline is None else deadline - time.monotonic()
-                if rem is not None and rem <= 0:
-                    return None
-                self._cv.wait(rem)
+        return self._blocking(src, timeout, lambda: self._move(src, dst))
 
     def rpoplpush(self, src, dst):
-        with self._cv:
-            q = self._lists.get(src)
-            if not q:
-                return None
-            v = q.pop()
-            self._lists[dst].appendleft(v)
-            self._cv.notify_all()
-            return v
+        with self._lock:
+            return self._move(src, dst)
 
     def lrem(self, key, count, value):
         """Remove up to ``count`` occurrences of ``value`` (0 = all; < 0 = from the tail), like Redis."""
-        with self._cv:
+        with self._lock:
             q = self._lists.get(key)
             if not q:
                 return 0
@@ -184,11 +204,15 @@ class MemoryBroker(Broker):
             elif count > 0:
                 idx = idx[:count]
             drop = set(idx)
-            self._lists[key] = deque(v for i, v in enumerate(items) if i not in drop)
+            rest = deque(v for i, v in enumerate(items) if i not in drop)
+            if rest:
+                self._lists[key] = rest
+            else:
+                del self._lists[key]
             return len(drop)
 
     def lrange(self, key, start, stop):
-        with self._cv:
+        with self._lock:
             items = list(self._lists.get(key, ()))
         n = len(items)
         start = max(0, start + n if start < 0 else start)
@@ -337,103 +361,240 @@ class RedisBroker(Broker):
             self._local.conn = None
 
 
+class AsyncRedisClient:
+    """asyncio RESP client for coroutine front-ends (:class:`~llmss_amd.serving.grpc_api.AioBrokerServicer`): the
+    commands of every in-flight request run on the server's event loop, not in a thread each. A pool of
+    connections, one per concurrently blocked command (a BRPOP holds its connection until its reply); a command
+    that is cancelled or fails closes its connection, whose reply stream is then out of step."""
+
+    def __init__(self, host: str = "127.0.0.1", port: int = 6379):
+        self.host, self.port = host, int(port)
+        self._free: list = []
+
+    async def execute(self, *args):
+        import asyncio
+
+        conn = self._free.pop() if self._free else None
+        if conn is None:
+            conn = await asyncio.open_connection(self.host, self.port)
+            conn[1].get_extra_info("socket").setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        rd, wr = conn
+        ok = False
+        try:
+            wr.write(_encode(*args))
+            out = await self._value(rd)
+            ok = True
+            return out
+        finally:
+            if ok:
+                self._free.append(conn)
+            else:
+                wr.close()
+
+    async def _value(self, rd):
+        ln = (await rd.readuntil(b"\r\n"))[:-2]
+        t, rest = ln[:1], ln[1:]
+        if t == b"+":
+            return rest.decode()
+        if t == b"-":
+            raise RuntimeError(rest.decode())
+        if t == b":":
+            return int(rest)
+        if t == b"$":
+            n = int(rest)
+            return None if n < 0 else (await rd.readexactly(n + 2))[:-2].decode("utf-8")
+        if t == b"*":
+            n = int(rest)
+            return None if n < 0 else [await self._value(rd) for _ in range(n)]
+        raise RuntimeError(f"bad RESP type {t!r}")
+
+    async def lpush(self, key, value):
+        return await self.execute("LPUSH", key, value)
+
+    async def brpop(self, key, timeout=0):
+        r = await self.execute("BRPOP", key, _fmt_timeout(timeout))
+        return None if r is None else r[1]
+
+    def close(self):
+        for _, wr in self._free:
+            wr.close()
+        self._free.clear()
+
+
 def _fmt_timeout(t: float) -> str:
     return str(int(t)) if float(t).is_integer() else f"{t:.3f}"
 
 
 # ------------------------------------------------------------------------------- mini server
 class MiniRedisServer:
-    """Threaded RESP server over a :class:`MemoryBroker` (subset of Redis list commands)."""
+    """RESP server for the list commands of the pub/sub path, on ONE asyncio event-loop thread as Redis itself
+    runs: a connection is a coroutine, a blocked pop a future parked on its key, and a push hands its element to
+    the oldest parked pop of that key directly. The thread-per-connection server it replaces spent most of a
+    cohort's turnaround handing the interpreter lock between its 64+ connection threads and the front-end's
+    handlers (bench/pubsub_rtt.py, profiles/r6_pubsub)."""
 
     def __init__(self, host: str = "127.0.0.1", port: int = 0):
-        self.store = MemoryBroker()
-        store = self.store
+        import asyncio
 
-        class Handler(socketserver.BaseRequestHandler):
-            def handle(self):
-                sock = self.request
-                sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                rd = _Reader(sock)
-                while True:
-                    try:
-                        cmd = rd.value()
-                    except (ConnectionError, OSError):
-                        return
-                    try:
-                        resp = MiniRedisServer._dispatch(store, cmd)
-                    except Exception as e:  # noqa: BLE001
-                        resp = RuntimeError(str(e))
-                    try:
-                        sock.sendall(MiniRedisServer._reply(resp))
-                    except OSError:
-                        return
+        self._lists: Dict[str, deque] = {}
+        self._waiters: Dict[str, deque] = {}  # key -> parked pops: (future, take) with take(key) -> value
+        self._sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        self._sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        self._sock.bind((host, port))
+        self._sock.listen(512)
+        self.host, self.port = self._sock.getsockname()[:2]
+        self.loop = asyncio.new_event_loop()
+        self._thread = threading.Thread(target=self._run, daemon=True, name="mini-redis")
+        self._server = None
+        self._conns: set = set()
 
-        class Server(socketserver.ThreadingMixIn, socketserver.TCPServer):
-            daemon_threads = True
-            allow_reuse_address = True
+    # list store (event-loop thread only)
+    def _push(self, key, value, left):
+        q = self._lists.get(key)
+        if q is None:
+            q = self._lists[key] = deque()
+        q.appendleft(value) if left else q.append(value)
+        n = len(q)
+        self._serve_waiters(key)
+        return n
 
-        self.server = Server((host, port), Handler)
-        self.host, self.port = self.server.server_address
-        self._thread = threading.Thread(target=self.server.serve_forever, daemon=True)
+    def _pop(self, key, right=True):
+        q = self._lists.get(key)
+        if not q:
+            return None
+        v = q.pop() if right else q.popleft()
+        if not q:
+            del self._lists[key]
+        return v
 
-    @staticmethod
-    def _dispatch(store: MemoryBroker, cmd: List[str]):
+    def _serve_waiters(self, key):
+        ws = self._waiters.get(key)
+        while ws and self._lists.get(key):
+            fut, take = ws.popleft()
+            if not fut.done():
+                fut.set_result(take(key))
+        if ws is not None and not ws:
+            del self._waiters[key]
+
+    async def _blocking(self, keys, timeout, take):
+        import asyncio
+
+        for k in keys:
+            if self._lists.get(k):
+                return k, take(k)
+        fut = self.loop.create_future()
+        for k in keys:
+            self._waiters.setdefault(k, deque()).append((fut, lambda key, k=k: (k, take(key))))
+        try:
+            return await (asyncio.wait_for(fut, timeout) if timeout > 0 else fut)
+        except asyncio.TimeoutError:
+            return None
+        finally:
+            for k in keys:  # drop this pop's parked entries (served, timed out or cancelled)
+                ws = self._waiters.get(k)
+                if ws is not None:
+                    rest = deque(w for w in ws if w[0] is not fut)
+                    if rest:
+                        self._waiters[k] = rest
+                    else:
+                        del self._waiters[k]
+
+    def _move(self, src, dst):
+        v = self._pop(src)
+        if v is not None:
+            self._push(dst, v, True)
+        return v
+
+    def _lrem(self, key, count, value):
+        q = self._lists.get(key)
+        if not q:
+            return 0
+        items = list(q)
+        idx = [i for i, v in enumerate(items) if v == value]
+        idx = idx[::-1][:-count] if count < 0 else (idx[:count] if count > 0 else idx)
+        drop = set(idx)
+        rest = deque(v for i, v in enumerate(items) if i not in drop)
+        if rest:
+            self._lists[key] = rest
+        else:
+            del self._lists[key]
+        return len(drop)
+
+    def _lrange(self, key, start, stop):
+        items = list(self._lists.get(key, ()))
+        n = len(items)
+        start = max(0, start + n if start < 0 else start)
+        stop = stop + n if stop < 0 else stop
+        return items[start:stop + 1]
+
+    async def _exec(self, cmd):
         if not isinstance(cmd, list) or not cmd:
             raise RuntimeError("ERR protocol")
         op = cmd[0].upper()
         a = cmd[1:]
         if op == "PING":
             return "PONG"
-        if op == "LPUSH":
+        if op in ("LPUSH", "RPUSH"):
             n = 0
             for v in a[1:]:
-                n = store.lpush(a[0], v)
+                n = self._push(a[0], v, op == "LPUSH")
             return n
-        if op == "RPUSH":
-            n = 0
-            for v in a[1:]:
-                n = store.rpush(a[0], v)
-            return n
-        if op == "RPOP":
-            return ("bulk", store.rpop(a[0]))
-        if op == "LPOP":
-            return ("bulk", store.lpop(a[0]))
+        if op in ("RPOP", "LPOP"):
+            return ("bulk", self._pop(a[0], op == "RPOP"))
         if op == "LLEN":
-            return store.llen(a[0])
+            return len(self._lists.get(a[0], ()))
         if op in ("BRPOP", "BLPOP"):
-            keys, t = a[:-1], float(a[-1])
-            fn = store.brpop if op == "BRPOP" else store.blpop
-            deadline = None if t == 0 else time.monotonic() + t
-            while True:  # poll the keys in order (subset of Redis semantics, fine for one key)
-                for k in keys:
-                    v = (store.rpop if op == "BRPOP" else store.lpop)(k)
-                    if v is not None:
-                        return ("array", [k, v])
-                rem = None if deadline is None else deadline - time.monotonic()
-                if rem is not None and rem <= 0:
-                    return ("array", None)
-                v = fn(keys[0], min(rem, 0.05) if rem is not None else 0.05)
-                if v is not None:
-                    return ("array", [keys[0], v])
-        if op == "DEL":
-            return sum(store.delete(k) for k in a)
+            r = await self._blocking(a[:-1], float(a[-1]), lambda k: self._pop(k, op == "BRPOP"))
+            return ("array", None if r is None else [r[0], r[1]])
         if op == "BRPOPLPUSH":
-            t = float(a[2])
-            deadline = None if t == 0 else time.monotonic() + t
-            while True:  # bounded waits so a stopping server is not held by an idle client
-                rem = None if deadline is None else deadline - time.monotonic()
-                if rem is not None and rem <= 0:
-                    return ("bulk", None)
-                v = store.brpoplpush(a[0], a[1], min(rem, 0.05) if rem is not None else 0.05)
-                if v is not None:
-                    return ("bulk", v)
+            r = await self._blocking([a[0]], float(a[2]), lambda k: self._move(k, a[1]))
+            return ("bulk", None if r is None else r[1])
         if op == "RPOPLPUSH":
-            return ("bulk", store.rpoplpush(a[0], a[1]))
+            return ("bulk", self._move(a[0], a[1]))
+        if op == "DEL":
+            return sum(1 for k in a if self._lists.pop(k, None) is not None)
         if op == "LREM":
-            return store.lrem(a[0], int(a[1]), a[2])
+            return self._lrem(a[0], int(a[1]), a[2])
         if op == "LRANGE":
-            return ("array", store.lrange(a[0], int(a[1]), int(a[2])))
+            return ("array", self._lrange(a[0], int(a[1]), int(a[2])))
         raise RuntimeError(f"ERR unknown command {op}")
+
+    async def _command(self, rd):
+        ln = (await rd.readuntil(b"\r\n"))[:-2]
+        if ln[:1] != b"*":
+            raise RuntimeError("ERR protocol")
+        out = []
+        for _ in range(int(ln[1:])):
+            hd = (await rd.readuntil(b"\r\n"))[:-2]
+            if hd[:1] != b"$":
+                raise RuntimeError("ERR protocol")
+            out.append((await rd.readexactly(int(hd[1:]) + 2))[:-2].decode("utf-8"))
+        return out
+
+    async def _client(self, rd, wr):
+        import asyncio
+
+        wr.get_extra_info("socket").setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        task = asyncio.current_task()
+        self._conns.add(task)
+        try:
+            while True:
+                try:
+                    cmd = await self._command(rd)
+                except (asyncio.IncompleteReadError, ConnectionError, RuntimeError):
+                    return
+                try:
+                    resp = await self._exec(cmd)
+                except Exception as e:  # noqa: BLE001 - an error reply; the connection stays in step
+                    resp = RuntimeError(str(e))
+                wr.write(self._reply(resp))
+                if not rd._buffer:  # noqa: SLF001 - pipelined commands still buffered: answer them first
+                    await wr.drain()
+        except (ConnectionError, OSError):
+            return
+        finally:
+            self._conns.discard(task)
+            wr.close()
 
     @staticmethod
     def _reply(r) -> bytes:
@@ -453,13 +614,37 @@ class MiniRedisServer:
             return b"*-1\r\n"
         return b"".join([b"*%d\r\n" % len(v)] + [MiniRedisServer._reply(("bulk", x)) for x in v])
 
+    def _run(self):
+        import asyncio
+
+        asyncio.set_event_loop(self.loop)
+
+        async def main():
+            self._server = await asyncio.start_server(self._client, sock=self._sock)
+
+        self.loop.run_until_complete(main())
+        self.loop.run_forever()
+        for t in list(self._conns):  # stop(): end the connection coroutines, then close the loop
+            t.cancel()
+        if self._conns:
+            self.loop.run_until_complete(asyncio.gather(*self._conns, return_exceptions=True))
+        self.loop.close()
+
     def start(self):
         self._thread.start()
         return self
 
     def stop(self):
-        self.server.shutdown()
-        self.server.server_close()
+        def _close():
+            if self._server is not None:
+                self._server.close()
+            self.loop.stop()
+
+        if self._thread.is_alive():
+            self.loop.call_soon_threadsafe(_close)
+            self._thread.join(10)
+        else:
+            self._sock.close()
 
 
 def make_broker(host: Optional[str], port: Optional[int]) -> Broker:

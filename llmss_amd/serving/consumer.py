@@ -156,11 +156,21 @@ class Consumer:
     def intake_loop(self):
         """Rank 0: broker -> engine (non-spinning blocking pop, then the rest of the queue in one pipeline)."""
         pk = processing_key(self.consumer_id)
+        backoff = 0.05
         while not self._stop.is_set():
-            if self.durable:
-                msg = self.broker.brpoplpush(PQUEUE, pk, timeout=self.poll_timeout)
-            else:
-                msg = self.broker.brpop(PQUEUE, timeout=self.poll_timeout)
+            try:
+                if self.durable:
+                    msg = self.broker.brpoplpush(PQUEUE, pk, timeout=self.poll_timeout)
+                else:
+                    msg = self.broker.brpop(PQUEUE, timeout=self.poll_timeout)
+            except (ConnectionError, OSError) as e:  # broker restarting / gone: reconnect on the next pop
+                if self._stop.is_set():
+                    return
+                log.warning("consumer intake: broker unreachable (%s); retrying in %.2f s", e, backoff)
+                self._stop.wait(backoff)
+                backoff = min(2 * backoff, 2.0)
+                continue
+            backoff = 0.05
             if msg is None:
                 continue
             msgs = [msg]

@@ -48,7 +48,7 @@ def _serve_replicas(driver, tok, args):
 
     from .broker import MiniRedisServer, RedisBroker
     from .consumer import Consumer
-    from .grpc_api import BrokerServicer
+    from .grpc_api import AioBrokerServicer
 
     g = driver.tp
     broker_srv = None
@@ -60,7 +60,7 @@ def _serve_replicas(driver, tok, args):
         # one processing list per replica (durable hand-off, consumer.py)
         Consumer(driver, tok, RedisBroker("127.0.0.1", args.broker_port), consumer_id=f"replica{g.replica}").start()
     if g.global_rank == 0:
-        server = serve(BrokerServicer(RedisBroker("127.0.0.1", args.broker_port)), args.grpc_port, args.grpc_host)
+        server = serve(AioBrokerServicer("127.0.0.1", args.broker_port), args.grpc_port, args.grpc_host)
         print(f"llmss gRPC Generate on {args.grpc_host}:{server.bound_port}: {g.dp} replicas x tp={g.size}", flush=True)
     driver.run()
 

@@ -26,7 +26,7 @@ def main(argv=None):
     import uvicorn
 
     from llmss_amd.serving.broker import MiniRedisServer, RedisBroker
-    from llmss_amd.serving.grpc_api import BrokerServicer, serve
+    from llmss_amd.serving.grpc_api import AioBrokerServicer, serve
     from llmss_amd.serving.producer import create_app
 
     args = get_args(argv)
@@ -34,7 +34,7 @@ def main(argv=None):
         MiniRedisServer(args.redis_host, args.redis_port).start()
     broker = RedisBroker(args.redis_host, args.redis_port)
     if args.grpc_port:
-        serve(BrokerServicer(broker), args.grpc_port)
+        serve(AioBrokerServicer(args.redis_host, args.redis_port), args.grpc_port)
     uvicorn.run(create_app(broker), host=args.fastapi_host, port=args.fastapi_port)
 
 

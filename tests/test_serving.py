@@ -47,6 +47,45 @@ def test_broker_list_semantics(kind):
         srv.stop()
 
 
+def test_memory_broker_wakes_each_key_and_leaves_no_empty_keys():
+    """64 blocked pops on 64 reply keys: each push wakes its own key's waiter (per-key conditions, not one shared
+    condition that every push broadcast to all waiters), every waiter gets its own value, several values on one key
+    go to several waiters, and emptied lists / waiter records are deleted (one-shot reply keys leave nothing)."""
+    b = MemoryBroker()
+    got = {}
+
+    def wait(i):
+        got[i] = b.brpop(f"squeue:{i}", 10)
+
+    ths = [threading.Thread(target=wait, args=(i,)) for i in range(64)]
+    for t in ths:
+        t.start()
+    deadline = time.time() + 10
+    while sum(w[1] for w in list(b._waiters.values())) < 64 and time.time() < deadline:
+        time.sleep(0.01)
+    assert len(b._waiters) == 64
+    b.pipeline([("LPUSH", f"squeue:{i}", f"v{i}") for i in range(64)])
+    for t in ths:
+        t.join(10)
+    assert got == {i: f"v{i}" for i in range(64)}
+    assert not b._lists and not b._waiters
+    # three waiters, one key, three values; brpoplpush moves and wakes the destination's waiter
+    out = []
+    ths = [threading.Thread(target=lambda: out.append(b.brpop("k", 10))) for _ in range(3)]
+    for t in ths:
+        t.start()
+    for v in ("a", "b", "c"):
+        b.lpush("k", v)
+    for t in ths:
+        t.join(10)
+    assert sorted(out) == ["a", "b", "c"] and not b._lists
+    b.lpush("src", "x")
+    assert b.brpoplpush("src", "proc", 1) == "x" and b.lrange("proc", 0, -1) == ["x"]
+    assert b.lrem("proc", 0, "x") == 1 and not b._lists and b.llen("proc") == 0
+    t0 = time.time()
+    assert b.brpop("none", 0.2) is None and 0.15 < time.time() - t0 < 5 and not b._waiters
+
+
 @pytest.fixture(scope="module")
 def model_dir(tmp_path_factory):
     d = str(tmp_path_factory.mktemp("gpt2tok"))
@@ -109,6 +148,29 @@ def test_producer_consumer_http(driver):
     assert "llmss_producer_completed 6" in client.get("/metrics").text
     consumer.stop()
     srv.stop()
+
+
+def test_consumer_survives_a_broker_restart(driver):
+    """The consumer's intake reconnects when the broker goes away and comes back on the same port (a Redis
+    restart): the request pushed after the restart is served, and the intake thread never dies."""
+    drv, tok, m = driver
+    srv = MiniRedisServer().start()
+    port = srv.port
+    consumer = Consumer(drv, tok, RedisBroker("127.0.0.1", port), poll_timeout=0.05, durable=False).start()
+    try:
+        time.sleep(0.2)
+        srv.stop()
+        time.sleep(0.3)  # the intake sees the connection drop and backs off
+        assert consumer._intake.is_alive()
+        srv = MiniRedisServer("127.0.0.1", port).start()
+        b = RedisBroker("127.0.0.1", port)
+        b.lpush(PQUEUE, json.dumps({"prompt": "hello", "max_new_tokens": 3, "is_greedy": True, "temperature": 1.0,
+                                    "top_p": 0.95, "top_k": 50, "request_id": "after"}))
+        d = json.loads(b.brpop(reply_key("after"), 30))
+        assert d["continuation"] == _offline(m, tok, "hello", 3)
+    finally:
+        consumer.stop()
+        srv.stop()
 
 
 def test_reference_format_interop(driver):
