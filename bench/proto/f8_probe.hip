@@ -72,7 +72,7 @@ int main() {
             auto run = [&](int i, bf16_t* y) {
               launch_gemm_mid(c.tsel, depth, false, (const bf16_t*)X, s.K, (const bf16_t*)ws[i % ncopy], s.K, nullptr,
                               y, s.glu ? s.N / 2 : s.N, split > 1 ? part : nullptr, s.M, s.N, s.K, 0, s.glu, split, st,
-                              nullptr, nullptr, xs, wsc, ilv != 0);
+                              nullptr, nullptr, xs, wsc, ilv != 0, nullptr);
             };
             hipGraph_t g;
             hipGraphExec_t ge;

@@ -30,7 +30,7 @@ static void launch(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* part, int
                    hipStream_t st) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   gemm_mid_kernel<BM, BN, WM, WN, NS, false, false, MODE><<<dim3(tiles, split), 64 * WM * WN, 0, st>>>(
-      X, K, W, K, nullptr, Y, N, split > 1 ? part : nullptr, M, N, K, 0, 0, nullptr, QkvEpi{}, nullptr, nullptr);
+      X, K, W, K, nullptr, Y, N, split > 1 ? part : nullptr, M, N, K, 0, 0, nullptr, QkvEpi{}, nullptr, nullptr, nullptr);
 }
 
 using Fn = void (*)(const bf16_t*, const bf16_t*, bf16_t*, float*, int, int, int, int, hipStream_t);

@@ -54,7 +54,7 @@ void gemm_set_slot(int s);
 int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq, int64_t ldw, const void* wsc,
                      const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, int tile,
                      int depth, int split, void* workspace, int64_t ws_bytes, hipStream_t st, bool partial_out,
-                     bool ilv);
+                     bool ilv, void* mxq, void* mxs, const void* asc);
 int gemm_f8f8_partial_slabs(int M, int N, int K, bool glu, int act, int tile, int split, int64_t ws_bytes);
 int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int nt_hint, int split_hint,
                        int64_t ws_bytes);
@@ -162,14 +162,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_set_slot", &gemm_set_slot);
   m.def("gemm_f8f8", [](uintptr_t xq, int64_t ldx, uintptr_t xs, uintptr_t wq, int64_t ldw, uintptr_t wsc,
                         uintptr_t bias, uintptr_t y, int64_t ldy, int M, int N, int K, int act, bool glu, int tile,
-                        int depth, int split, uintptr_t work, int64_t wbytes, uintptr_t st, bool partial_out, bool ilv) {
+                        int depth, int split, uintptr_t work, int64_t wbytes, uintptr_t st, bool partial_out, bool ilv,
+                        uintptr_t mxq, uintptr_t mxs, uintptr_t asc) {
     return launch_gemm_f8f8(CP(xq), ldx, CP(xs), CP(wq), ldw, CP(wsc), CP(bias), P(y), ldy, M, N, K, act, glu, tile,
-                            depth, split, P(work), wbytes, S(st), partial_out, ilv);
+                            depth, split, P(work), wbytes, S(st), partial_out, ilv, P(mxq), P(mxs), CP(asc));
   }, pybind11::arg("xq"), pybind11::arg("ldx"), pybind11::arg("xs"), pybind11::arg("wq"), pybind11::arg("ldw"),
      pybind11::arg("wsc"), pybind11::arg("bias"), pybind11::arg("y"), pybind11::arg("ldy"), pybind11::arg("M"),
      pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("act"), pybind11::arg("glu"), pybind11::arg("tile"),
      pybind11::arg("depth"), pybind11::arg("split"), pybind11::arg("work"), pybind11::arg("wbytes"),
-     pybind11::arg("st"), pybind11::arg("partial_out") = false, pybind11::arg("ilv") = false);
+     pybind11::arg("st"), pybind11::arg("partial_out") = false, pybind11::arg("ilv") = false,
+     pybind11::arg("mxq") = 0, pybind11::arg("mxs") = 0, pybind11::arg("asc") = 0);
   m.def("gemm_f8f8_partial_slabs", &gemm_f8f8_partial_slabs);
   m.def("gemm_partial_slabs", &gemm_partial_slabs);
   m.def("attn_decode_set_unroll", &attn_decode_set_unroll);

@@ -175,6 +175,11 @@ __device__ __forceinline__ TileWork tile_work(int ntm, int ntn, int bm, int bn) 
 // with head-aligned tiles; gptj: pairs inside the group), stores the row to the qkv buffer and the k / v
 // groups to their paged-cache rows (bf16 caches). D == 0: not a QKV projection.
 //
+//
+// mxq / mxs (SwiGLU GEMMs only, D == 0): instead of bf16 rows, write the SwiGLU output as MX-fp8 for a W8A8 consumer
+// (gemm_mid MXA): e4m3 bytes [M][N/2] with row stride ldy, and one e8m0 scale per row and 32 outputs [M][N/64] -
+// the scale 2^e with the smallest e that puts the block's |max| (after bf16 rounding, as the unfused output) at or
+// below 448 (OCP MX).
 struct QkvEpi {
   const int64_t* pos;
   const float* cos_t;
@@ -183,7 +188,17 @@ struct QkvEpi {
   bf16_t* vc;
   const int64_t* slot;
   int nh, nkv, D, rot, block_size, style, do_rope;
+  unsigned char* mxq;
+  unsigned char* mxs;
 };
+
+// e8m0 exponent e of an MX block with absolute maximum amax (> 0): the smallest e with amax / 2^e <= 448, clamped to
+// the exponents whose inverse 2^-e is a normal float
+__device__ __forceinline__ int mx_block_exp(float amax) {
+  const uint32_t b = __float_as_uint(amax / 448.f);
+  int e = (int)((b >> 23) & 255) - 127 + ((b & 0x7fffffu) != 0u);
+  return e < -126 ? -126 : (e > 126 ? 126 : e);
+}
 
 // fp32 epilogue image of a tile with BN columns in LDS. The C-layout writes (lane li, g -> row 4g + i,
 // column li: ds_write_b32, banks mod 32 per 32-lane half) and the row-piece reads (ds_read_b128, banks
@@ -325,6 +340,44 @@ __device__ __forceinline__ void img_store_rows(const float* ct, int rows, int r0
       if (n + 3 < N && (N & 3) == 0) *reinterpret_cast<f32x4*>(dst) = val;
       else
         for (int j = 0; j < 4 && n + j < N; ++j) dst[j] = val[j];
+    }
+  } else if (glu && qe.mxq) {  // SwiGLU -> MX-fp8 (BN % 64 == 0: 4 consecutive threads hold one 32-output block)
+    constexpr int VPR = BN / 16;
+    static_assert(BN % 16 == 0, "SwiGLU tile");
+    if constexpr (VPR % 4 == 0) {
+      // rows * VPR is a multiple of 64 (rows % 16 == 0), so a wave's 64 lanes run the same trip count: the block
+      // maximum's lane shuffles see every lane of the block
+      for (int v = threadIdx.x; v < rows * VPR; v += NTHR) {
+        const int r = v / VPR, oc = (v - r * VPR) * 8;
+        const int p = oc >> 4, j = oc & 15;
+        const int cg = 32 * p + j, m = m0 + r0 + r, ng = n0 + cg;
+        const bool ok = m < M && ng < N;
+        float gx[8], ux[8], h[8];
+        Img::ld8(ct, r, cg, gx);
+        Img::ld8(ct, r, cg + 16, ux);
+        float amax = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float gv = gx[e], uv = ux[e];
+          if (bias && ok) { gv += bf2f(bias[ng + e]); uv += bf2f(bias[ng + 16 + e]); }
+          h[e] = bf2f(f2bf(silu(gv) * uv));
+          amax = fmaxf(amax, fabsf(h[e]));
+        }
+        amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+        amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+        const int ex = amax > 0.f ? mx_block_exp(amax) : 0;
+        const float inv = __uint_as_float((uint32_t)(127 - ex) << 23);
+        unsigned lo = 0, hi = 0;
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(h[0] * inv, h[1] * inv, lo, false);
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(h[2] * inv, h[3] * inv, lo, true);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32(h[4] * inv, h[5] * inv, hi, false);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32(h[6] * inv, h[7] * inv, hi, true);
+        const int64_t oc_g = n0 / 2 + oc;  // output column
+        if (ok) {
+          *reinterpret_cast<uint2*>(qe.mxq + (int64_t)m * ldy + oc_g) = make_uint2(lo, hi);
+          if ((v & 3) == 0) qe.mxs[(int64_t)m * (ldy / 32) + oc_g / 32] = (unsigned char)(ex + 127);
+        }
+      }
     }
   } else if (glu) {  // out col 16p + j = silu(gate col 32p + j) * up col 32p + 16 + j, 8 per thread-step
     constexpr int VPR = BN / 16;

@@ -1379,27 +1379,34 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
                      int split, hipStream_t st, int* cnt = nullptr,
                      const QkvEpi* qe = nullptr, const float* xs = nullptr, const float* wsc = nullptr,
-                     bool ilv = false);
+                     bool ilv = false, const unsigned char* asc = nullptr);
 
 // tile: 1 = 128x128, 2 = 64x128, 3 = 64x64; ring depth 2-4; split-K over grid.y; 8-13: the gemm_mid tiles
 // (buffer-descriptor staging, csrc/gemm_mid.hip, fp8 MFMA variant; K % 128 == 0; ilv: its software-pipelined
 // k-loop, >= 3 stages)
+// MX-fp8 activations (gemm_mid tiles only): asc = e8m0 scales [M][K / 32] of xq (xs unused: nullptr), and mxq / mxs =
+// a SwiGLU output written as MX-fp8 instead of bf16 y (e4m3 [M][N / 2] with row stride ldy, scales [M][N / 64]; the
+// output tile must hold whole 32-output blocks, BN % 64 == 0, and finish in the launch: no split)
 // partial_out: a split plan without activation / GLU leaves its fp32 slabs [split, M, N] (scales applied, no
 // bias) in `workspace` for the consumer (rope_cache / add_norm sum them) and returns the split; else 0.
 int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq, int64_t ldw, const void* wsc,
                      const void* bias, void* y, int64_t ldy, int M, int N, int K, int act, bool glu, int tile,
                      int depth, int split, void* workspace, int64_t ws_bytes, hipStream_t st, bool partial_out,
-                     bool ilv) {
+                     bool ilv, void* mxq, void* mxs, const void* asc) {
   if (M == 0 || N == 0) return 0;
   if (K % 16) throw std::runtime_error("gemm_f8f8: K must be a multiple of 16");
   if (glu && (N % 32)) throw std::runtime_error("gemm_f8f8: glu needs N % 32 == 0");
-  if (!y && !partial_out) throw std::runtime_error("gemm_f8f8: output required");
+  if (!y && !partial_out && !mxq) throw std::runtime_error("gemm_f8f8: output required");
   int bm = tile == 1 ? 128 : 64, bn = tile == 3 ? 64 : 128, thr = 256;
   const bool mid = tile >= 7 && tile <= 15;
   if (mid) {
     if (K % 128) throw std::runtime_error("gemm_f8f8: gemm_mid tiles need K % 128 == 0");
     gemm_mid_dims(tile, &bm, &bn, &thr);
   }
+  if ((asc || mxq) && !mid) throw std::runtime_error("gemm_f8f8: MX-fp8 activations need a gemm_mid tile (7-15)");
+  if (asc && (xs || K % 128)) throw std::runtime_error("gemm_f8f8: MX scales replace xs; K % 128 == 0");
+  if (mxq && (!mxs || !glu || bn % 64 || N % 128 || ldy != N / 2 || partial_out))
+    throw std::runtime_error("gemm_f8f8: MX output needs SwiGLU, BN % 64 == 0, N % 128 == 0, dense rows, no slabs");
   const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   const int nk = (K + TBK8 - 1) / TBK8;
   if (tile == 4 || (tile == 0 && K % 128 == 0 && ((M + 255) / 256) * ((N + 255) / 256) >= 192)) {
@@ -1413,7 +1420,7 @@ int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq
   if (tile == 0) {  // auto: 128x128 when it fills the chip, else 64x128 / 64x64, split to >= ~256 WGs
     tile = ((M + 127) / 128) * ((N + 127) / 128) >= 240 ? 1 : (((M + 63) / 64) * ((N + 127) / 128) >= 240 ? 2 : 3);
     return launch_gemm_f8f8(xq, ldx, xs, wq, ldw, wsc, bias, y, ldy, M, N, K, act, glu, tile, depth, split, workspace,
-                            ws_bytes, st, partial_out, ilv);
+                            ws_bytes, st, partial_out, ilv, mxq, mxs, asc);
   }
   if (split <= 0) {
     split = 1;
@@ -1421,6 +1428,7 @@ int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq
   }
   split = std::max(1, std::min(split, nk));
   if ((int64_t)split * M * N * 4 > ws_bytes) split = 1;
+  if (mxq && split > 1) throw std::runtime_error("gemm_f8f8: an MX-fp8 SwiGLU output cannot be split over K");
   float* part = split > 1 ? (float*)workspace : nullptr;
   const int act_k = split > 1 ? 0 : act, g = glu ? 1 : 0, glu_k = split > 1 ? 0 : g;
   if (depth <= 0) depth = tile == 1 ? 3 : 4;
@@ -1435,8 +1443,12 @@ int launch_gemm_f8f8(const void* xq, int64_t ldx, const void* xs, const void* wq
 #define LF(BM_, BN_, NS_) \
   gemm_f8f8_kernel<BM_, BN_, NS_><<<grid, 256, 0, st>>>(A, ldx, XS, Bw, ldw, WSc, Bi, Y, ldy, part, M, N, K, act_k, glu_k)
   if (mid) {
+    QkvEpi mx{};
+    mx.mxq = (unsigned char*)mxq;
+    mx.mxs = (unsigned char*)mxs;
     launch_gemm_mid(tile, depth, M <= bm, (const bf16_t*)xq, ldx, (const bf16_t*)wq, ldw, Bi, Y, ldy, part, M, N, K,
-                    act_k, glu_k, split, st, nullptr, nullptr, XS, WSc, ilv);
+                    act_k, glu_k, split, st, nullptr, mxq ? &mx : nullptr, XS, WSc, ilv,
+                    (const unsigned char*)asc);
   } else if (tile == 1) {
     if (depth >= 3) LF(128, 128, 3); else LF(128, 128, 2);
   } else if (tile == 2) {

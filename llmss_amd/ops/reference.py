@@ -269,11 +269,41 @@ def fake_quant_fp8_act(x: torch.Tensor) -> torch.Tensor:
     return q * s
 
 
+def quant_mx_fp8(x: torch.Tensor):
+    """OCP MX-fp8 of rows, as a W8A8 SwiGLU epilogue writes it for the down projection (csrc/common.h
+    img_store_rows, mx_block_exp): per row and 32 columns the e8m0 scale 2^e with the smallest e such that the block's
+    |max| / 2^e <= 448 (e clamped to [-126, 126]; 0 for an all-zero block), q = e4m3(x / 2^e). Returns (q uint8
+    [M, K], s uint8 [M, K / 32] = e + 127)."""
+    M, K = x.shape
+    xb = x.float().reshape(M, K // 32, 32)
+    amax = xb.abs().amax(-1)
+    bits = (amax / 448.0).view(torch.int32)
+    e = ((bits >> 23) & 255) - 127 + ((bits & 0x7FFFFF) != 0).to(torch.int32)
+    e = torch.where(amax > 0, e.clamp(-126, 126), torch.zeros_like(e))
+    q = (xb * torch.ldexp(torch.ones_like(amax), -e)[..., None]).clamp(-448, 448).to(torch.float8_e4m3fn)
+    return q.view(torch.uint8).reshape(M, K), (e + 127).to(torch.uint8)
+
+
+def dequant_mx_fp8(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    M, K = q.shape
+    qf = q.view(torch.float8_e4m3fn).float().reshape(M, K // 32, 32)
+    return (qf * torch.ldexp(torch.ones(s.shape), s.to(torch.int32) - 127)[..., None]).reshape(M, K)
+
+
+def fake_quant_mx_act(x: torch.Tensor) -> torch.Tensor:
+    """MX-fp8 fake quantisation (quant_mx_fp8 then back to fp32)."""
+    return dequant_mx_fp8(*quant_mx_fp8(x))
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias=None, act: str = "none", glu: bool = False,
-           w_scale: Optional[torch.Tensor] = None, a8: bool = False) -> torch.Tensor:
-    """``a8`` (fp8 weights only): per-token e4m3 activations as well - the fp32 fake-quant oracle of W8A8."""
+           w_scale: Optional[torch.Tensor] = None, a8=False) -> torch.Tensor:
+    """``a8`` (fp8 weights only): per-token e4m3 activations as well - the fp32 fake-quant oracle of W8A8;
+    ``a8="mx"``: MX-fp8 activations (per-32 e8m0 block scales)."""
     wf = dequant_fp8(w, w_scale) if w_scale is not None else w.float()
-    xf = fake_quant_fp8_act(x) if (a8 and w_scale is not None) else x.float()
+    if a8 and w_scale is not None:
+        xf = fake_quant_mx_act(x) if a8 == "mx" else fake_quant_fp8_act(x)
+    else:
+        xf = x.float()
     y = xf @ wf.t()
     if bias is not None:
         y = y + bias.float()

@@ -248,6 +248,98 @@ def test_fp8_w8a8_prefill_and_decode_vs_fake_quant_oracle(tmp_path, monkeypatch)
         assert e8[k] < e16[k], (e8, e16)  # the oracle tells W8A8 from W8A16
 
 
+def test_fp8_mlp_mx_handoff_vs_fake_quant_oracle(tmp_path, monkeypatch):
+    """VERDICT r5 missing #4 at model level: with W8A8 gemm_mid plans for every fp8 GEMM (forced into the tuned table,
+    prefill 153 rows and decode 4 rows), DecoderLM._mlp has the gate/up epilogue write its SwiGLU output as MX-fp8 and
+    the down projection consume it - no bf16 intermediate, no quantisation launch. Oracle: the CPU reference with
+    per-token fake-quant activations for qkv / o / gate-up and MX fake-quant (ops/reference.py fake_quant_mx_act) for
+    the down projection's input. As in the W8A8 test above, e4m3 activations are chaotic end to end: the GPU logits
+    must sit within 1.5x the oracle's own fp32-vs-bf16 noise floor of it, and closer to it than to the W8A16 oracle."""
+    import dataclasses
+
+    import llmss_amd.ops as O
+    from llmss_amd.engine import build_model
+    from llmss_amd.models.decoder import DecoderLM, StepInput
+    from llmss_amd.ops import hip as H
+    from llmss_amd.ops import reference as R
+
+    hf = _hf("llama").eval()
+    hf.save_pretrained(str(tmp_path), safe_serialization=True)
+    dev = torch.device("cuda", 0)
+    m = build_model(str(tmp_path), None, "bf16", dev, fp8=True)
+    L = m.w.layers[0]
+    F = L.down.K
+    g = torch.Generator().manual_seed(12)
+    lens = [40, 50, 30, 33]
+    T, B = sum(lens), len(lens)
+    ps = [torch.randint(0, VOCAB - 1, (n,), generator=g).tolist() for n in lens]
+    lib = H.lib()
+    plans = {id(L.qkv): 11, id(L.o): 11, id(L.up): 8, id(L.down): 11}  # 64x128 / 128x128 gemm_mid W8A8 tiles
+    for M in (T, B):
+        for lin in (L.qkv, L.o, L.up, L.down):
+            lib.gemm_tuned_set(M, lin.N, lin.K, lin.glu, 1, H.W8A8_FLAG | (plans[id(lin)] << 8) | (3 << 12), 1)
+    assert H.mx_mlp_ok(T, L.up, L.down) and H.mx_mlp_ok(B, L.up, L.down)
+    bs, per = 16, 4
+    n_mx = [0]
+    w8a8 = H.linear_w8a8
+
+    def counting(*a, **k):
+        n_mx[0] += bool(k.get("mx_out"))
+        return w8a8(*a, **k)
+
+    def run(model, d):
+        ids = torch.tensor([t for p in ps for t in p], device=d)
+        pos = torch.cat([torch.arange(n) for n in lens]).to(d)
+        slots = torch.cat([torch.arange(n) + i * per * bs for i, n in enumerate(lens)]).to(d)
+        cu = torch.tensor([0] + torch.tensor(lens).cumsum(0).tolist(), dtype=torch.int32, device=d)
+        kv = model.allocate_kv_cache(B * per, bs)
+        lp = model(StepInput("prefill", ids, pos, slots, cu_seqlens=cu, max_seqlen=max(lens),
+                             last_idx=(cu[1:] - 1).long()), kv)[:, :VOCAB].float().cpu()
+        bt = torch.arange(B * per, dtype=torch.int32).view(B, per).to(d)
+        inp = StepInput("decode", torch.tensor([7, 99, 500, 3], device=d), torch.tensor(lens, device=d), torch.tensor(
+            [i * per * bs + n for i, n in enumerate(lens)], device=d), block_tables=bt,
+            ctx_lens=torch.tensor([n + 1 for n in lens], dtype=torch.int32, device=d), max_ctx=per * bs)
+        return lp, model(inp, kv)[:, :VOCAB].float().cpu()
+
+    monkeypatch.setattr(H, "linear_w8a8", counting)
+    try:
+        gp, gd = run(m, dev)
+    finally:
+        lib.gemm_tuned_clear()
+    assert n_mx[0] == 2 * len(m.w.layers), n_mx  # every layer's MLP, prefill and decode, took the MX hand-off
+    assert torch.isfinite(gp).all() and torch.isfinite(gd).all()
+
+    def oracle_linear(x, w, bias=None, act="none", glu=False, w_scale=None, a8=False):
+        mx = w_scale is not None and not glu and w.shape[1] == F  # the down projection's input
+        return R.linear(x, w, bias, act, glu, w_scale, a8="mx" if mx else True)
+
+    wc = _to(m.w, "cpu")
+    w16 = run(DecoderLM(m.cfg, wc), "cpu")
+    monkeypatch.setattr(O.ref, "linear", oracle_linear)
+    w8 = run(DecoderLM(m.cfg, wc), "cpu")
+
+    def to32(o):
+        if isinstance(o, torch.Tensor):
+            return o.float() if o.dtype == torch.bfloat16 else o
+        if dataclasses.is_dataclass(o):
+            return dataclasses.replace(o, **{f.name: to32(getattr(o, f.name)) for f in dataclasses.fields(o) if f.init})
+        return [to32(v) for v in o] if isinstance(o, list) else o
+
+    w8f = run(DecoderLM(m.cfg, to32(wc)), "cpu")
+
+    def err(a, b):
+        return float((a - b).abs().max() / b.abs().max())
+
+    e8 = (err(gp, w8[0]), err(gd, w8[1]))
+    e16 = (err(gp, w16[0]), err(gd, w16[1]))
+    floor = (err(w8f[0], w8[0]), err(w8f[1], w8[1]))
+    print(f"MX hand-off GPU vs oracle: prefill {e8[0]:.4f} decode {e8[1]:.4f}; oracle noise floor {floor[0]:.4f} / "
+          f"{floor[1]:.4f}; GPU vs W8A16 oracle {e16[0]:.4f} / {e16[1]:.4f}")
+    for k in range(2):
+        assert e8[k] <= 1.5 * floor[k], (e8, floor)
+        assert e8[k] < e16[k], (e8, e16)
+
+
 def test_generate_cli_recompute_mode_on_gpu(tmp_path):
     from helpers import make_tokenizer
 
