@@ -38,9 +38,7 @@
 // MXA (W8A8 with MX A-scales, csrc/gemm.hip launch_gemm_f8f8 `asc`): the fp8 activations carry one e8m0 scale per
 // row and 32-element block (OCP MX; asc [M][K / 32] bytes, written by a SwiGLU epilogue, img_store_rows) instead of
 // one fp32 scale per row. Each ring stage also stages the tile's 4 scale bytes per row of that k-step (one 4-byte
-// LDS-DMA piece per wave: its BM / NW rows), and the lane's 32 k-bytes are the contiguous block g of the k-step
-// (chunks 2g and 2g + 1, the odd lane groups reading them in swapped order so every ds_read_b128 stays conflict-free),
-// whose scale byte the MX-fp8 MFMA applies per lane.
+// LDS-DMA piece per wave: its BM / NW rows); lane group g passes the byte of block g to the MX-fp8 MFMA.
 template <int BM, int BN, int WM, int WN, int NS, bool WNT, bool F8 = false, int MODE = 0, bool ILV = false,
           bool MXA = false>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __restrict__ A, int64_t lda,
@@ -145,9 +143,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mid_kernel(const bf16_t* __
   // fp8: each lane feeds the 16x16x128 MFMA 32 k-bytes of its fragment row. It takes the 16-B chunks g and
   // g + 4 (the bf16 read pattern, conflict-free on the swizzled image) instead of 2g, 2g + 1 (PMC: 48 % of the
   // LDS cycles were bank conflicts). A and B use the same k permutation, so the dot products are unchanged.
-  const int y0 = MXA ? (((2 * g + (g & 1)) ^ (li & 7)) << 4) : x0;
-  const int y1 = MXA ? (((2 * g + 1 - (g & 1)) ^ (li & 7)) << 4) : x1;
-  // MXA: the scale word (4 blocks) of tile row r in a stage, and the lane's block byte of it
+  const int y0 = x0, y1 = x1;
+  // MXA: the scale word (4 blocks) of tile row r in a stage, and the byte of block g of it: the MFMA takes the scale
+  // of k-block b (k [32b, 32b + 32) of the step) from lane group b, and its k order - lane group g's first 16 bytes
+  // are k [16g, 16g + 16), its last 16 are k [64 + 16g, ...) - is exactly the chunk g / g + 4 reads above
+  // (bench/proto/mx_scale_probe.hip, scripts/mx_debug.py: a per-lane contiguous-block order scaled the wrong data)
   auto mx_scale = [&](const char* st, int r) -> int {
     return (int)(*reinterpret_cast<const uint32_t*>(st + A_BYTES + B_BYTES + (r / RW) * 256 + (r % RW) * 4) >> (8 * g));
   };
