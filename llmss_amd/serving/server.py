@@ -41,7 +41,7 @@ def main(argv=None):
 
 
 def _serve_replicas(driver, tok, args):
-    """torchrun world = dp x tp: global rank 0 hosts a broker and the gRPC front-end (BrokerServicer);
+    """torchrun world = dp x tp: global rank 0 hosts a broker and the gRPC front-end (AioBrokerServicer);
     every replica leader runs a Consumer on that broker (BRPOP = load balancing, replies correlated
     by request id); followers run their replica's driver loop."""
     import torch.distributed as dist
@@ -53,8 +53,7 @@ def _serve_replicas(driver, tok, args):
     g = driver.tp
     broker_srv = None
     if g.global_rank == 0:
-        broker_srv = MiniRedisServer("127.0.0.1", args.broker_port)
-        broker_srv._thread.start()
+        broker_srv = MiniRedisServer("127.0.0.1", args.broker_port).start()
     dist.barrier()  # the broker is listening before replicas connect
     if driver.leader:
         # one processing list per replica (durable hand-off, consumer.py)
