@@ -209,6 +209,10 @@ _PRESETS: Dict[str, Dict[str, Any]] = {
     "tiny-llama": dict(model_type="llama", hidden_size=64, num_hidden_layers=2, num_attention_heads=4,
                        num_key_value_heads=2, intermediate_size=160, vocab_size=211,
                        max_position_embeddings=128),
+    # TP up to 8 (16 q / kv heads: 2 per rank at TP=8, as Llama-2-7B's 32 give 4)
+    "tiny-llama16h": dict(model_type="llama", hidden_size=256, num_hidden_layers=2, num_attention_heads=16,
+                          num_key_value_heads=16, intermediate_size=512, vocab_size=211,
+                          max_position_embeddings=128),
 }
 
 

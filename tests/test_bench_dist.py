@@ -22,20 +22,24 @@ def _free_port():
     return p
 
 
-def test_bench_two_ranks_gloo():
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_two_ranks_gloo(n):
+    """n = 8: the driver's full-node invocation rehearsed rank for rank (TP=8 over 8 gloo processes, a 16-head tiny
+    Llama: 2 heads per rank)."""
     port = _free_port()
-    args = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "tiny-llama", "--secondary",
+    args = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--model",
+            "tiny-llama" if n <= 4 else "tiny-llama16h", "--secondary",
             "tiny-gpt2", "--steps", "2", "--warmup", "1", "--batch-per-gpu", "2", "--prompt-len", "8", "--gen-len", "4"]
     procs = []
-    for r in range(2):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
         procs.append(subprocess.Popen(args, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                                       cwd=ROOT))
     outs = []
     try:
         for p in procs:
-            outs.append(p.communicate(timeout=240))
+            outs.append(p.communicate(timeout=420))
     finally:
         for p in procs:
             if p.poll() is None:
@@ -43,15 +47,15 @@ def test_bench_two_ranks_gloo():
     for p, (o, e) in zip(procs, outs):
         assert p.returncode == 0, e[-2000:]
     lines = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
-    assert len(lines) == 1 and not [ln for ln in outs[1][0].splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and not [ln for o, _ in outs[1:] for ln in o.splitlines() if ln.startswith("{")]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["config"]["parallelism"] == "tp2"
-    assert d["config"]["global_batch"] == 4
-    # TP: both ranks generate the same 4 x 4 tokens per step, counted once
-    assert abs(d["value"] * d["ms_per_step"] / 1e3 - 16) < 0.05  # value and ms_per_step are rounded
+    assert d["n_gpus"] == n and d["steps"] == 2 and d["config"]["parallelism"] == f"tp{n}"
+    assert d["config"]["global_batch"] == 2 * n and len(d["rank_elapsed_s"]) == n
+    # TP: every rank generates the same 2n x 4 tokens per step, counted once
+    assert abs(d["value"] * d["ms_per_step"] / 1e3 - 8 * n) < 0.05 * n  # value and ms_per_step are rounded
     s = d["secondary"]
-    assert s["config"]["parallelism"] == "dp2xtp1" and s["config"]["global_batch"] == 4
-    assert abs(s["value"] * s["ms_per_step"] / 1e3 - 16) < 0.05  # 2 replicas x 2 requests x 4 tokens
+    assert s["config"]["parallelism"] == f"dp{n}xtp1" and s["config"]["global_batch"] == 2 * n
+    assert abs(s["value"] * s["ms_per_step"] / 1e3 - 8 * n) < 0.05 * n  # n replicas x 2 requests x 4 tokens
 
 
 def _cpu_env(**kw):
