@@ -27,6 +27,10 @@ def make_hf_model(name: str, vocab: int = 101, seed: int = 0):
         m = LlamaForCausalLM(LlamaConfig(hidden_size=64, num_hidden_layers=2, num_attention_heads=4,
                                          num_key_value_heads=2, intermediate_size=160, vocab_size=vocab,
                                          max_position_embeddings=64, bos_token_id=vocab - 1, eos_token_id=vocab - 1))
+    elif name == "llama16":  # TP up to 8: 16 q / 8 kv heads (2 q heads and 1 kv head per rank at TP=8)
+        m = LlamaForCausalLM(LlamaConfig(hidden_size=128, num_hidden_layers=2, num_attention_heads=16,
+                                         num_key_value_heads=8, intermediate_size=256, vocab_size=vocab,
+                                         max_position_embeddings=64, bos_token_id=vocab - 1, eos_token_id=vocab - 1))
     else:
         raise ValueError(name)
     return m.eval()

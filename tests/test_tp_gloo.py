@@ -93,7 +93,10 @@ _COL = {"LLMSS_TP_COL": "2"}  # column-chunked decode: row-parallel outputs as 2
                                                 ("gptj", 2, _PTBO), ("bigcode", 4, {**_PTBO, **_TBO}),
                                                 ("llama", 2, _RSAG), ("gptj", 2, _RSAG), ("bigcode", 4, _RSAG),
                                                 ("gpt2", 4, _RSAG), ("llama", 2, _COL), ("gpt2", 2, _COL),
-                                                ("bigcode", 4, {"LLMSS_TP_COL": "4"})])
+                                                ("bigcode", 4, {"LLMSS_TP_COL": "4"}),
+                                                # the full node: TP=8 (one kv head per rank), plain and overlapped
+                                                ("llama16", 8, None), ("llama16", 8, _TBO),
+                                                ("llama16", 8, {"LLMSS_TP_COL": "2"})])
 def test_tp_matches_single(tmp_path, name, world, overlap):
     d = str(tmp_path / name)
     save_hf_model(name, d, vocab=101)  # 101 % world != 0 -> exercises the padded vocab-parallel head
