@@ -587,9 +587,8 @@ class MiniRedisServer:
                     resp = await self._exec(cmd)
                 except Exception as e:  # noqa: BLE001 - an error reply; the connection stays in step
                     resp = RuntimeError(str(e))
-                wr.write(self._reply(resp))
-                if not rd._buffer:  # noqa: SLF001 - pipelined commands still buffered: answer them first
-                    await wr.drain()
+                wr.write(self._reply(resp))  # the transport sends at once; drain() waits only past its high-water mark
+                await wr.drain()
         except (ConnectionError, OSError):
             return
         finally:
