@@ -394,26 +394,36 @@ __global__ __launch_bounds__(256, 2) void gemm_stream2_kernel(const bf16_t* __re
   }
 }
 
-// split-K reduction + epilogue: part [S, M, N] fp32 (w_scale already applied)
+// split-K reduction + epilogue: part [S, M, N] fp32 (w_scale already applied). The slabs are read in groups of 8 with
+// every load of a group issued before its adds (one memory round trip per group, not per slab; adds in slab order).
+__device__ __forceinline__ float slab_sum(const float* __restrict__ part, int S, int64_t stride, int64_t off) {
+  constexpr int SG = 8;
+  float v = 0.f;
+  for (int s0 = 0; s0 < S; s0 += SG) {
+    float x[SG];
+#pragma unroll
+    for (int g = 0; g < SG; ++g) x[g] = part[(int64_t)min(s0 + g, S - 1) * stride + off];
+#pragma unroll
+    for (int g = 0; g < SG; ++g) v += s0 + g < S ? x[g] : 0.f;
+  }
+  return v;
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N,
                                                             const bf16_t* __restrict__ bias, bf16_t* __restrict__ Y,
                                                             int64_t ldy, int act, int glu) {
   const int m = blockIdx.y;
   const int nout = glu ? N / 2 : N;
+  const int64_t stride = (int64_t)M * N;
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < nout; c += gridDim.x * blockDim.x) {
     if (glu) {
       const int p = c >> 4, i = c & 15;
       const int ng = 32 * p + i, nu = ng + 16;
-      float gv = 0.f, uv = 0.f;
-      for (int s = 0; s < S; ++s) {
-        gv += part[((int64_t)s * M + m) * N + ng];
-        uv += part[((int64_t)s * M + m) * N + nu];
-      }
+      float gv = slab_sum(part, S, stride, (int64_t)m * N + ng), uv = slab_sum(part, S, stride, (int64_t)m * N + nu);
       if (bias) { gv += bf2f(bias[ng]); uv += bf2f(bias[nu]); }
       Y[(int64_t)m * ldy + c] = f2bf(silu(gv) * uv);
     } else {
-      float v = 0.f;
-      for (int s = 0; s < S; ++s) v += part[((int64_t)s * M + m) * N + c];
+      float v = slab_sum(part, S, stride, (int64_t)m * N + c);
       if (bias) v += bf2f(bias[c]);
       Y[(int64_t)m * ldy + c] = f2bf(apply_act(v, act));
     }

@@ -58,12 +58,22 @@ __global__ __launch_bounds__(256) void add_norm_kernel(const bf16_t* __restrict_
           for (int sp = 0; sp < PS; ++sp)
 #pragma unroll
             for (int j = 0; j < 4; ++j) { v[c][j] += p[sp][0][j]; v[c][4 + j] += p[sp][1][j]; }
-        } else {
-          for (int sp = 0; sp < S; ++sp) {
-            const f32x4 p0 = *reinterpret_cast<const f32x4*>(pr + sp * slab);
-            const f32x4 p1 = *reinterpret_cast<const f32x4*>(pr + sp * slab + 4);
+        } else {  // runtime S: the slabs in groups of SG, every load of a group issued before its adds (one memory
+                  // round trip per group, not per slab; the adds stay in slab order 0..S-1)
+          constexpr int SG = MAXC == 1 ? 8 : (MAXC == 2 ? 4 : 2);
+          for (int s0 = 0; s0 < S; s0 += SG) {
+            f32x4 p[SG][2];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) { v[c][j] += p0[j]; v[c][4 + j] += p1[j]; }
+            for (int g = 0; g < SG; ++g) {
+              const int sp = min(s0 + g, S - 1);
+              p[g][0] = *reinterpret_cast<const f32x4*>(pr + sp * slab);
+              p[g][1] = *reinterpret_cast<const f32x4*>(pr + sp * slab + 4);
+            }
+#pragma unroll
+            for (int g = 0; g < SG; ++g)
+              if (s0 + g < S)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) { v[c][j] += p[g][0][j]; v[c][4 + j] += p[g][1][j]; }
           }
         }
         if (xbias) {

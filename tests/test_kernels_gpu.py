@@ -544,6 +544,32 @@ def test_splitk_partials_fused_into_add_norm(M, N, K, rms):
     close(out, out_ref, 3e-2)
 
 
+@pytest.mark.parametrize("S", [3, 5, 6, 9, 11, 12])
+@pytest.mark.parametrize("rms", [True, False])
+def test_split_slab_sums_at_any_split_count(S, rms):
+    """Split counts without a compile-time add_norm variant (2 / 4 / 8 have one) sum their slabs in load groups
+    (csrc/norm.hip PS = -1, csrc/gemm.hip slab_sum): GPT-2-XL's o / down plans leave 5 slabs. add_norm over the
+    slabs and the split-K reduce (activation / SwiGLU epilogues) vs fp32."""
+    torch.manual_seed(S)
+    M, N, K = 64, 1600, 6400
+    x, w, b = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
+    res = rnd(M, N)
+    nw, nb = rnd(N, scale=0.2) + 1, (None if rms else rnd(N, scale=0.1))
+    hint = (14 | 32) << 8  # gemm_mid 64x32, 4 stages
+    p = H.linear(x, w, b, nt_hint=hint, split_hint=S, partial_ok=True)
+    assert isinstance(p, H.PartialSum) and p.S == S
+    y32 = R.linear(x.float(), w.float(), b.float())
+    out, r_out = H.add_norm(p, nw, nb, 1e-5, rms, residual=res.clone())
+    r_ref = (y32.to(torch.bfloat16).float() + res.float()).to(torch.bfloat16)
+    close(r_out, r_ref, 2e-2)
+    out_ref, _ = R.add_norm(r_ref, nw, nb, 1e-5, rms)
+    close(out, out_ref, 3e-2)
+    close(H.linear(x, w, b, act="gelu_tanh", nt_hint=hint, split_hint=S), R.linear(x.float(), w.float(), b.float(),
+                                                                                 act="gelu_tanh"), 2e-2)
+    close(H.linear(x, w, None, glu=True, nt_hint=hint, split_hint=S), R.linear(x.float(), w.float(), None, glu=True),
+          2e-2)
+
+
 @pytest.mark.parametrize("V", [32000, 50257, 1000])
 def test_sample_topk_topp_sets(V):
     """Every sampled token must lie in the reference top-k -> top-p kept set."""
