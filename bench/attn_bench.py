@@ -22,7 +22,6 @@ def main():
     ap.add_argument("--splits", default="", help="context splits to sweep (default: the engine's decode_splits)")
     ap.add_argument("--unrolls", default="1,2,4,11,12,14")
     ap.add_argument("--bs", type=int, default=16, help="KV cache block (page) size in tokens")
-    ap.add_argument("--pairs", default="1", help="D = 64 MHA: two kv heads per workgroup on (1) / off (0), swept")
     a = ap.parse_args()
     dev, bs, D = "cuda", a.bs, a.D
     for hk in a.heads.split(","):
@@ -40,10 +39,9 @@ def main():
             q = torch.randn(a.B, (nh + 2 * nkv) * D, device=dev).to(torch.bfloat16)
             out = torch.empty(a.B, nh * D, device=dev, dtype=torch.bfloat16)
             res = {"B": a.B, "nh": nh, "nkv": nkv, "ctx": ctx, "MB": round(kv_bytes / 1e6, 1)}
-            for u, sp, pr in [(u, sp, pr) for u in map(int, a.unrolls.split(",")) for pr in map(int, a.pairs.split(","))
-                              for sp in (map(int, a.splits.split(",")) if a.splits else [0])]:
+            for u, sp in [(u, sp) for u in map(int, a.unrolls.split(",")) for sp in
+                          (map(int, a.splits.split(",")) if a.splits else [0])]:
                 H.lib().attn_decode_set_unroll(u)
-                H.lib().attn_decode_set_pair(bool(pr))
                 spl = None
                 if sp:
                     ps = -(-ctx // sp)
@@ -73,11 +71,10 @@ def main():
                     torch.cuda.synchronize()
                     us = min(us, s.elapsed_time(e) * 1e3 / 50)
                 del g
-                tag = f"u{u}" + (f"s{sp}" if sp else "") + ("" if a.pairs == "1" else f"p{pr}")
+                tag = f"u{u}" + (f"s{sp}" if sp else "")
                 res[f"{tag}_us"] = round(us, 2)
                 res[f"{tag}_TBps"] = round(kv_bytes / us / 1e6, 2)
-            H.lib().attn_decode_set_unroll(0)  # back to the defaults
-            H.lib().attn_decode_set_pair(True)
+            H.lib().attn_decode_set_unroll(0)  # back to the default
             print(res, flush=True)
 
 

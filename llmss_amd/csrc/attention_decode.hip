@@ -44,11 +44,8 @@ __device__ __forceinline__ float token_sum(float s) {
 // KV8: the paged cache holds fp8 rows (D e4m3 bytes + fp32 scale at byte D, 16-B tail; reference.py
 // kv_rows_quant): each lane loads 8 bytes per token instead of 16 and the row scales multiply the score
 // (K) and the probability (V) instead of every element.
-// MH (multi-head MHA workgroups, bf16 cache): the GB query heads of a workgroup are GB consecutive kv heads of an MHA
-// model (G == 1), each with its own K / V rows - a D = 64 (sequence, head) pair streams only ~48 KB at GPT-2-XL's
-// contexts, so pairing heads halves the per-workgroup fixed costs (q / page-table round trips, the merge) per byte.
-template <int D, int GB, int UNROLL, bool PIPE = false, bool KV8 = false, bool MH = false>
-__global__ __launch_bounds__(256, (GB == 1 || MH) ? 8 : 1) void attn_decode_kernel(
+template <int D, int GB, int UNROLL, bool PIPE = false, bool KV8 = false>
+__global__ __launch_bounds__(256, GB == 1 ? 8 : 1) void attn_decode_kernel(
     const bf16_t* __restrict__ q, int64_t q_stride, void* __restrict__ kcv, void* __restrict__ vcv,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens, bf16_t* __restrict__ out,
     int64_t out_stride, float* __restrict__ part_o, float* __restrict__ part_ml, int nh, int nkv, int G, int ngroups,
@@ -60,15 +57,13 @@ __global__ __launch_bounds__(256, (GB == 1 || MH) ? 8 : 1) void attn_decode_kern
   bf16_t* __restrict__ vc = (bf16_t*)vcv;
   const unsigned char* __restrict__ kc8 = (const unsigned char*)kcv;
   const unsigned char* __restrict__ vc8 = (const unsigned char*)vcv;
-  static_assert(!MH || !KV8, "multi-head workgroups: bf16 cache");
-  constexpr int NKH = MH ? GB : 1;  // kv heads a workgroup streams
   const int b = blockIdx.x;
-  const int kvh = MH ? blockIdx.y * GB : blockIdx.y / ngroups, grp = MH ? 0 : blockIdx.y % ngroups;
+  const int kvh = blockIdx.y / ngroups, grp = blockIdx.y % ngroups;
   const int split = blockIdx.z, nsplit = gridDim.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int slot = lane / LPT, sub = lane % LPT;
-  const int h0 = MH ? kvh : kvh * G + grp * GB;
-  const int nvalid = MH ? min(GB, nkv - kvh) : min(GB, G - grp * GB);
+  const int h0 = kvh * G + grp * GB;
+  const int nvalid = min(GB, G - grp * GB);
 
   // q (pre-scaled into the log2 domain)
   float qv[GB][8];
@@ -121,11 +116,10 @@ __global__ __launch_bounds__(256, (GB == 1 || MH) ? 8 : 1) void attn_decode_kern
   };
   // a token's K / V registers: bf16 rows 16 B per lane; fp8 rows 8 B per lane + the row's two scales
   struct KVRegs {
-    u16x8 k[NKH][UNROLL], v[NKH][UNROLL];
+    u16x8 k[UNROLL], v[UNROLL];
     u32x2 k8[UNROLL], v8[UNROLL];
     float ks[UNROLL], vs[UNROLL];
   };
-  const int64_t head_rows = (int64_t)block_size * RB;  // MH: the next kv head's rows in the same page
   auto load_tokens = [&](int tb, KVRegs& r) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
@@ -138,12 +132,8 @@ __global__ __launch_bounds__(256, (GB == 1 || MH) ? 8 : 1) void attn_decode_kern
         r.ks[u] = *reinterpret_cast<const float*>(kc8 + a - sub * 8 + D);
         r.vs[u] = *reinterpret_cast<const float*>(vc8 + a - sub * 8 + D);
       } else {
-#pragma unroll
-        for (int hk = 0; hk < NKH; ++hk) {
-          const int64_t ah = a + (hk < nvalid ? hk : 0) * head_rows;  // a missing last head re-reads head 0
-          r.k[hk][u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(kc + ah));
-          r.v[hk][u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(vc + ah));
-        }
+        r.k[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(kc + a));
+        r.v[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(vc + a));
       }
     }
   };
@@ -161,16 +151,12 @@ __global__ __launch_bounds__(256, (GB == 1 || MH) ? 8 : 1) void attn_decode_kern
         vf[0] = v0[0]; vf[1] = v0[1]; vf[2] = v1[0]; vf[3] = v1[1]; vf[4] = v2[0]; vf[5] = v2[1]; vf[6] = v3[0]; vf[7] = v3[1];
         ks = r.ks[u];
         vs = r.vs[u];
-      } else if constexpr (!MH) {
+      } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { kf[j] = bf2f(r.k[0][u][j]); vf[j] = bf2f(r.v[0][u][j]); }
+        for (int j = 0; j < 8; ++j) { kf[j] = bf2f(r.k[u][j]); vf[j] = bf2f(r.v[u][j]); }
       }
 #pragma unroll
       for (int h = 0; h < GB; ++h) {
-        if constexpr (MH) {  // query head h reads its own kv head's rows
-#pragma unroll
-          for (int j = 0; j < 8; ++j) { kf[j] = bf2f(r.k[h][u][j]); vf[j] = bf2f(r.v[h][u][j]); }
-        }
         float s = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) s = fmaf(qv[h][j], kf[j], s);
@@ -290,24 +276,19 @@ __global__ __launch_bounds__(256) void attn_decode_reduce_kernel(const float* __
 // 192 / 1024 tokens and 12-17% ahead for GQA groups of 4)
 static int g_decode_unroll = 11;
 void attn_decode_set_unroll(int u) { g_decode_unroll = (u == 1 || u == 2 || u == 4 || u == 11 || u == 12 || u == 14) ? u : 11; }
-// two kv heads per workgroup for D = 64 MHA (the MH kernel); a switch for the A/B test and the probe
-static bool g_decode_pair = true;
-void attn_decode_set_pair(bool on) { g_decode_pair = on; }
 
-template <int D, int GB, bool MH = false>
+template <int D, int GB>
 static void launch_decode_t(const bf16_t* q, int64_t qs, bf16_t* kc, bf16_t* vc, const int* bt, int bts,
                             const int* cl, bf16_t* out, int64_t os, float* po, float* pml, int B, int nh, int nkv,
                             int bs, int nsplit, int psize, float scale, hipStream_t st, bool kv8) {
   const int G = nh / nkv;
   const int ngroups = (G + GB - 1) / GB;
-  dim3 grid(B, MH ? (nkv + GB - 1) / GB : nkv * ngroups, nsplit);
+  dim3 grid(B, nkv * ngroups, nsplit);
   const float sl2 = scale * kLog2e;
 #define AD(U_, PIPE_, KV8_)                                                                                      \
-  attn_decode_kernel<D, GB, U_, PIPE_, KV8_ && !MH, MH><<<grid, 256, 0, st>>>(q, qs, kc, vc, bt, bts, cl, out, os, po, \
-                                                                           pml, nh, nkv, G, ngroups, bs, psize, sl2)
-  if constexpr (MH) {
-    AD(1, true, false);  // the default pipeline (two register sets of one token)
-  } else if (kv8) {
+  attn_decode_kernel<D, GB, U_, PIPE_, KV8_><<<grid, 256, 0, st>>>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, nh, \
+                                                                  nkv, G, ngroups, bs, psize, sl2)
+  if (kv8) {
     switch (g_decode_unroll) {
       case 2: AD(2, false, true); break;
       case 12: AD(2, true, true); break;
@@ -336,10 +317,7 @@ static void launch_decode_d(const bf16_t* q, int64_t qs, bf16_t* kc, bf16_t* vc,
                             const int* cl, bf16_t* out, int64_t os, float* po, float* pml, int B, int nh, int nkv,
                             int bs, int nsplit, int psize, float scale, hipStream_t st, bool kv8) {
   const int G = nh / nkv;
-  // D = 64 MHA (GPT-2-XL: 25 heads) with the default pipeline: two kv heads per workgroup
-  if (D == 64 && G == 1 && nkv >= 2 && !kv8 && g_decode_unroll == 11 && g_decode_pair)
-    launch_decode_t<D, 2, true>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, kv8);
-  else if (G == 1) launch_decode_t<D, 1>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, kv8);
+  if (G == 1) launch_decode_t<D, 1>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, kv8);
   else if (G == 2) launch_decode_t<D, 2>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, kv8);
   else if (G <= 4) launch_decode_t<D, 4>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, kv8);
   else launch_decode_t<D, 8>(q, qs, kc, vc, bt, bts, cl, out, os, po, pml, B, nh, nkv, bs, nsplit, psize, scale, st, kv8);
