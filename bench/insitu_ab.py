@@ -23,6 +23,12 @@ VARIANTS = {  # label: {projection: (nt_hint, split)} at M = 64
         ("up,o,down mid64x32", {"up": ((14 | 32) << 8, 1), "o": ((14 | 32) << 8, 4), "down": ((14 | 32) << 8, 5)}),
         ("up dec64x64", {"up": ((4 | 32 | 1024) << 8, 1)}),
     ],
+    "llama2-7b": [
+        ("o,down mid64x96", {"o": ((15 | 32) << 8, 6), "down": ((15 | 32) << 8, 6)}),
+        ("o,down dec64x64", {"o": ((4 | 32 | 1024) << 8, 4), "down": ((4 | 32 | 1024) << 8, 4)}),
+        ("o,down mid64x128", {"o": ((11 | 32) << 8, 8), "down": ((11 | 32) << 8, 8)}),
+        ("qkv mid64x96", {"qkv": ((15 | 32) << 8, 2)}),
+    ],
 }
 
 
