@@ -58,8 +58,12 @@ def main():
                     help="dev tool: one process computes rank 0 of a TP=N shard plan with no communication "
                          "(per-rank compute time at TP=N shapes; not a headline number)")
     ap.add_argument("--sim-comm", default="",
-                    help="with --simulate-tp: model each all-reduce / all-gather as LAT_US,GBPS (latency + bytes / "
-                         "algorithmic bandwidth, a spin kernel on the collective's stream) to measure comm overlap")
+                    help="with --simulate-tp: model each all-reduce / all-gather as LAT_US,GBPS[,CHANNELS] (latency + "
+                         "bytes / algorithmic bandwidth on the collective's stream: a one-workgroup spin kernel, or "
+                         "CHANNELS workgroups moving the collective's memory traffic) to measure comm overlap")
+    ap.add_argument("--sim-tbo", type=int, default=0,
+                    help="with --simulate-tp and --sim-comm: run decode steps of >= N sequences as two micro-batches "
+                         "(the overlap schedule the real communicator's capture-time A/B can pick)")
     ap.add_argument("--clients", type=int, default=4,
                     help="gRPC client processes for the served secondary config (each sends its share of the "
                          "step's concurrent requests)")
@@ -363,6 +367,8 @@ def run_config(args, model_name, tp, batch, progress, dp=False, client=None):
     local_batch = batch // world if dp else batch
     t_setup = time.perf_counter()
     model = build_model(model_name, tp if not dp else None, "bf16", dev, fp8=args.fp8, random_init=True)
+    if args.simulate_tp > 1 and args.sim_tbo:  # dev tool: decode steps of >= N sequences as two micro-batches
+        model.tbo_min = args.sim_tbo
     t_model = time.perf_counter() - t_setup
     max_len = min(model.cfg.max_position_embeddings, max(256, args.prompt_len + args.gen_len))
     eng = LLMEngine(model, max_num_seqs=local_batch, max_batched_tokens=max(8192, local_batch * args.prompt_len),
@@ -446,7 +452,8 @@ def run_config(args, model_name, tp, batch, progress, dp=False, client=None):
     e2e = np.nanmedian([m["e2e_s"] for m in mets]) * 1e3
     value = total / el
     if args.simulate_tp > 1:
-        par = f"tp{args.simulate_tp}-simulated-" + (f"comm-model-{args.sim_comm}" if args.sim_comm else "no-comm")
+        par = f"tp{args.simulate_tp}-simulated-" + (f"comm-model-{args.sim_comm}" if args.sim_comm else "no-comm") + (
+            f"-tbo{args.sim_tbo}" if args.sim_tbo else "")
     else:
         par = (f"dp{world}xtp1" if world > 1 else "tp1") if dp else f"tp{world}"
     out = {

@@ -59,6 +59,8 @@ int gemm_f8f8_partial_slabs(int M, int N, int K, bool glu, int act, int tile, in
 int gemm_partial_slabs(int M, int N, int K, bool w_fp8, bool glu, int act, int nt_hint, int split_hint,
                        int64_t ws_bytes);
 void attn_decode_set_unroll(int u);
+void launch_comm_model(void* buf, int channels, int64_t nbytes, double us, hipStream_t st);
+int64_t comm_model_slice(int channels, int64_t nbytes);
 
 bool gemm_tuned_get(int M, int N, int K, bool glu, int kind, int* nt_hint, int* split);
 void launch_add_norm_partial(const void* part, int S, int64_t slab, const void* xbias, const void* res_in,
@@ -175,6 +177,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_f8f8_partial_slabs", &gemm_f8f8_partial_slabs);
   m.def("gemm_partial_slabs", &gemm_partial_slabs);
   m.def("attn_decode_set_unroll", &attn_decode_set_unroll);
+  m.def("comm_model", [](uintptr_t buf, int channels, int64_t nbytes, double us, uintptr_t st) {
+    launch_comm_model(P(buf), channels, nbytes, us, S(st));
+  });
+  m.def("comm_model_slice", &comm_model_slice);
   m.def("gemm_tuned_get", [](int M, int N, int K, bool glu, int kind) -> py::object {
     int nt, s;
     if (!gemm_tuned_get(M, N, K, glu, kind, &nt, &s)) return py::none();

@@ -44,9 +44,10 @@ class TPGroup:
         # native RCCL communicator (device tensors); `group` then is the CPU (gloo) group of the same ranks
         self.comm = comm
         self._suspend = False  # suspended(): data-plane collectives are skipped (shape-only warm-up)
-        # fake groups only: (latency us, algorithmic GB/s) of a modelled all-reduce. Each all-reduce
-        # then occupies the issuing stream for latency + bytes/bandwidth (a spin kernel on one
-        # workgroup), so the comm/compute overlap of a TP=N schedule can be measured on one GPU.
+        # fake groups only: (latency us, algorithmic GB/s[, channels]) of a modelled all-reduce. Each all-reduce
+        # then occupies the issuing stream for latency + bytes/bandwidth, so the comm/compute overlap of a TP=N
+        # schedule can be measured on one GPU: a spin kernel on one workgroup, or with `channels` the many-CU model
+        # (csrc/comm_model.hip: that many workgroups moving the collective's local memory traffic, as RCCL's do).
         self.sim_comm = sim_comm if fake and size > 1 else None
         # fake groups standing in for a TP=N rank (bench --simulate-tp): all-gathers return N copies of the
         # local shard, so what consumes them (the candidate sampler's N groups, a full-width logits row)
@@ -78,8 +79,20 @@ class TPGroup:
             e.record()
             e.synchronize()
             self._cycles_per_us = 2_000_000 / (s.elapsed_time(e) * 1e3)
-        lat, gbps = self.sim_comm
+        lat, gbps = self.sim_comm[:2]
         us = lat + nbytes / (gbps * 1e3)
+        if len(self.sim_comm) > 2:
+            from .. import _native
+
+            lib, ch = _native(), int(self.sim_comm[2])
+            need = ch * 2 * lib.comm_model_slice(ch, nbytes)
+            buf = getattr(self, "_sim_buf", None)
+            if buf is None or buf.numel() < need:
+                if torch.cuda.is_current_stream_capturing():
+                    raise RuntimeError("modelled-collective scratch must be allocated before graph capture")
+                buf = self._sim_buf = torch.empty(need, dtype=torch.uint8, device="cuda")
+            lib.comm_model(buf.data_ptr(), ch, nbytes, us, torch.cuda.current_stream().cuda_stream)
+            return
         torch.cuda._sleep(max(1, int(us * self._cycles_per_us)))
 
     @property

@@ -909,3 +909,26 @@ def test_gemm_w8a8_mid_tiles_software_pipelined(tile, depth, split, M, N, K):
     # through the nt_hint encoding a tuned plan carries
     hint = H.W8A8_FLAG | H.W8A8_ILV | (tile << 8) | (depth << 12)
     close(H.linear(x, q, b, w_scale=s, nt_hint=hint, split_hint=split), R.linear(xd, q, b.float(), w_scale=s), 2e-2)
+
+
+@pytest.mark.parametrize("ch,nbytes,us", [(32, 4 << 20, 40.0), (16, 64 << 10, 12.0), (64, 32 << 20, 120.0)])
+def test_comm_model_holds_its_channels_for_the_modelled_time(ch, nbytes, us):
+    """The many-CU modelled collective of the simulated TP shard (csrc/comm_model.hip): each call lasts the modelled
+    time (its traffic done within it, or the time stretched by the traffic), timed over 10 calls in a HIP graph."""
+    lib = H.lib()
+    buf = torch.empty(ch * 2 * lib.comm_model_slice(ch, nbytes), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    lib.comm_model(buf.data_ptr(), ch, nbytes, us, st)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        for _ in range(10):
+            lib.comm_model(buf.data_ptr(), ch, nbytes, us, torch.cuda.current_stream().cuda_stream)
+    g.replay()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    g.replay()
+    e.record()
+    e.synchronize()
+    per = s.elapsed_time(e) * 1e3 / 10
+    assert us * 0.98 <= per <= us * 1.5 + 10, per
