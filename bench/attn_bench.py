@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--splits", default="", help="context splits to sweep (default: the engine's decode_splits)")
     ap.add_argument("--unrolls", default="1,2,4,11,12,14")
     ap.add_argument("--bs", type=int, default=16, help="KV cache block (page) size in tokens")
+    ap.add_argument("--rotate-mb", type=float, default=700,
+                    help="K/V copies rotated over at least this many MB (default: past the 256 MiB Infinity Cache; "
+                         "the decode step's own working set is ~20 GB)")
     a = ap.parse_args()
     dev, bs, D = "cuda", a.bs, a.D
     for hk in a.heads.split(","):
@@ -30,7 +33,7 @@ def main():
             maxb = (ctx + bs - 1) // bs
             nb = a.B * maxb
             kv_bytes = 2 * a.B * ctx * nkv * D * 2
-            ncopy = max(1, int(700e6 // kv_bytes) + 1)  # rotate copies past the 256 MiB Infinity Cache
+            ncopy = max(1, int(a.rotate_mb * 1e6 // kv_bytes) + 1)  # rotate copies past the 256 MiB Infinity Cache
             kcs = [torch.randn(nb, nkv, bs, D, device=dev).to(torch.bfloat16) for _ in range(ncopy)]
             vcs = [torch.randn_like(kcs[0]) for _ in range(ncopy)]
             pages = torch.randperm(nb, device=dev) if a.random_pages else torch.arange(nb, device=dev)
