@@ -473,8 +473,8 @@ class MiniRedisServer:
             fut, take = ws.popleft()
             if not fut.done():
                 fut.set_result(take(key))
-        if ws is not None and not ws:
-            del self._waiters[key]
+        if ws is not None and not ws and self._waiters.get(key) is ws:  # a nested serve (a move onto the same key)
+            del self._waiters[key]                                         # may have removed it already
 
     async def _blocking(self, keys, timeout, take):
         import asyncio
@@ -497,7 +497,7 @@ class MiniRedisServer:
                     if rest:
                         self._waiters[k] = rest
                     else:
-                        del self._waiters[k]
+                        self._waiters.pop(k, None)
 
     def _move(self, src, dst):
         v = self._pop(src)

@@ -319,6 +319,27 @@ def test_redis_broker_list_commands():
     srv.stop()
 
 
+def test_redis_rotation_onto_the_same_key_with_parked_pops():
+    """Two BRPOPLPUSH q -> q pops park on an empty list; one push serves both (the first pop's move onto q serves
+    the second from inside the first's wake-up), as Redis rotates a list onto itself. The server stays up."""
+    srv = MiniRedisServer().start()
+    try:
+        got = []
+        ts = [threading.Thread(target=lambda: got.append(RedisBroker(srv.host, srv.port).brpoplpush("q", "q", 5)))
+              for _ in range(2)]
+        for t in ts:
+            t.start()
+        time.sleep(0.3)
+        b = RedisBroker(srv.host, srv.port)
+        b.lpush("q", "x")
+        for t in ts:
+            t.join(10)
+        assert got == ["x", "x"] and b.lrange("q", 0, -1) == ["x"]
+        assert b.pipeline([("PING",)]) == ["PONG"]
+    finally:
+        srv.stop()
+
+
 @pytest.mark.parametrize("kind", ["memory", "resp"])
 def test_broker_pipeline(kind):
     """Pipelined commands run in order with one reply each; an error reply sits in its slot and the commands after
