@@ -258,6 +258,7 @@ class DecodeWorkspace:
                 raise RuntimeError("decode workspace must be allocated before graph capture")
             n_o = max(need * D, 0 if self.po is None else self.po.numel())
             n_ml = max(need * 2, 0 if self.pml is None else self.pml.numel())
+            _retire(self.po, self.pml)
             self.po = torch.empty(n_o, dtype=torch.float32, device=device)
             self.pml = torch.empty(n_ml, dtype=torch.float32, device=device)
         return self.po, self.pml
@@ -275,6 +276,15 @@ class _Slotted:
 
 
 _SLOT = threading.local()  # per host thread, like the native slot (csrc/gemm.hip gemm_set_slot)
+
+# Scratch buffers outgrown by a later (eager) call are kept, never freed: a decode graph captured earlier still
+# writes to the old addresses on every replay, and a freed block would go back to the caching allocator and be
+# handed to live tensors (the native counters do the same, csrc/gemm.hip sk_counters).
+_RETIRED: list = []
+
+
+def _retire(*ts):
+    _RETIRED.extend(t for t in ts if t is not None)
 
 
 class workspace_slot:
@@ -344,6 +354,7 @@ class GemmWorkspace:
         if self.buf is None or self.buf.numel() * 4 < nbytes or self.buf.device != device:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("gemm workspace must be allocated before graph capture")
+            _retire(self.buf)
             self.buf = torch.empty((max(nbytes, 1 << 20) + 3) // 4, dtype=torch.float32, device=device)
         return self.buf
 
@@ -405,6 +416,7 @@ class _QuantScratch:
                 raise RuntimeError(f"fp8 activation scratch for [{M}, {K}] must be allocated before graph capture")
             nq = max(M * K, 0 if self.q is None else self.q.numel())
             ns = max(M, 0 if self.s is None else self.s.numel())
+            _retire(self.q, self.s)
             self.q = torch.empty(nq, dtype=torch.uint8, device=device)
             self.s = torch.empty(ns, dtype=torch.float32, device=device)
         return self.q[:M * K].view(M, K), self.s[:M]
@@ -443,6 +455,7 @@ class _MxScratch:
         if self.q is None or self.q.numel() < M * K or self.q.device != device:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError(f"MX-fp8 activation scratch for [{M}, {K}] must be allocated before graph capture")
+            _retire(self.q, self.s)
             self.q = torch.empty(M * K, dtype=torch.uint8, device=device)
             self.s = torch.empty(M * K // 32, dtype=torch.uint8, device=device)
         return self.q[:M * K].view(M, K), self.s[:M * K // 32].view(M, K // 32)
@@ -544,6 +557,7 @@ class _PreQScratch:
         if self.q is None or self.q.numel() < M * K or self.s.numel() < M or self.q.device != device:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError(f"fp8 norm-output scratch for [{M}, {K}] must be allocated before graph capture")
+            _retire(self.q, self.s)
             self.q = torch.empty(max(M * K, 0 if self.q is None else self.q.numel()), dtype=torch.uint8, device=device)
             self.s = torch.empty(max(M, 0 if self.s is None else self.s.numel()), dtype=torch.float32, device=device)
         return self.q[:M * K].view(M, K), self.s[:M]

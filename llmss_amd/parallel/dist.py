@@ -85,12 +85,17 @@ class TPGroup:
             from .. import _native
 
             lib, ch = _native(), int(self.sim_comm[2])
-            need = ch * 2 * lib.comm_model_slice(ch, nbytes)
             buf = getattr(self, "_sim_buf", None)
-            if buf is None or buf.numel() < need:
+            if buf is None:
+                # sized once for the largest slice (comm_model_slice caps it), never re-allocated: graphs captured
+                # earlier keep its address, so freeing it for a larger collective would leave them writing into
+                # memory the allocator has handed out again
                 if torch.cuda.is_current_stream_capturing():
                     raise RuntimeError("modelled-collective scratch must be allocated before graph capture")
-                buf = self._sim_buf = torch.empty(need, dtype=torch.uint8, device="cuda")
+                buf = self._sim_buf = torch.empty(ch * 2 * lib.comm_model_slice(ch, 1 << 40), dtype=torch.uint8,
+                                                  device="cuda")
+            if buf.numel() < ch * 2 * lib.comm_model_slice(ch, nbytes):
+                raise RuntimeError("modelled-collective scratch too small")
             lib.comm_model(buf.data_ptr(), ch, nbytes, us, torch.cuda.current_stream().cuda_stream)
             return
         torch.cuda._sleep(max(1, int(us * self._cycles_per_us)))
