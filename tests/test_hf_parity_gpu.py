@@ -342,6 +342,45 @@ def test_fp8_mlp_mx_handoff_vs_fake_quant_oracle(tmp_path, monkeypatch):
         assert e8[k] < e16[k], (e8, e16)
 
 
+def test_fp8_decode_graphs_survive_a_prefill_that_grows_the_scratch(tmp_path):
+    """Decode graphs are captured at engine start with the W8A8 / MX-fp8 activation scratch sized for <= 4 rows; the
+    first prompt batch (320 rows) then grows it. The graphs keep the old addresses, so the old buffers must stay
+    allocated (ops/hip.py _retire): greedy tokens with graphs equal the eager engine's, and the grown buffers were
+    retired, not freed."""
+    from llmss_amd.engine import LLMEngine, SamplingParams, build_model
+    from llmss_amd.ops import hip as H
+
+    hf = _hf("llama").eval()
+    hf.save_pretrained(str(tmp_path), safe_serialization=True)
+    dev = torch.device("cuda", 0)
+    m = build_model(str(tmp_path), None, "bf16", dev, fp8=True)
+    L = m.w.layers[0]
+    lib = H.lib()
+    plans = {id(L.qkv): 11, id(L.o): 11, id(L.up): 8, id(L.down): 11}  # W8A8 gemm_mid tiles, MX hand-off in the MLP
+    g = torch.Generator().manual_seed(21)
+    ps = [torch.randint(0, VOCAB - 1, (n,), generator=g).tolist() for n in (100, 90, 70, 60)]
+    sp = SamplingParams(max_new_tokens=12, is_greedy=True, ignore_eos=True)
+    for slotted, cls in ((H._QSCRATCH, H._QuantScratch), (H._PRESCRATCH, H._PreQScratch), (H._MXSCRATCH, H._MxScratch)):
+        for it in slotted._items:  # start from empty scratch (earlier tests may have grown it past 320 rows)
+            H._retire(it.q, it.s)
+        slotted._items = [cls() for _ in slotted._items]
+    outs = {}
+    try:
+        for graphs in (True, False):
+            for M in (1, 2, 4):
+                for lin in (L.qkv, L.o, L.up, L.down):
+                    lib.gemm_tuned_set(M, lin.N, lin.K, lin.glu, 1, H.W8A8_FLAG | (plans[id(lin)] << 8) | (3 << 12), 1)
+            eng = LLMEngine(m, max_num_seqs=4, block_size=16, autotune=False, use_graphs=graphs)
+            n0 = len(H._RETIRED)
+            outs[graphs] = eng.generate(ps, sp)
+            if graphs:
+                assert eng.graphs and len(H._RETIRED) > n0  # the prompt batch outgrew the captured scratch
+            del eng
+    finally:
+        lib.gemm_tuned_clear()
+    assert outs[True] == outs[False]
+
+
 def test_generate_cli_recompute_mode_on_gpu(tmp_path):
     from helpers import make_tokenizer
 
