@@ -288,6 +288,8 @@ class EngineServicer:
             raise
         if h.finish_reason == "error":
             await ctx.abort(grpc.StatusCode.UNAVAILABLE, h.error or "engine failure")
+        if h.finish_reason == "deadline":  # the driver's copy of the call's deadline fired first: same status as above
+            await ctx.abort(grpc.StatusCode.DEADLINE_EXCEEDED, "generation deadline exceeded")
         m = h.metrics or {}
         return GenerateResponse(prompt=req.prompt, continuation=self.tok.decode(h.output_ids), request_id=req.request_id,
                                 token_ids=h.output_ids, finish_reason=h.finish_reason,
@@ -320,6 +322,8 @@ class EngineServicer:
             raise
         if h.finish_reason == "error":
             await ctx.abort(grpc.StatusCode.UNAVAILABLE, h.error or "engine failure")
+        if h.finish_reason == "deadline":  # the tokens so far were streamed; the call ends as its deadline says
+            await ctx.abort(grpc.StatusCode.DEADLINE_EXCEEDED, "generation deadline exceeded")
         yield Token(token_id=-1, text=dec.flush(), finished=True, finish_reason=h.finish_reason)
 
     async def Stats(self, req, ctx):

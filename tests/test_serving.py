@@ -631,3 +631,53 @@ def test_serving_bench_runs_on_cpu(mode):
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["requests"] == 6 and d["value"] > 0
     assert d["frontend"] == (None if "grpc" in mode else ("in-process" if "--frontend-inproc" in mode else "own process"))
+
+
+def test_servicer_reports_an_expired_server_deadline_as_deadline_exceeded():
+    """The driver holds a copy of the call's deadline; when that copy fires before the servicer's own wait, the
+    call still ends DEADLINE_EXCEEDED (unary and streaming), never OK with a silently truncated output."""
+    import asyncio
+    import types
+
+    from llmss_amd.serving.grpc_api import EngineServicer, GenerateRequest
+
+    class Aborted(Exception):
+        pass
+
+    class Ctx:
+        def time_remaining(self):
+            return 30.0
+
+        async def abort(self, code, msg):
+            raise Aborted(code)
+
+    class Drv:  # finishes every request at once as the driver's deadline check would: partial tokens, "deadline"
+        def submit(self, ids, params, deadline_s=None, on_done=None, sink=None, sink_q=None):
+            h = types.SimpleNamespace(rid=1, output_ids=[3, 4], finish_reason="deadline", error="deadline exceeded",
+                                      metrics={}, done=threading.Event())
+            h.done.set()
+            if sink_q is not None:
+                for t in (3, 4, None):
+                    sink_q.put_nowait(t)
+            if on_done is not None:
+                on_done(h)
+            return h
+
+        def abort(self, rid):
+            pass
+
+    tok = types.SimpleNamespace(decode=lambda ids: "", convert_ids_to_tokens=lambda ids: [])
+    sv = EngineServicer(Drv(), tok)
+    req = GenerateRequest(prompt_token_ids=[1, 2], max_new_tokens=50, is_greedy=True)
+
+    async def unary():
+        await sv.Generate(req, Ctx())
+
+    async def stream():
+        async for _ in sv.GenerateStream(req, Ctx()):
+            pass
+
+    for f in (unary, stream):
+        with pytest.raises(Aborted) as e:
+            asyncio.run(f())
+        assert e.value.args[0] == grpc.StatusCode.DEADLINE_EXCEEDED
