@@ -62,6 +62,11 @@ class Broker:
     def lrem(self, key: str, count: int, value: str) -> int:
         raise NotImplementedError
 
+    def expire(self, key: str, seconds: float) -> int:
+        """Delete ``key`` after ``seconds`` unless it empties (and so disappears) first, as Redis EXPIRE: reply
+        lists whose caller gave up are not kept forever. 1 if the key exists, else 0."""
+        raise NotImplementedError
+
     def lrange(self, key: str, start: int, stop: int) -> List[str]:
         raise NotImplementedError
 
@@ -72,7 +77,7 @@ class Broker:
         """Run ``cmds`` (tuples like ``("LPUSH", key, value)``) in order and return their replies; a command that
         fails yields its exception object in place of a reply, and the rest still run."""
         ops = {"LPUSH": self.lpush, "RPUSH": self.rpush, "RPOP": self.rpop, "LPOP": self.lpop, "LLEN": self.llen,
-               "RPOPLPUSH": self.rpoplpush, "LREM": self.lrem, "DEL": self.delete}
+               "RPOPLPUSH": self.rpoplpush, "LREM": self.lrem, "DEL": self.delete, "EXPIRE": self.expire}
         out = []
         for c in cmds:
             try:
@@ -97,9 +102,35 @@ class MemoryBroker(Broker):
         self._lists: Dict[str, deque] = {}
         self._lock = threading.Lock()
         self._waiters: Dict[str, list] = {}  # key -> [Condition on self._lock, number of waiting threads]
+        self._expiry: Dict[str, float] = {}  # key -> time.monotonic() deadline (EXPIRE)
+        self._swept = 0.0
+
+    def _live(self, key):  # lock held: the key's list, or None once it has expired (then deleted)
+        self._sweep()
+        t = self._expiry.get(key)
+        if t is not None and time.monotonic() >= t:
+            self._lists.pop(key, None)
+            del self._expiry[key]
+        return self._lists.get(key)
+
+    def _sweep(self):  # lock held: drop expired keys nobody touches any more, at most once a second
+        now = time.monotonic()
+        if now - self._swept >= 1.0:
+            self._swept = now
+            for k in [k for k, t in self._expiry.items() if now >= t]:
+                self._lists.pop(k, None)
+                del self._expiry[k]
+
+    def expire(self, key, seconds):
+        with self._lock:
+            self._sweep()
+            if self._live(key) is None:
+                return 0
+            self._expiry[key] = time.monotonic() + float(seconds)
+            return 1
 
     def _push(self, key, value, left):  # lock held
-        q = self._lists.get(key)
+        q = self._live(key)
         if q is None:
             q = self._lists[key] = deque()
         if left:
@@ -112,12 +143,13 @@ class MemoryBroker(Broker):
         return len(q)
 
     def _pop(self, key, right=True):  # lock held
-        q = self._lists.get(key)
+        q = self._live(key)
         if not q:
             return None
         v = q.pop() if right else q.popleft()
         if not q:
             del self._lists[key]
+            self._expiry.pop(key, None)
         return v
 
     def _wait(self, key, rem):  # lock held; False once the deadline has passed
@@ -166,7 +198,7 @@ class MemoryBroker(Broker):
 
     def llen(self, key):
         with self._lock:
-            return len(self._lists.get(key, ()))
+            return len(self._live(key) or ())
 
     def brpop(self, key, timeout=0):
         return self._blocking(key, timeout, lambda: self._pop(key))
@@ -176,6 +208,7 @@ class MemoryBroker(Broker):
 
     def delete(self, key):
         with self._lock:
+            self._expiry.pop(key, None)
             return 1 if self._lists.pop(key, None) is not None else 0
 
     def _move(self, src, dst):  # lock held
@@ -194,7 +227,7 @@ class MemoryBroker(Broker):
     def lrem(self, key, count, value):
         """Remove up to ``count`` occurrences of ``value`` (0 = all; < 0 = from the tail), like Redis."""
         with self._lock:
-            q = self._lists.get(key)
+            q = self._live(key)
             if not q:
                 return 0
             items = list(q)
@@ -209,11 +242,12 @@ class MemoryBroker(Broker):
                 self._lists[key] = rest
             else:
                 del self._lists[key]
+                self._expiry.pop(key, None)
             return len(drop)
 
     def lrange(self, key, start, stop):
         with self._lock:
-            items = list(self._lists.get(key, ()))
+            items = list(self._live(key) or ())
         n = len(items)
         start = max(0, start + n if start < 0 else start)
         stop = stop + n if stop < 0 else stop
@@ -354,6 +388,9 @@ class RedisBroker(Broker):
     def lrange(self, key, start, stop):
         return self.execute("LRANGE", key, int(start), int(stop)) or []
 
+    def expire(self, key, seconds):
+        return self.execute("EXPIRE", key, int(max(1, round(float(seconds)))))
+
     def close(self):
         c = getattr(self._local, "conn", None)
         if c is not None:
@@ -438,6 +475,8 @@ class MiniRedisServer:
 
         self._lists: Dict[str, deque] = {}
         self._waiters: Dict[str, deque] = {}  # key -> parked pops: (future, take) with take(key) -> value
+        self._expiry: Dict[str, float] = {}  # key -> time.monotonic() deadline (EXPIRE)
+        self._swept = 0.0
         self._sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         self._sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
         self._sock.bind((host, port))
@@ -449,8 +488,23 @@ class MiniRedisServer:
         self._conns: set = set()
 
     # list store (event-loop thread only)
+    def _live(self, key):  # the key's list, or None once it has expired (then deleted)
+        t = self._expiry.get(key)
+        if t is not None and time.monotonic() >= t:
+            self._lists.pop(key, None)
+            del self._expiry[key]
+        return self._lists.get(key)
+
+    def _sweep(self):  # expired keys nobody touches any more, at most once a second
+        now = time.monotonic()
+        if now - self._swept >= 1.0:
+            self._swept = now
+            for k in [k for k, t in self._expiry.items() if now >= t]:
+                self._lists.pop(k, None)
+                del self._expiry[k]
+
     def _push(self, key, value, left):
-        q = self._lists.get(key)
+        q = self._live(key)
         if q is None:
             q = self._lists[key] = deque()
         q.appendleft(value) if left else q.append(value)
@@ -459,12 +513,13 @@ class MiniRedisServer:
         return n
 
     def _pop(self, key, right=True):
-        q = self._lists.get(key)
+        q = self._live(key)
         if not q:
             return None
         v = q.pop() if right else q.popleft()
         if not q:
             del self._lists[key]
+            self._expiry.pop(key, None)
         return v
 
     def _serve_waiters(self, key):
@@ -480,7 +535,7 @@ class MiniRedisServer:
         import asyncio
 
         for k in keys:
-            if self._lists.get(k):
+            if self._live(k):
                 return k, take(k)
         fut = self.loop.create_future()
         for k in keys:
@@ -506,7 +561,7 @@ class MiniRedisServer:
         return v
 
     def _lrem(self, key, count, value):
-        q = self._lists.get(key)
+        q = self._live(key)
         if not q:
             return 0
         items = list(q)
@@ -518,10 +573,11 @@ class MiniRedisServer:
             self._lists[key] = rest
         else:
             del self._lists[key]
+            self._expiry.pop(key, None)
         return len(drop)
 
     def _lrange(self, key, start, stop):
-        items = list(self._lists.get(key, ()))
+        items = list(self._live(key) or ())
         n = len(items)
         start = max(0, start + n if start < 0 else start)
         stop = stop + n if stop < 0 else stop
@@ -532,6 +588,7 @@ class MiniRedisServer:
             raise RuntimeError("ERR protocol")
         op = cmd[0].upper()
         a = cmd[1:]
+        self._sweep()
         if op == "PING":
             return "PONG"
         if op in ("LPUSH", "RPUSH"):
@@ -542,7 +599,7 @@ class MiniRedisServer:
         if op in ("RPOP", "LPOP"):
             return ("bulk", self._pop(a[0], op == "RPOP"))
         if op == "LLEN":
-            return len(self._lists.get(a[0], ()))
+            return len(self._live(a[0]) or ())
         if op in ("BRPOP", "BLPOP"):
             r = await self._blocking(a[:-1], float(a[-1]), lambda k: self._pop(k, op == "BRPOP"))
             return ("array", None if r is None else [r[0], r[1]])
@@ -552,7 +609,14 @@ class MiniRedisServer:
         if op == "RPOPLPUSH":
             return ("bulk", self._move(a[0], a[1]))
         if op == "DEL":
+            for k in a:
+                self._expiry.pop(k, None)
             return sum(1 for k in a if self._lists.pop(k, None) is not None)
+        if op == "EXPIRE":
+            if self._live(a[0]) is None:
+                return 0
+            self._expiry[a[0]] = time.monotonic() + float(a[1])
+            return 1
         if op == "LREM":
             return self._lrem(a[0], int(a[1]), a[2])
         if op == "LRANGE":

@@ -44,7 +44,7 @@ def processing_key(consumer_id: str) -> str:
 
 class Consumer:
     def __init__(self, driver: EngineDriver, tokenizer, broker: Optional[Broker] = None, poll_timeout: float = 1.0,
-                 consumer_id: str = "0", durable: bool = True, intake_batch: int = 32):
+                 consumer_id: str = "0", durable: bool = True, intake_batch: int = 32, reply_ttl_s: float = 300.0):
         self.driver = driver
         self.tok = tokenizer
         self.broker = broker
@@ -52,6 +52,9 @@ class Consumer:
         self.consumer_id = str(consumer_id)
         self.durable = durable
         self.intake_batch = max(1, int(intake_batch))
+        # every reply list gets this TTL (EXPIRE): the reply of a caller that gave up (deadline, cancelled call,
+        # front-end restart) is deleted by the broker instead of being kept forever
+        self.reply_ttl_s = reply_ttl_s
         self._stop = threading.Event()
         self._out: "queue.Queue" = queue.Queue()
         self.served = 0
@@ -108,6 +111,9 @@ class Consumer:
                     log.exception("consumer publish: could not format a reply")
             try:
                 flush()
+                if self.reply_ttl_s:
+                    keys = dict.fromkeys(c[1] for c in cmds if c[0] == "LPUSH")  # reply lists, in order, once each
+                    cmds += [("EXPIRE", k, int(max(1, round(self.reply_ttl_s)))) for k in keys]
                 for r in self.broker.pipeline(cmds):
                     if isinstance(r, Exception):
                         log.error("consumer publish: broker error %s", r)
@@ -232,7 +238,7 @@ class Consumer:
             def on_token(h, t, req=req):
                 self._out.put(("tokens", req, [int(t)]))
         self.driver.submit(ids, params, on_done=lambda h, req=req, raw=raw: self._out.put(("done", req, h, raw)),
-                           on_token=on_token)
+                           on_token=on_token, deadline_s=req.deadline_s)
 
     def start(self):
         if self.driver.leader:

@@ -343,24 +343,25 @@ class BrokerServicer:
         self.stats = {"requests": 0, "timeouts": 0}
 
     @staticmethod
-    def _body(req, rid, stream=False):
+    def _body(req, rid, stream=False, deadline_s=None):
         from .protocol import Request
 
+        # deadline_s: the call's remaining time, so the consumer stops generating when nobody waits any more
         return Request(prompt=req.prompt, max_new_tokens=req.max_new_tokens or 20, is_greedy=req.is_greedy,
                        temperature=req.temperature or 1.0, top_p=req.top_p or 0.95, top_k=req.top_k or 50,
                        request_id=rid, seed=req.seed or None, ignore_eos=req.ignore_eos, stream=stream,
-                       prompt_token_ids=list(req.prompt_token_ids) or None)
+                       prompt_token_ids=list(req.prompt_token_ids) or None, deadline_s=deadline_s)
 
     def Generate(self, req, ctx):
         from .broker import PQUEUE, reply_key
         from .protocol import new_request_id
 
         rid = req.request_id or new_request_id()
-        body = self._body(req, rid)
+        remaining = ctx.time_remaining()
+        body = self._body(req, rid, deadline_s=remaining)
         t0 = time.perf_counter()
         self.broker.lpush(PQUEUE, body.model_dump_json(exclude_none=True))
         self.stats["requests"] += 1
-        remaining = ctx.time_remaining()
         msg = self.broker.brpop(reply_key(rid), timeout=remaining if remaining else self.timeout)
         if msg is None:
             self.stats["timeouts"] += 1
@@ -378,9 +379,10 @@ class BrokerServicer:
         from .protocol import new_request_id
 
         rid = req.request_id or new_request_id()
-        self.broker.lpush(PQUEUE, self._body(req, rid, stream=True).model_dump_json(exclude_none=True))
-        self.stats["requests"] += 1
         remaining = ctx.time_remaining()
+        self.broker.lpush(PQUEUE, self._body(req, rid, stream=True, deadline_s=remaining).model_dump_json(
+            exclude_none=True))
+        self.stats["requests"] += 1
         deadline = time.monotonic() + (remaining if remaining else self.timeout)
         while True:
             msg = self.broker.brpop(reply_key(rid), timeout=max(0.001, deadline - time.monotonic()))
@@ -420,9 +422,9 @@ class AioBrokerServicer(BrokerServicer):
 
         rid = req.request_id or new_request_id()
         t0 = time.perf_counter()
-        await self.client.lpush(PQUEUE, self._body(req, rid).model_dump_json(exclude_none=True))
-        self.stats["requests"] += 1
         remaining = ctx.time_remaining()
+        await self.client.lpush(PQUEUE, self._body(req, rid, deadline_s=remaining).model_dump_json(exclude_none=True))
+        self.stats["requests"] += 1
         msg = await self.client.brpop(reply_key(rid), timeout=remaining if remaining else self.timeout)
         if msg is None:
             self.stats["timeouts"] += 1
@@ -437,9 +439,10 @@ class AioBrokerServicer(BrokerServicer):
         from .protocol import new_request_id
 
         rid = req.request_id or new_request_id()
-        await self.client.lpush(PQUEUE, self._body(req, rid, stream=True).model_dump_json(exclude_none=True))
-        self.stats["requests"] += 1
         remaining = ctx.time_remaining()
+        await self.client.lpush(PQUEUE, self._body(req, rid, stream=True, deadline_s=remaining).model_dump_json(
+            exclude_none=True))
+        self.stats["requests"] += 1
         deadline = time.monotonic() + (remaining if remaining else self.timeout)
         while True:
             msg = await self.client.brpop(reply_key(rid), timeout=max(0.001, deadline - time.monotonic()))

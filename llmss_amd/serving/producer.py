@@ -27,11 +27,13 @@ def create_app(broker: Broker, timeout_s: float = 600.0) -> FastAPI:
     @app.post("/generate")
     async def generate(request: Request) -> Response:
         rid = request.request_id or new_request_id()
-        req = request.model_copy(update={"request_id": rid})
+        # the consumer stops generating when this endpoint stops waiting for the reply
+        wait_s = min(timeout_s, request.deadline_s) if request.deadline_s else timeout_s
+        req = request.model_copy(update={"request_id": rid, "deadline_s": wait_s})
         t0 = time.perf_counter()
         stats["requests"] += 1
         await asyncio.to_thread(broker.lpush, PQUEUE, req.model_dump_json())
-        msg: Optional[str] = await asyncio.to_thread(broker.brpop, reply_key(rid), timeout_s)
+        msg: Optional[str] = await asyncio.to_thread(broker.brpop, reply_key(rid), wait_s)
         if msg is None:
             stats["timeouts"] += 1
             raise HTTPException(status_code=504, detail="generation timed out")

@@ -30,6 +30,7 @@ class Request(BaseModel):
     ignore_eos: bool = False
     stream: bool = False  # reply per engine step on squeue:<request_id>, then a final "finished" message
     prompt_token_ids: Optional[List[int]] = None  # pre-tokenized prompt (prompt text ignored)
+    deadline_s: Optional[float] = None  # seconds the caller waits for the reply: the consumer stops generating then
 
 
 class Response(BaseModel):

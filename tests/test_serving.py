@@ -681,3 +681,57 @@ def test_servicer_reports_an_expired_server_deadline_as_deadline_exceeded():
         with pytest.raises(Aborted) as e:
             asyncio.run(f())
         assert e.value.args[0] == grpc.StatusCode.DEADLINE_EXCEEDED
+
+
+@pytest.mark.parametrize("kind", ["memory", "resp"])
+def test_broker_expire(kind):
+    """EXPIRE as Redis: the key is gone after its TTL (lazily on access, and swept when nobody touches it again); a
+    list that empties loses its TTL with it; EXPIRE on a missing key is 0."""
+    srv = MiniRedisServer().start() if kind == "resp" else None
+    b = RedisBroker(srv.host, srv.port) if srv else MemoryBroker()
+    try:
+        assert b.expire("none", 1) == 0
+        b.lpush("a", "x")
+        b.lpush("b", "y")
+        b.lpush("c", "z")
+        assert b.expire("a", 1) == 1 and b.expire("b", 1) == 1
+        assert b.rpop("b") == "y"  # emptied: deleted, TTL gone with it
+        b.lpush("b", "y2")
+        time.sleep(1.3)
+        assert b.llen("a") == 0 and b.lrange("a", 0, -1) == []  # expired
+        assert b.lrange("b", 0, -1) == ["y2"] and b.llen("c") == 1  # no TTL / never had one
+        b.lpush("d", "w")
+        assert b.expire("d", 1) == 1
+        time.sleep(1.3)
+        b.llen("c")  # any command sweeps: "d" is dropped although nobody asks for it
+        store = srv._lists if srv else b._lists
+        assert "d" not in store and "a" not in store
+        assert b.pipeline([("LPUSH", "e", "v"), ("EXPIRE", "e", 5)]) == [1, 1]
+    finally:
+        if srv:
+            srv.stop()
+
+
+def test_consumer_expires_replies_and_honours_request_deadlines(driver):
+    """The pub/sub path bounds what an abandoned call costs: the request carries its caller's deadline (the engine
+    stops generating then) and every reply list gets a TTL (a reply nobody pops is deleted by the broker)."""
+    from llmss_amd.serving.broker import PQUEUE, reply_key
+
+    drv, tok, m = driver
+    b = MemoryBroker()
+    consumer = Consumer(drv, tok, b, poll_timeout=0.05, durable=False, reply_ttl_s=3).start()
+    try:
+        b.lpush(PQUEUE, json.dumps({"prompt": "y", "prompt_token_ids": [4, 5], "max_new_tokens": 2, "is_greedy": True,
+                                    "ignore_eos": True, "request_id": "gone"}))
+        t0 = time.time()
+        while b.llen(reply_key("gone")) == 0 and time.time() - t0 < 30:
+            time.sleep(0.02)
+        assert b.llen(reply_key("gone")) == 1  # answered, never popped ...
+        b.lpush(PQUEUE, json.dumps({"prompt": "x", "prompt_token_ids": [1, 2, 3], "max_new_tokens": 100000,
+                                    "is_greedy": True, "ignore_eos": True, "request_id": "late", "deadline_s": 0.0}))
+        late = json.loads(b.brpop(reply_key("late"), timeout=60))
+        assert late["finish_reason"] == "deadline" and late["output_tokens"] < 100000
+        time.sleep(max(0.0, t0 + 4.0 - time.time()))
+        assert b.llen(reply_key("gone")) == 0  # ... and expired
+    finally:
+        consumer.stop()
