@@ -5,7 +5,10 @@ every completed call returned exactly its max_new_tokens (ignore_eos); only the 
 the engine is idle with every KV block back in the pool and the driver healthy; and one greedy probe request, run
 alone before and after the load, returns the same tokens (nothing leaks from one request into another).
 
-usage: python bench/soak.py [--model gpt2-xl] [--seconds 120] [--clients 48]
+--pubsub: the same traffic through the pub/sub path instead (gRPC front-end -> embedded broker -> consumer ->
+engine); then also every broker list must be gone at the end (acknowledged, popped or expired by its TTL).
+
+usage: python bench/soak.py [--model gpt2-xl] [--seconds 120] [--clients 48] [--pubsub]
 """
 import argparse
 import collections
@@ -26,6 +29,7 @@ def main():
     ap.add_argument("--model", default="gpt2-xl")
     ap.add_argument("--seconds", type=float, default=120)
     ap.add_argument("--clients", type=int, default=48)
+    ap.add_argument("--pubsub", action="store_true")
     a = ap.parse_args()
 
     import grpc
@@ -41,7 +45,18 @@ def main():
     eng = LLMEngine(model, max_num_seqs=64, max_batched_tokens=8192, max_model_len=1024)
     free0 = eng.sched.num_free_blocks()
     drv = EngineDriver(eng).start()
-    server = serve(EngineServicer(drv, load_tokenizer(a.model, V)), port=0, host="127.0.0.1")
+    tok = load_tokenizer(a.model, V)
+    broker = consumer = None
+    if a.pubsub:
+        from llmss_amd.serving.broker import MiniRedisServer, RedisBroker
+        from llmss_amd.serving.consumer import Consumer
+        from llmss_amd.serving.grpc_api import AioBrokerServicer
+
+        broker = MiniRedisServer().start()
+        consumer = Consumer(drv, tok, RedisBroker(broker.host, broker.port), reply_ttl_s=5).start()
+        server = serve(AioBrokerServicer(broker.host, broker.port), port=0, host="127.0.0.1")
+    else:
+        server = serve(EngineServicer(drv, tok), port=0, host="127.0.0.1")
     ch = grpc.insecure_channel(f"127.0.0.1:{server.bound_port}")
     stub = Stub(ch)
     probe = GenerateRequest(prompt_token_ids=list(range(7, 57)), max_new_tokens=32, is_greedy=True, ignore_eos=True)
@@ -115,18 +130,25 @@ def main():
     while time.time() < deadline and (drv.handles or eng.sched.num_running() or eng.sched.num_waiting()):
         time.sleep(0.2)
     idle = not drv.handles and not eng.sched.num_running() and not eng.sched.num_waiting()
+    left_keys = None
+    if broker is not None:  # abandoned replies expire (TTL 5 s); acknowledged requests leave no processing entry
+        time.sleep(7)
+        left_keys = sorted(broker._lists)[:20]  # the consumer's polls keep the broker's once-a-second sweep running
     free1 = eng.sched.num_free_blocks()
     after = list(stub.Generate(probe, timeout=300).token_ids)
-    out = {"model": a.model, "seconds": round(time.time() - t0, 1), "clients": a.clients, "outcomes": dict(stats),
+    out = {"model": a.model, "path": "pubsub" if a.pubsub else "grpc", "seconds": round(time.time() - t0, 1), "clients": a.clients, "outcomes": dict(stats),
            "engine_tokens": eng.stats["tokens"], "engine_steps": eng.stats["steps"],
            "preemptions": eng.stats["preemptions"], "idle_at_end": idle, "free_blocks": [free0, free1],
            "probe_same": before == after, "driver_healthy": drv.error is None,
-           "engine_requests_left": len(eng.requests), "errors": bad}
-    ok = (idle and free1 == free0 and before == after and drv.error is None and not bad
+           "engine_requests_left": len(eng.requests), "broker_lists_left": left_keys, "errors": bad}
+    ok = (idle and free1 == free0 and not left_keys and before == after and drv.error is None and not bad
           and stats["unary_ok"] > 0 and stats["stream_ok"] > 0)
     out["pass"] = ok
     print(json.dumps(out), flush=True)
     server.stop(1).wait(30)
+    if consumer is not None:
+        consumer.stop()
+        broker.stop()
     drv.stop()
     sys.exit(0 if ok else 1)
 

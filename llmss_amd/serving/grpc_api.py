@@ -367,6 +367,8 @@ class BrokerServicer:
             self.stats["timeouts"] += 1
             ctx.abort(grpc.StatusCode.DEADLINE_EXCEEDED, "no reply from consumer")
         d = json.loads(msg)
+        if d.get("finish_reason") == "deadline":  # the consumer stopped at the deadline this call sent along
+            ctx.abort(grpc.StatusCode.DEADLINE_EXCEEDED, "generation deadline exceeded")
         return GenerateResponse(prompt=d.get("prompt", ""), continuation=d.get("continuation", ""), request_id=rid,
                                 token_ids=d.get("token_ids") or [], finish_reason=d.get("finish_reason", ""), ttft_s=float(d.get("ttft_s") or 0.0),
                                 e2e_s=float(time.perf_counter() - t0))
@@ -392,6 +394,8 @@ class BrokerServicer:
             d = json.loads(msg)
             if d.get("error"):
                 ctx.abort(grpc.StatusCode.UNAVAILABLE, d["error"])
+            if d.get("finished") and d.get("finish_reason") == "deadline":
+                ctx.abort(grpc.StatusCode.DEADLINE_EXCEEDED, "generation deadline exceeded")
             if d.get("finished"):
                 yield Token(token_id=-1, text=d.get("text", ""), finished=True, finish_reason=d.get("finish_reason", ""))
                 return
@@ -430,6 +434,8 @@ class AioBrokerServicer(BrokerServicer):
             self.stats["timeouts"] += 1
             await ctx.abort(grpc.StatusCode.DEADLINE_EXCEEDED, "no reply from consumer")
         d = json.loads(msg)
+        if d.get("finish_reason") == "deadline":  # the consumer stopped at the deadline this call sent along
+            await ctx.abort(grpc.StatusCode.DEADLINE_EXCEEDED, "generation deadline exceeded")
         return GenerateResponse(prompt=d.get("prompt", ""), continuation=d.get("continuation", ""), request_id=rid,
                                 token_ids=d.get("token_ids") or [], finish_reason=d.get("finish_reason", ""),
                                 ttft_s=float(d.get("ttft_s") or 0.0), e2e_s=float(time.perf_counter() - t0))
@@ -452,6 +458,8 @@ class AioBrokerServicer(BrokerServicer):
             d = json.loads(msg)
             if d.get("error"):
                 await ctx.abort(grpc.StatusCode.UNAVAILABLE, d["error"])
+            if d.get("finished") and d.get("finish_reason") == "deadline":
+                await ctx.abort(grpc.StatusCode.DEADLINE_EXCEEDED, "generation deadline exceeded")
             if d.get("finished"):
                 yield Token(token_id=-1, text=d.get("text", ""), finished=True, finish_reason=d.get("finish_reason", ""))
                 return
