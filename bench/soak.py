@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=120)
     ap.add_argument("--clients", type=int, default=48)
     ap.add_argument("--pubsub", action="store_true")
+    ap.add_argument("--device", default="cuda", help="cuda, or cpu for a dry run of the harness on a tiny preset")
     a = ap.parse_args()
 
     import grpc
@@ -39,8 +40,8 @@ def main():
     from llmss_amd.serving.grpc_api import EngineServicer, GenerateRequest, Stub, serve
     from llmss_amd.utils.tokenizer import load_tokenizer
 
-    dev = torch.device("cuda", 0)
-    model = build_model(a.model, None, "bf16", dev, random_init=True)
+    dev = torch.device("cuda", 0) if a.device == "cuda" else torch.device("cpu")
+    model = build_model(a.model, None, "bf16" if a.device == "cuda" else "fp32", dev, random_init=True)
     V = model.cfg.vocab_size
     eng = LLMEngine(model, max_num_seqs=64, max_batched_tokens=8192, max_model_len=1024)
     free0 = eng.sched.num_free_blocks()
