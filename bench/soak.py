@@ -146,6 +146,7 @@ def main():
           and stats["unary_ok"] > 0 and stats["stream_ok"] > 0)
     out["pass"] = ok
     print(json.dumps(out), flush=True)
+    ch.close()  # the client channel's core threads end before the interpreter does
     server.stop(1).wait(30)
     if consumer is not None:
         consumer.stop()
