@@ -22,6 +22,8 @@ def get_args(argv=None):
     # durable hand-off: in-flight requests sit in pqueue:processing:<id> until answered; a consumer restarted
     # with the same id re-queues what its previous incarnation left there
     consumer_group.add_argument("--consumer_id", type=str, default="0")
+    consumer_group.add_argument("--reply_ttl_s", type=float, default=300.0,
+                                help="TTL of every reply list (Redis EXPIRE): replies nobody pops are deleted")
     broker_group = parser.add_argument_group("broker")
     broker_group.add_argument("--redis_host", type=str, default="127.0.0.1")
     broker_group.add_argument("--redis_port", type=int, default=20000)
@@ -44,7 +46,8 @@ def main(argv=None):
     # --dp N with torchrun: world = N replicas x TP; every replica leader pulls from the same broker
     if driver.leader:
         print(f"{model.cfg.model_type} setup is done.", flush=True)
-        Consumer(driver, tok, RedisBroker(args.redis_host, args.redis_port), consumer_id=args.consumer_id).start()
+        Consumer(driver, tok, RedisBroker(args.redis_host, args.redis_port), consumer_id=args.consumer_id,
+                 reply_ttl_s=args.reply_ttl_s).start()
         if args.grpc_port:
             serve(EngineServicer(driver, tok), args.grpc_port)
     driver.run()  # blocks forever on every rank (leader: driver loop in this thread)
