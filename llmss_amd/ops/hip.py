@@ -253,11 +253,11 @@ class DecodeWorkspace:
     def get(self, B, nh, nsplit, D, device):
         need = B * nh * nsplit
         if (self.po is None or self.po.numel() < need * D or self.pml.numel() < need * 2
-                or self.po.device != device):
+                or self.po.device != _dev(device)):
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("decode workspace must be allocated before graph capture")
-            n_o = max(need * D, 0 if self.po is None else self.po.numel())
-            n_ml = max(need * 2, 0 if self.pml is None else self.pml.numel())
+            n_o = max(need * D, 0 if self.po is None else 2 * self.po.numel())  # geometric: few retired buffers
+            n_ml = max(need * 2, 0 if self.pml is None else 2 * self.pml.numel())
             _retire(self.po, self.pml)
             self.po = torch.empty(n_o, dtype=torch.float32, device=device)
             self.pml = torch.empty(n_ml, dtype=torch.float32, device=device)
@@ -285,6 +285,15 @@ _RETIRED: list = []
 
 def _retire(*ts):
     _RETIRED.extend(t for t in ts if t is not None)
+
+
+def _dev(device) -> torch.device:
+    """``device`` as tensors report it ("cuda" -> "cuda:<current>"): a scratch buffer is reused only on its own device,
+    and an unindexed name must not look like another device (every call would grow the buffer again)."""
+    d = torch.device(device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
 
 
 class workspace_slot:
@@ -351,7 +360,7 @@ class GemmWorkspace:
         self.buf = None
 
     def get(self, nbytes, device):
-        if self.buf is None or self.buf.numel() * 4 < nbytes or self.buf.device != device:
+        if self.buf is None or self.buf.numel() * 4 < nbytes or self.buf.device != _dev(device):
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("gemm workspace must be allocated before graph capture")
             _retire(self.buf)
@@ -411,11 +420,11 @@ class _QuantScratch:
         self.s = None
 
     def get(self, M, K, device):
-        if self.q is None or self.q.numel() < M * K or self.s.numel() < M or self.q.device != device:
+        if self.q is None or self.q.numel() < M * K or self.s.numel() < M or self.q.device != _dev(device):
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError(f"fp8 activation scratch for [{M}, {K}] must be allocated before graph capture")
-            nq = max(M * K, 0 if self.q is None else self.q.numel())
-            ns = max(M, 0 if self.s is None else self.s.numel())
+            nq = max(M * K, 0 if self.q is None else 2 * self.q.numel())  # geometric: few retired buffers
+            ns = max(M, 0 if self.s is None else 2 * self.s.numel())
             _retire(self.q, self.s)
             self.q = torch.empty(nq, dtype=torch.uint8, device=device)
             self.s = torch.empty(ns, dtype=torch.float32, device=device)
@@ -452,12 +461,13 @@ class _MxScratch:
         self.q = self.s = None
 
     def get(self, M, K, device):
-        if self.q is None or self.q.numel() < M * K or self.q.device != device:
+        if self.q is None or self.q.numel() < M * K or self.q.device != _dev(device):
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError(f"MX-fp8 activation scratch for [{M}, {K}] must be allocated before graph capture")
+            n = max(M * K, 0 if self.q is None else 2 * self.q.numel())  # geometric: few retired buffers
             _retire(self.q, self.s)
-            self.q = torch.empty(M * K, dtype=torch.uint8, device=device)
-            self.s = torch.empty(M * K // 32, dtype=torch.uint8, device=device)
+            self.q = torch.empty(n, dtype=torch.uint8, device=device)
+            self.s = torch.empty(n // 32, dtype=torch.uint8, device=device)
         return self.q[:M * K].view(M, K), self.s[:M * K // 32].view(M, K // 32)
 
 
@@ -554,12 +564,14 @@ class _PreQScratch:
         self.q = self.s = None
 
     def get(self, M, K, device):
-        if self.q is None or self.q.numel() < M * K or self.s.numel() < M or self.q.device != device:
+        if self.q is None or self.q.numel() < M * K or self.s.numel() < M or self.q.device != _dev(device):
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError(f"fp8 norm-output scratch for [{M}, {K}] must be allocated before graph capture")
             _retire(self.q, self.s)
-            self.q = torch.empty(max(M * K, 0 if self.q is None else self.q.numel()), dtype=torch.uint8, device=device)
-            self.s = torch.empty(max(M, 0 if self.s is None else self.s.numel()), dtype=torch.float32, device=device)
+            nq = max(M * K, 0 if self.q is None else 2 * self.q.numel())  # geometric: few retired buffers
+            ns = max(M, 0 if self.s is None else 2 * self.s.numel())
+            self.q = torch.empty(nq, dtype=torch.uint8, device=device)
+            self.s = torch.empty(ns, dtype=torch.float32, device=device)
         return self.q[:M * K].view(M, K), self.s[:M]
 
 

@@ -25,3 +25,14 @@ def test_outgrown_scratch_is_retired_not_freed(make, grow, monkeypatch):
     assert big[0].untyped_storage().data_ptr() != ptrs[0]  # it did grow
     kept = {t.untyped_storage().data_ptr() for t in H._RETIRED}
     assert all(p in kept for p in ptrs)
+
+
+def test_scratch_grows_geometrically(monkeypatch):
+    """Prompt batches of every size from 1 to 1000 rows retire at most ~log2(1000) buffers, not one per size."""
+    monkeypatch.setattr(H.torch.cuda, "is_current_stream_capturing", lambda: False)
+    w = H._QuantScratch()
+    n0 = len(H._RETIRED)
+    for M in range(1, 1001):
+        q, s = w.get(M, 64, "cpu")
+        assert q.shape == (M, 64) and s.shape == (M,)
+    assert len(H._RETIRED) - n0 <= 2 * 11
