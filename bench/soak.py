@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=120)
     ap.add_argument("--clients", type=int, default=48)
     ap.add_argument("--pubsub", action="store_true")
+    ap.add_argument("--fp8", action="store_true", help="fp8 (e4m3) weights: W8A8 / MX-fp8 GEMMs")
     ap.add_argument("--device", default="cuda", help="cuda, or cpu for a dry run of the harness on a tiny preset")
     a = ap.parse_args()
 
@@ -41,7 +42,7 @@ def main():
     from llmss_amd.utils.tokenizer import load_tokenizer
 
     dev = torch.device("cuda", 0) if a.device == "cuda" else torch.device("cpu")
-    model = build_model(a.model, None, "bf16" if a.device == "cuda" else "fp32", dev, random_init=True)
+    model = build_model(a.model, None, "bf16" if a.device == "cuda" else "fp32", dev, random_init=True, fp8=a.fp8)
     V = model.cfg.vocab_size
     eng = LLMEngine(model, max_num_seqs=64, max_batched_tokens=8192, max_model_len=1024)
     free0 = eng.sched.num_free_blocks()
@@ -137,7 +138,7 @@ def main():
         left_keys = sorted(broker._lists)[:20]  # the consumer's polls keep the broker's once-a-second sweep running
     free1 = eng.sched.num_free_blocks()
     after = list(stub.Generate(probe, timeout=300).token_ids)
-    out = {"model": a.model, "path": "pubsub" if a.pubsub else "grpc", "seconds": round(time.time() - t0, 1), "clients": a.clients, "outcomes": dict(stats),
+    out = {"model": a.model, "fp8": a.fp8, "path": "pubsub" if a.pubsub else "grpc", "seconds": round(time.time() - t0, 1), "clients": a.clients, "outcomes": dict(stats),
            "engine_tokens": eng.stats["tokens"], "engine_steps": eng.stats["steps"],
            "preemptions": eng.stats["preemptions"], "idle_at_end": idle, "free_blocks": [free0, free1],
            "probe_same": before == after, "driver_healthy": drv.error is None,
